@@ -1,0 +1,196 @@
+"""Benchmark: simplex pivots/s and HBM GB/s of the rank-1 tableau update on MI355X.
+
+Workload (BASELINE.json configs[2], the config the roofline target is quoted on):
+generateRandomProblem(n=8192, m=4096, seed=823296, [1,100]) -- the reference's own -t
+instance (main.cu:56-64) -- phase-1 tableau 4096 x 16385 fp64 (537 MB) resident in HBM.
+A "step" is one simplex pivot (entering argmin, ratio test, pivot-row fetch, rank-1
+update of the whole tableau).  W untimed pivots, then K timed pivots.
+
+N GPUs (torchrun, one process per GPU): the constraint rows are split into N contiguous
+512-aligned blocks; every pivot does one tile-winner allgather and one pivot-row
+allreduce over RCCL.  The problem is the same at every N ("strong" scaling).
+
+The CPU baseline is the serial C oracle (oracle/, a restatement of the reference's
+algorithm -- the reference has no CPU path) on the first pivots of the same instance,
+pinned to one core; the same pivots are re-run on the GPU and checked bit for bit.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (n, m, seed) -- seed n*100+m as main.cu:63, values in [+1,+100] (main.cu:64)
+    "config2": (2048, 1024, 205824),
+    "config3": (8192, 4096, 823296),
+    "config4": (4096, 16384, 425984),
+    "config5": (8192, 32768, 851968),
+}
+# oracle pivots timed for the CPU baseline (first 50 / 10 / 3 pivots)
+CPU_SAMPLE = {"config2": 200, "config3": 50, "config4": 10, "config5": 3}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# reference: RTX 2070 Super, config 3 phase 1, mean 7607.5 us per pivot
+REF_PIVOTS_PER_S = {"config3": 1e6 / 7607.5}
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(n, m, seed, pivots, sx):
+    """Time the serial oracle on the first `pivots` phase-1 pivots (one pinned core) and
+    check the GPU reproduces the same pivots bit for bit."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+
+    import oracle
+
+    A, b, c = oracle.generate(n, m, seed, 1, 100)
+    T, d, base = oracle.build_phase1(A, b)
+    oracle.update_objective(T, d, base)
+    T_gpu, d_gpu, base_gpu = T.copy(), d.copy(), base.copy()
+    old = os.sched_getaffinity(0)
+    core = min(old)
+    os.sched_setaffinity(0, {core})
+    try:
+        t0 = time.perf_counter()
+        st, done = oracle.solve(T, d, base, max_pivots=pivots)
+        dt = time.perf_counter() - t0
+    finally:
+        os.sched_setaffinity(0, old)
+    sx.dev_pivots(T_gpu, d_gpu, base_gpu, pivots)
+    same = (np.array_equal(T.view(np.uint64), T_gpu.view(np.uint64))
+            and np.array_equal(d.view(np.uint64), d_gpu.view(np.uint64))
+            and np.array_equal(base, base_gpu))
+    N1 = 1 + n + 2 * m
+    return {
+        "value": done / dt,
+        "unit": "pivots/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"first {done} phase-1 pivots of the same instance ({m}x{N1} fp64 tableau), serial C oracle",
+        "seconds": dt,
+        "update_GBps": 16.0 * (m + 1) * N1 * done / dt / 1e9,
+        "cpu_model": cpu_model(),
+        "core_used": core,
+        "host_cores_total": os.cpu_count(),
+        "gpu_bit_exact_on_sample": bool(same),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000, help="timed pivots")
+    ap.add_argument("--warmup", type=int, default=50, help="untimed pivots before timing")
+    ap.add_argument("--config", default="config3", choices=sorted(CONFIGS))
+    ap.add_argument("--update-rows", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-file", default=None, help="per-launch HBM bytes from rocprofv3 --pmc (JSON)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    import simplexoncuda_amd as sx
+    from simplexoncuda_amd import dist as sxdist
+
+    if world > 1:
+        sxdist.init_from_torch(local_rank)
+    else:
+        sx.load().simplex_set_device(local_rank)
+    sx.set_update_rows(args.update_rows)
+
+    n, m, seed = CONFIGS[args.config]
+    problem = sx.generateRandomProblem(n, m, seed, 1, 100)
+    sess = sx.Session(problem)
+    if args.warmup > 0:
+        sess.pivots(args.warmup)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tim = sess.pivots(args.steps, time_updates=True)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    pivots = tim.pivots
+    avg_update_s = tim.update_ms / 1e3 / max(tim.update_launches, 1)
+    achieved = tim.update_bytes / avg_update_s / 1e9
+    traffic = None
+    if args.pmc_file and os.path.exists(args.pmc_file):
+        with open(args.pmc_file) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    N1 = 1 + n + 2 * m
+    out = {
+        "metric": "simplex pivots/sec + HBM GB/s on gaussian update, dense m×n tableau",
+        "value": pivots / elapsed,
+        "unit": "pivots/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / max(pivots, 1),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": (pivots / elapsed) / REF_PIVOTS_PER_S[args.config] if args.config in REF_PIVOTS_PER_S else None,
+        "dtype": "f64",
+        "data": f"synthetic: generateRandomProblem(n={n}, m={m}, seed={seed}, [1,100]) (generator.cu/cuRAND-XORWOW restatement)",
+        "config": {
+            "workload": f"{args.config}: phase-1 pivots, {m}x{N1} fp64 tableau (m={m}, n={n})",
+            "m": m, "n": n, "seed": seed, "tableau_width": tim.width,
+            "rows_per_gpu_rank0": tim.local_rows, "parallelism": f"row-block x{world}",
+            "pivots_timed": pivots, "status_after": tim.status,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "kernel": "k_update (rank-1 pivot update, rank 0)",
+            "algorithmic_bytes_per_launch": tim.update_bytes,
+            "avg_launch_us": avg_update_s * 1e6,
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(n, m, seed, CPU_SAMPLE[args.config], sx)
+    sess.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        sxdist.finalize()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,88 @@
+/*
+ * simplex_hip.h -- MI355X engine extensions of the C-ABI (libsimplex_hip.so).
+ *
+ * Nothing here exists in the reference; it is what a benchmark, a parity test or a
+ * multi-GPU launcher needs on top of the drop-in entry points (twoPhaseMethod.h).
+ * Plain C types only.
+ */
+#ifndef SIMPLEX_HIP_H
+#define SIMPLEX_HIP_H
+
+#include "problem.h"
+#include "tabular.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SIMPLEX_NOT_ENDED -10    /* solver.cu:77 */
+#define SIMPLEX_PIVOT_CAP -11    /* opt-in pivot budget reached */
+#define SIMPLEX_NUMERIC_FAIL -12 /* eligible pivot but the ratio argmin found no row */
+
+/* ---- configuration ---- */
+int simplex_version(void);
+void simplex_set_verbose(int on);            /* reference progress lines on stdout */
+void simplex_set_update_rows(int rb);        /* rows per update workgroup: 4, 8 or 16 */
+void simplex_set_batch(int pivots);          /* pivots enqueued between status polls */
+void simplex_set_device(int device);
+
+/* ---- multi-GPU: one process per GPU, RCCL communicator over xGMI ---- */
+int simplex_dist_unique_id_size(void);
+int simplex_dist_get_unique_id(unsigned char *out); /* rank 0; out has unique_id_size bytes */
+int simplex_dist_init(int rank, int world, const unsigned char *unique_id, int device);
+int simplex_dist_finalize(void);
+/* single-process emulation of W row-block shards on the current device (collectives are
+ * device copies); used to test the sharded path on one GPU. 0 or 1 disables. */
+void simplex_set_virtual_ranks(int world);
+
+/* ---- extended drop-in entry ---- */
+/* twoPhaseMethod + final basis (base_out[m]) and per-phase pivot counts (pivots_out[2]);
+ * max_pivots < 0 = no cap (parity mode), else per-phase cap (status SIMPLEX_PIVOT_CAP). */
+int twoPhaseMethodEx(problem_t *problem, double *solution, double *optimalValue, int *base_out,
+                     long long *pivots_out, long long max_pivots);
+
+/* problem_t from caller arrays (copied; A column-major m x n); free with freeProblem()
+ * and then free() of the struct, as the reference's callers do. */
+problem_t *simplex_problem_from_arrays(int n, int m, const double *A_colmajor, const double *b,
+                                       const double *c);
+/* the generator with an explicit CRT flavour: 0 = MSVC rand() (default, matches the
+ * published pivot counts), 1 = glibc rand() */
+problem_t *simplex_generate_problem_ex(int n, int m, unsigned int seed, int lo, int hi, int rand_kind);
+void simplex_free_problem_struct(problem_t *problem);
+
+/* ---- benchmark session: a resident phase-1 tableau and timed pivots ---- */
+typedef struct {
+    double wall_ms;            /* device time of the whole call (events on the engine stream) */
+    double update_ms;          /* sum of rank-1 update kernel durations (events around each launch) */
+    long long pivots;          /* pivots applied during the call */
+    long long update_launches; /* update kernel launches timed */
+    int status;                /* phase status after the call (SIMPLEX_NOT_ENDED while running) */
+    int width;                 /* tableau width N of the phase */
+    long long local_rows;      /* constraint rows owned by this process */
+    double update_bytes;       /* algorithmic bytes per update launch: 16 * (local_rows + 1) * N */
+} simplex_timing_t;
+
+typedef struct simplex_session simplex_session;
+simplex_session *simplex_session_open(problem_t *problem); /* builds phase 1 + canonicalises d */
+int simplex_session_pivots(simplex_session *s, long long k, int time_updates, simplex_timing_t *out);
+double simplex_session_objective(simplex_session *s);   /* d[0] */
+long long simplex_session_total_pivots(simplex_session *s);
+void simplex_session_close(simplex_session *s);
+
+/* ---- kernel-level parity hooks (host arrays in/out, device compute) ---- */
+/* epsilon argmin of v[0..L) with the reference combine tree; returns index (or -1) */
+long long simplex_dev_argmin(const double *v, long long L, double *vmin);
+/* k full pivots on a caller tableau (row-major m x ld, width N) + d + base; returns the
+ * phase status after them (SIMPLEX_NOT_ENDED if still running); *done = pivots applied */
+int simplex_dev_pivots(double *T, long long m, long long N, long long ld, double *d, int *base, long long k,
+                       long long *done);
+/* objective canonicalisation d[j] -= sum_i T[i][j] * d[1+base[i]] on the device */
+int simplex_dev_update_objective(const double *T, long long m, long long N, long long ld, const int *base,
+                                 double *d);
+/* phase-1 tableau as built on the device (row-major m x ld, ld >= 1+n+2m), d and base */
+int simplex_dev_build_phase1(problem_t *problem, double *T, long long ld, double *d, int *base);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,13 @@
+"""simplexoncuda_amd -- MI355X-native dense two-phase simplex (drop-in for rik1599/SimplexOnCuda).
+
+The solver is libsimplex_hip.so: hand-written gfx950 HIP kernels behind the reference's C
+host API (include/problem.h, tabular.h, solver.h, twoPhaseMethod.h).  This package is the
+thin Python mirror of that API; see DESIGN.md.
+"""
+from .api import (  # noqa: F401
+    DEGENERATE, FEASIBLE, INFEASIBLE, NOT_ENDED, NUMERIC_FAIL, PIVOT_CAP, RAND_GLIBC, RAND_MSVC,
+    STATUS_NAMES, UNBOUNDED, Problem, Result, Session, dev_argmin, dev_build_phase1, dev_pivots,
+    dev_update_objective, generateRandomProblem, printProblemToStream, readProblemFromFile,
+    readRandomProblemFromFile, set_batch, set_update_rows, set_verbose, set_virtual_ranks,
+    twoPhaseMethod, twoPhaseMethodEx)
+from ._lib import LIB_PATH, load  # noqa: F401

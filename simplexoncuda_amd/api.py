@@ -1,0 +1,247 @@
+"""Python mirror of the reference host API, over the C-ABI of libsimplex_hip.so.
+
+Names, argument meaning and status codes follow the reference headers:
+  problem.h (readProblemFromFile, readRandomProblemFromFile, generateRandomProblem,
+  printProblemToStream, freeProblem), twoPhaseMethod.h (twoPhaseMethod, FEASIBLE ...).
+The compute always runs in the HIP library on the GPU; this module only marshals arrays.
+"""
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+
+FEASIBLE = 0
+INFEASIBLE = -1
+UNBOUNDED = -2
+DEGENERATE = -3
+NOT_ENDED = -10
+PIVOT_CAP = -11
+NUMERIC_FAIL = -12
+
+STATUS_NAMES = {FEASIBLE: "FEASIBLE", INFEASIBLE: "INFEASIBLE", UNBOUNDED: "UNBOUNDED",
+                DEGENERATE: "DEGENERATE", NOT_ENDED: "NOT_ENDED", PIVOT_CAP: "PIVOT_CAP",
+                NUMERIC_FAIL: "NUMERIC_FAIL"}
+
+RAND_MSVC = 0
+RAND_GLIBC = 1
+
+_libc = ctypes.CDLL(None)
+_libc.fopen.restype = ctypes.c_void_p
+_libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+_libc.fclose.argtypes = [ctypes.c_void_p]
+_libc.fflush.argtypes = [ctypes.c_void_p]
+
+
+def _dp(a):
+    return a.ctypes.data_as(_lib.c_double_p)
+
+
+def _ip(a):
+    return a.ctypes.data_as(_lib.c_int_p)
+
+
+class Problem:
+    """Owns a problem_t* allocated by the library (A column-major, problem.h:10-26)."""
+
+    def __init__(self, ptr):
+        if not ptr:
+            raise ValueError("null problem_t")
+        self._ptr = ptr
+
+    @property
+    def ptr(self):
+        return self._ptr
+
+    @property
+    def n(self):
+        return self._ptr.contents.vars
+
+    @property
+    def m(self):
+        return self._ptr.contents.constraints
+
+    def arrays(self):
+        """Copies of (A as an m x n array, b, c)."""
+        p = self._ptr.contents
+        n, m = p.vars, p.constraints
+        A_cm = np.ctypeslib.as_array(p.constraintsMatrix, shape=(n * m,)).copy() if n * m else np.zeros(0)
+        A = A_cm.reshape(n, m).T.copy() if n * m else np.zeros((m, n))
+        b = np.ctypeslib.as_array(p.knownTermsVector, shape=(m,)).copy() if m else np.zeros(0)
+        c = np.ctypeslib.as_array(p.objectiveFunction, shape=(n,)).copy() if n else np.zeros(0)
+        return A, b, c
+
+    @classmethod
+    def from_arrays(cls, A, b, c):
+        A = np.asarray(A, dtype=np.float64)
+        m, n = A.shape
+        A_cm = np.ascontiguousarray(A.T).reshape(-1)
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        c = np.ascontiguousarray(c, dtype=np.float64)
+        lib = _lib.load()
+        return cls(lib.simplex_problem_from_arrays(n, m, _dp(A_cm), _dp(b), _dp(c)))
+
+    def close(self):
+        if self._ptr:
+            _lib.load().simplex_free_problem_struct(self._ptr)
+            self._ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def generateRandomProblem(nVars, nConstraints, seed, minGenerator=-100, maxGenerator=100, rand_kind=RAND_MSVC):
+    """problem.cu:49-126 (defaults of problem.h:54)."""
+    lib = _lib.load()
+    return Problem(lib.simplex_generate_problem_ex(nVars, nConstraints, seed & 0xFFFFFFFF, minGenerator,
+                                                   maxGenerator, rand_kind))
+
+
+def _with_file(path, mode, fn):
+    f = _libc.fopen(str(path).encode(), mode.encode())
+    if not f:
+        raise OSError(f"Cannot open file! ({path})")
+    try:
+        return fn(f)
+    finally:
+        _libc.fclose(f)
+
+
+def readProblemFromFile(path):
+    """problem.cu:20-47."""
+    lib = _lib.load()
+    return Problem(_with_file(path, "r", lib.readProblemFromFile))
+
+
+def readRandomProblemFromFile(path):
+    """problem.cu:128-139 ("n m seed min max")."""
+    lib = _lib.load()
+    return Problem(_with_file(path, "r", lib.readRandomProblemFromFile))
+
+
+def printProblemToStream(problem, path):
+    """problem.cu:141-181, written to `path`."""
+    lib = _lib.load()
+    _with_file(path, "w", lambda f: lib.printProblemToStream(f, problem.ptr))
+
+
+@dataclass
+class Result:
+    status: int
+    solution: np.ndarray
+    optimal_value: float
+    base: np.ndarray
+    pivots: tuple
+
+    @property
+    def status_name(self):
+        return STATUS_NAMES.get(self.status, str(self.status))
+
+
+def twoPhaseMethod(problem):
+    """twoPhaseMethod.h:19 -> (status, solution, optimalValue)."""
+    lib = _lib.load()
+    x = np.zeros(max(problem.n, 1))
+    opt = ctypes.c_double(0.0)
+    st = lib.twoPhaseMethod(problem.ptr, _dp(x), ctypes.byref(opt))
+    return st, x[:problem.n], opt.value
+
+
+def twoPhaseMethodEx(problem, max_pivots=-1):
+    """twoPhaseMethod + final basis and per-phase pivot counts (simplex_hip.h)."""
+    lib = _lib.load()
+    x = np.zeros(max(problem.n, 1))
+    base = np.zeros(max(problem.m, 1), dtype=np.int32)
+    piv = (ctypes.c_longlong * 2)()
+    opt = ctypes.c_double(0.0)
+    st = lib.twoPhaseMethodEx(problem.ptr, _dp(x), ctypes.byref(opt), _ip(base), piv, max_pivots)
+    return Result(st, x[:problem.n], opt.value, base[:problem.m], (piv[0], piv[1]))
+
+
+class Session:
+    """A resident phase-1 tableau on this process's GPU shard, for timed pivots."""
+
+    def __init__(self, problem):
+        self._lib = _lib.load()
+        self._h = self._lib.simplex_session_open(problem.ptr)
+        if not self._h:
+            raise RuntimeError("simplex_session_open failed")
+
+    def pivots(self, k, time_updates=False):
+        t = _lib.TimingT()
+        self._lib.simplex_session_pivots(self._h, k, 1 if time_updates else 0, ctypes.byref(t))
+        return t
+
+    def objective(self):
+        return self._lib.simplex_session_objective(self._h)
+
+    def total_pivots(self):
+        return self._lib.simplex_session_total_pivots(self._h)
+
+    def close(self):
+        if self._h:
+            self._lib.simplex_session_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ---- kernel-level parity hooks ----
+def dev_argmin(v):
+    lib = _lib.load()
+    v = np.ascontiguousarray(v, dtype=np.float64)
+    vm = ctypes.c_double(0.0)
+    idx = lib.simplex_dev_argmin(_dp(v), len(v), ctypes.byref(vm))
+    return int(idx), vm.value
+
+
+def dev_pivots(T, d, base, k):
+    """k pivots on the device; T (m x ld, width len(d)), d, base updated in place."""
+    lib = _lib.load()
+    assert T.dtype == np.float64 and T.flags.c_contiguous and d.flags.c_contiguous
+    assert base.dtype == np.int32
+    m, ld = T.shape
+    done = ctypes.c_longlong(0)
+    st = lib.simplex_dev_pivots(_dp(T), m, len(d), ld, _dp(d), _ip(base), k, ctypes.byref(done))
+    return st, done.value
+
+
+def dev_update_objective(T, d, base):
+    lib = _lib.load()
+    m, ld = T.shape
+    return lib.simplex_dev_update_objective(_dp(T), m, len(d), ld, _ip(base), _dp(d))
+
+
+def dev_build_phase1(problem):
+    lib = _lib.load()
+    n, m = problem.n, problem.m
+    N1 = 1 + n + 2 * m
+    T = np.zeros((m, N1))
+    d = np.zeros(N1)
+    base = np.zeros(max(m, 1), dtype=np.int32)
+    lib.simplex_dev_build_phase1(problem.ptr, _dp(T), N1, _dp(d), _ip(base))
+    return T, d, base[:m]
+
+
+def set_virtual_ranks(w):
+    _lib.load().simplex_set_virtual_ranks(int(w))
+
+
+def set_verbose(on):
+    _lib.load().simplex_set_verbose(1 if on else 0)
+
+
+def set_update_rows(rb):
+    _lib.load().simplex_set_update_rows(int(rb))
+
+
+def set_batch(p):
+    _lib.load().simplex_set_batch(int(p))

@@ -1,0 +1,76 @@
+// sx_common.hpp -- shared host/device definitions of the MI355X simplex engine.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+// Status codes: twoPhaseMethod.h:5-8 (reference), solver.cu:77 (NOT_ENDED), plus two
+// engine-only codes that the reference has no equivalent for.
+#define SX_FEASIBLE 0
+#define SX_INFEASIBLE (-1)
+#define SX_UNBOUNDED (-2)
+#define SX_DEGENERATE (-3)
+#define SX_NOT_ENDED (-10)
+#define SX_PIVOT_CAP (-11)     // opt-in pivot budget reached (off in parity mode)
+#define SX_NUMERIC_FAIL (-12)  // ratio argmin returned no row although a pivot is eligible
+
+#define SX_TILE 512     // argmin tile = reference THREADS (reduction.cu:6)
+#define SX_EPS 1e-9     // macro.h:28
+
+// One 512-element argmin tile winner, plus "this tile has an entry >= eps" for the
+// unbounded test.  16 bytes: moved as raw bytes by the tile allgather.
+struct __attribute__((aligned(16))) TilePart {
+    double v;
+    int idx;
+    int elig;
+};
+
+// Per-shard pivot state, resident in device memory (never read by the host inside a
+// batch of pivots).
+struct __attribute__((aligned(16))) DevState {
+    int status;         // SX_NOT_ENDED while the phase runs
+    int e;              // entering variable (0-based variable index; column e+1)
+    int r;              // leaving constraint row (global index)
+    int pad0;
+    double dmin;        // reduced cost of the entering variable (d[e+1] before update)
+    long long pivots;   // pivots applied in this phase
+    long long max_pivots;  // < 0: no cap (reference behaviour)
+};
+
+// Error convention of the reference (error.cu:5-12): print "<msg> in <file> at line <n>"
+// and exit(EXIT_FAILURE).
+void sx_handle_error(hipError_t err, const char *file, int line);
+#define SX_HIP(call) sx_handle_error((call), __FILE__, __LINE__)
+void sx_fatal(const char *msg, const char *file, int line);
+#define SX_FATAL(msg) sx_fatal((msg), __FILE__, __LINE__)
+
+// ---- kernel launchers (sx_kernels.hip) ----
+struct LaunchCfg {
+    int update_rows;     // rows per update block (template RB)
+};
+
+void sx_launch_enter_partials(const double *d, int L, TilePart *out, const DevState *st, hipStream_t s);
+int sx_enter_blocks(int L);
+void sx_launch_ratio_partials(const double *T, int rows, int row0, size_t ld, const TilePart *enter_parts,
+                              int B1, TilePart *tiles_local, double *colE, DevState *st, hipStream_t s);
+void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, int N, const TilePart *tiles_all,
+                          int B2, double *prow_out, bool multi, int *base, DevState *st, hipStream_t s);
+void sx_launch_update(double *T, int rows, int row0, size_t ld, int N, double *d, const double *prow,
+                      const double *colE, const DevState *st, int rb, hipStream_t s);
+void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s);
+
+void sx_launch_coef(const double *d, const int *base, int row0, int rows, double *coef, hipStream_t s);
+void sx_launch_gemv_partials(const double *T, int rows, size_t ld, int N, const double *coef, double *partials,
+                             hipStream_t s);
+void sx_launch_gemv_apply(double *d, int N, const double *partials, int nblk, hipStream_t s);
+
+void sx_launch_build_rows(double *T, int rows, int row0, size_t ld, int n, int m, const double *A_local,
+                          const double *b_full, hipStream_t s);
+void sx_launch_init_vectors(double *d, int N1, int n, int m, int *base, hipStream_t s);
+void sx_launch_phase2_costs(double *d, int n, int m, const double *c, hipStream_t s);
+void sx_launch_gather_rhs(const double *T, int rows, size_t ld, double *out, hipStream_t s);
+void sx_launch_argmin_vector(const double *v, long long L, TilePart *parts, int *out_idx, double *out_v,
+                             hipStream_t s);

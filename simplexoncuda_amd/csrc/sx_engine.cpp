@@ -1,0 +1,721 @@
+// sx_engine.cpp -- host side of the MI355X simplex: shards, the device-resident pivot
+// loop, the two-phase driver and the C-ABI entry points of include/*.h.
+//
+// Reference call structure replaced: twoPhaseMethod (twoPhaseMethod.cu:385)
+// -> phase1/phase2 (:225, :285) -> solve (solver.cu:128) -> per-iteration solve (:78).
+// The reference crosses PCIe ~10 times per pivot (blocking copies, mallocs, syncs).  Here a
+// pivot is four kernels (plus, on several GPUs, two RCCL collectives) enqueued on one
+// stream; the host only polls a pinned status word once per batch of pivots.
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "../../include/simplex_hip.h"
+#include "../../include/twoPhaseMethod.h"
+#include "sx_common.hpp"
+
+// ------------------------------------------------------------------ errors (error.cu:5-18)
+void sx_handle_error(hipError_t err, const char *file, int line) {
+    if (err != hipSuccess) {
+        printf("%s in %s at line %d\n", hipGetErrorString(err), file, line);
+        fflush(stdout);
+        exit(EXIT_FAILURE);
+    }
+}
+
+void sx_fatal(const char *msg, const char *file, int line) {
+    printf("%s in %s at line %d\n", msg, file, line);
+    fflush(stdout);
+    exit(EXIT_FAILURE);
+}
+
+static void nccl_check(ncclResult_t r, const char *file, int line) {
+    if (r != ncclSuccess) {
+        printf("%s in %s at line %d\n", ncclGetErrorString(r), file, line);
+        fflush(stdout);
+        exit(EXIT_FAILURE);
+    }
+}
+#define SX_NCCL(call) nccl_check((call), __FILE__, __LINE__)
+
+// ------------------------------------------------------------------ global configuration
+namespace {
+
+struct Config {
+    int verbose = 0;
+    int update_rows = 8;
+    int batch = 16;
+    int device = -1;
+    int virtual_ranks = 1;
+    bool benchmark = false;
+    // distributed
+    bool dist = false;
+    int rank = 0;
+    int world = 1;
+    ncclComm_t comm = nullptr;
+};
+
+Config g_cfg;
+std::mutex g_mu;
+
+void say(const char *s) {
+    if (g_cfg.verbose) {
+        printf("%s\n", s);
+        fflush(stdout);
+    }
+}
+
+inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+template <typename T>
+T *dalloc(size_t count) {
+    T *p = nullptr;
+    if (count == 0) count = 1;
+    SX_HIP(hipMalloc(reinterpret_cast<void **>(&p), count * sizeof(T)));
+    return p;
+}
+
+// ------------------------------------------------------------------ shard + engine
+struct Shard {
+    int rank = 0;
+    int row0 = 0;
+    int rows = 0;
+    double *T = nullptr;
+    double *d = nullptr;
+    double *colE = nullptr;
+    double *prow = nullptr;
+    double *prow_send = nullptr;
+    double *coef = nullptr;
+    double *gemv_local = nullptr;
+    double *gemv_all = nullptr;
+    double *rhs_local = nullptr;
+    double *rhs_all = nullptr;
+    int *base = nullptr;
+    TilePart *enter_parts = nullptr;
+    TilePart *tiles_local = nullptr;
+    TilePart *tiles_all = nullptr;
+    DevState *st = nullptr;
+};
+
+class Engine {
+  public:
+    int n = 0, m = 0;
+    int W = 1;             // total shards (ranks)
+    bool rccl = false;     // true: one shard per process, collectives over RCCL
+    int N1 = 0, N2 = 0, N = 0;
+    size_t ld = 0;         // row stride in doubles
+    int rpr = 0;           // rows per rank (multiple of 512)
+    int slots = 0;         // argmin tiles / GEMV blocks per rank
+    int device = 0;
+    hipStream_t s = nullptr;
+    std::vector<Shard> sh;
+    const double **sum_srcs = nullptr;  // device array of prow_send pointers (virtual ranks)
+    DevState *st_host = nullptr;        // pinned: 2 poll slots
+    hipEvent_t poll_ev[2] = {nullptr, nullptr};
+    double *c_dev = nullptr;            // objective coefficients c (phase 2)
+    long long phase_pivots[2] = {0, 0};
+
+    Engine(int n_, int m_) : n(n_), m(m_) {
+        N1 = 1 + n + 2 * m;
+        N2 = 1 + n + m;
+        N = N1;
+        ld = round_up((size_t)N1, 16);
+        if (g_cfg.dist && g_cfg.world > 1) {
+            rccl = true;
+            W = g_cfg.world;
+        } else if (g_cfg.virtual_ranks > 1) {
+            W = g_cfg.virtual_ranks;
+        }
+        int dev = 0;
+        if (g_cfg.device >= 0) SX_HIP(hipSetDevice(g_cfg.device));
+        SX_HIP(hipGetDevice(&dev));
+        device = dev;
+        SX_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        rpr = (int)round_up((size_t)((m + W - 1) / W), SX_TILE);
+        if (rpr == 0) rpr = SX_TILE;
+        slots = rpr / SX_TILE;
+        if ((long long)W * slots > SX_TILE) SX_FATAL("too many constraint tiles for the exact argmin tree");
+        std::vector<int> ranks;
+        if (rccl)
+            ranks.push_back(g_cfg.rank);
+        else
+            for (int k = 0; k < W; ++k) ranks.push_back(k);
+        for (int k : ranks) {
+            Shard x;
+            x.rank = k;
+            x.row0 = k * rpr;
+            x.rows = m - x.row0;
+            if (x.rows < 0) x.rows = 0;
+            if (x.rows > rpr) x.rows = rpr;
+            alloc_shard(x);
+            sh.push_back(x);
+        }
+        if (!rccl && W > 1) {
+            std::vector<const double *> ptrs;
+            for (auto &x : sh) ptrs.push_back(x.prow_send);
+            sum_srcs = dalloc<const double *>(W);
+            SX_HIP(hipMemcpy(sum_srcs, ptrs.data(), sizeof(double *) * W, hipMemcpyHostToDevice));
+        }
+        SX_HIP(hipHostMalloc(reinterpret_cast<void **>(&st_host), 2 * sizeof(DevState), hipHostMallocDefault));
+        for (auto &e : poll_ev) SX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+
+    ~Engine() {
+        (void)hipStreamSynchronize(s);
+        for (auto &x : sh) free_shard(x);
+        if (sum_srcs) (void)hipFree(sum_srcs);
+        if (c_dev) (void)hipFree(c_dev);
+        if (st_host) (void)hipHostFree(st_host);
+        for (auto &e : poll_ev)
+            if (e) (void)hipEventDestroy(e);
+        (void)hipStreamDestroy(s);
+    }
+
+    void alloc_shard(Shard &x) {
+        const size_t rows_alloc = x.rows > 0 ? (size_t)x.rows : 1;
+        x.T = dalloc<double>(rows_alloc * ld);
+        x.d = dalloc<double>(ld);
+        x.colE = dalloc<double>(rows_alloc);
+        x.prow = dalloc<double>(ld);
+        if (W > 1) x.prow_send = dalloc<double>(ld);
+        x.coef = dalloc<double>(rows_alloc);
+        x.rhs_local = dalloc<double>(rpr);
+        if (W > 1) x.rhs_all = dalloc<double>((size_t)W * rpr);
+        x.base = dalloc<int>(m);
+        x.enter_parts = dalloc<TilePart>(SX_TILE);
+        x.tiles_local = dalloc<TilePart>(slots);
+        if (W > 1) x.tiles_all = dalloc<TilePart>((size_t)W * slots);
+        x.st = dalloc<DevState>(1);
+        SX_HIP(hipMemsetAsync(x.T, 0, rows_alloc * ld * sizeof(double), s));
+        SX_HIP(hipMemsetAsync(x.d, 0, ld * sizeof(double), s));
+        SX_HIP(hipMemsetAsync(x.prow, 0, ld * sizeof(double), s));
+        // padding tile entries must read (DBL_MAX, -1, not eligible)
+        std::vector<TilePart> pad((size_t)W * slots);
+        for (auto &t : pad) {
+            t.v = 1.7976931348623157e308;
+            t.idx = -1;
+            t.elig = 0;
+        }
+        SX_HIP(hipMemcpy(x.tiles_local, pad.data(), sizeof(TilePart) * slots, hipMemcpyHostToDevice));
+        if (W > 1)
+            SX_HIP(hipMemcpy(x.tiles_all, pad.data(), sizeof(TilePart) * pad.size(), hipMemcpyHostToDevice));
+    }
+
+    void free_shard(Shard &x) {
+        for (void *p : {(void *)x.T, (void *)x.d, (void *)x.colE, (void *)x.prow, (void *)x.prow_send,
+                        (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
+                        (void *)x.rhs_all, (void *)x.base, (void *)x.enter_parts, (void *)x.tiles_local,
+                        (void *)x.tiles_all, (void *)x.st})
+            if (p) (void)hipFree(p);
+    }
+
+    // ---------------------------------------------------------------- phase-1 tableau
+    // fillTableu (twoPhaseMethod.cu:145-200): each shard copies only its rows of A.
+    void build_phase1(const problem_t *P) {
+        double *b_dev = dalloc<double>(m);
+        SX_HIP(hipMemcpyAsync(b_dev, P->knownTermsVector, sizeof(double) * m, hipMemcpyHostToDevice, s));
+        for (auto &x : sh) {
+            double *A_local = nullptr;
+            if (x.rows > 0 && n > 0) {
+                A_local = dalloc<double>((size_t)x.rows * n);
+                SX_HIP(hipMemcpy2DAsync(A_local, sizeof(double) * x.rows, P->constraintsMatrix + x.row0,
+                                        sizeof(double) * m, sizeof(double) * x.rows, n, hipMemcpyHostToDevice, s));
+            }
+            sx_launch_build_rows(x.T, x.rows, x.row0, ld, n, m, A_local, b_dev, s);
+            sx_launch_init_vectors(x.d, N1, n, m, x.base, s);
+            SX_HIP(hipStreamSynchronize(s));
+            if (A_local) (void)hipFree(A_local);
+        }
+        (void)hipFree(b_dev);
+        if (!c_dev) {
+            c_dev = dalloc<double>(n);
+            if (n > 0)
+                SX_HIP(hipMemcpy(c_dev, P->objectiveFunction, sizeof(double) * n, hipMemcpyHostToDevice));
+        }
+    }
+
+    // ---------------------------------------------------------------- collectives
+    void allgather_tiles() {
+        if (rccl) {
+            Shard &x = sh[0];
+            SX_NCCL(ncclAllGather(x.tiles_local, x.tiles_all, sizeof(TilePart) * slots, ncclUint8, g_cfg.comm, s));
+            return;
+        }
+        for (auto &dst : sh)
+            for (auto &src : sh)
+                SX_HIP(hipMemcpyAsync(dst.tiles_all + (size_t)src.rank * slots, src.tiles_local,
+                                      sizeof(TilePart) * slots, hipMemcpyDeviceToDevice, s));
+    }
+
+    void allreduce_prow() {
+        if (rccl) {
+            Shard &x = sh[0];
+            SX_NCCL(ncclAllReduce(x.prow_send, x.prow, N, ncclDouble, ncclSum, g_cfg.comm, s));
+            return;
+        }
+        for (auto &dst : sh) sx_launch_sum_rows(dst.prow, sum_srcs, W, N, s);
+    }
+
+    void allgather_doubles(double *Shard::*local, double *Shard::*all, size_t count) {
+        if (rccl) {
+            Shard &x = sh[0];
+            SX_NCCL(ncclAllGather(x.*local, x.*all, count, ncclDouble, g_cfg.comm, s));
+            return;
+        }
+        for (auto &dst : sh)
+            for (auto &src : sh)
+                SX_HIP(hipMemcpyAsync(dst.*all + (size_t)src.rank * count, src.*local, sizeof(double) * count,
+                                      hipMemcpyDeviceToDevice, s));
+    }
+
+    // ---------------------------------------------------------------- objective GEMV
+    // updateObjectiveFunction (gaussian.cu:132-162), deterministic blocked order.
+    void update_objective(int width) {
+        const size_t part = (size_t)slots * width;
+        for (auto &x : sh) {
+            if (!x.gemv_local) x.gemv_local = dalloc<double>((size_t)slots * N1);
+            if (W > 1 && !x.gemv_all) x.gemv_all = dalloc<double>((size_t)W * slots * N1);
+            SX_HIP(hipMemsetAsync(x.gemv_local, 0, part * sizeof(double), s));
+            sx_launch_coef(x.d, x.base, x.row0, x.rows, x.coef, s);
+            sx_launch_gemv_partials(x.T, x.rows, ld, width, x.coef, x.gemv_local, s);
+        }
+        if (W > 1) allgather_doubles(&Shard::gemv_local, &Shard::gemv_all, part);
+        const int nblk = (m + SX_TILE - 1) / SX_TILE;
+        for (auto &x : sh) sx_launch_gemv_apply(x.d, width, W > 1 ? x.gemv_all : x.gemv_local, nblk, s);
+    }
+
+    void phase2_costs() {
+        for (auto &x : sh) sx_launch_phase2_costs(x.d, n, m, c_dev, s);
+    }
+
+    // ---------------------------------------------------------------- one pivot
+    void enqueue_pivot(hipEvent_t ev0, hipEvent_t ev1) {
+        const int L = N - 1;
+        const int B1 = sx_enter_blocks(L);
+        for (auto &x : sh) {
+            sx_launch_enter_partials(x.d, L, x.enter_parts, x.st, s);
+            sx_launch_ratio_partials(x.T, x.rows, x.row0, ld, x.enter_parts, B1, x.tiles_local, x.colE, x.st, s);
+        }
+        if (W > 1) allgather_tiles();
+        const int B2 = W * slots;
+        for (auto &x : sh)
+            sx_launch_select_row(x.T, x.rows, x.row0, ld, N, W > 1 ? x.tiles_all : x.tiles_local, B2,
+                                 W > 1 ? x.prow_send : x.prow, W > 1, x.base, x.st, s);
+        if (W > 1) allreduce_prow();
+        if (ev0) SX_HIP(hipEventRecord(ev0, s));
+        for (auto &x : sh)
+            sx_launch_update(x.T, x.rows, x.row0, ld, N, x.d, x.prow, x.colE, x.st, g_cfg.update_rows, s);
+        if (ev1) SX_HIP(hipEventRecord(ev1, s));
+    }
+
+    void reset_state(long long max_pivots) {
+        DevState init;
+        std::memset(&init, 0, sizeof(init));
+        init.status = SX_NOT_ENDED;
+        init.e = -1;
+        init.r = -1;
+        init.max_pivots = max_pivots;
+        for (auto &x : sh) SX_HIP(hipMemcpyAsync(x.st, &init, sizeof(init), hipMemcpyHostToDevice, s));
+        SX_HIP(hipStreamSynchronize(s));
+    }
+
+    DevState read_state() {
+        DevState out;
+        SX_HIP(hipMemcpyAsync(&out, sh[0].st, sizeof(out), hipMemcpyDeviceToHost, s));
+        SX_HIP(hipStreamSynchronize(s));
+        return out;
+    }
+
+    // solve (solver.cu:128-149): pivots until the phase ends.  Batches of pivots are
+    // enqueued back to back; the host polls the status of the batch before the last one,
+    // so the device never waits on the host.  Kernels of a finished phase return at once.
+    int run_phase(int width, long long max_pivots, long long *pivots) {
+        N = width;
+        reset_state(max_pivots);
+        const int batch = g_cfg.batch > 0 ? g_cfg.batch : 16;
+        long long k = 0;
+        for (;; ++k) {
+            for (int b = 0; b < batch; ++b) enqueue_pivot(nullptr, nullptr);
+            const int slot = (int)(k & 1);
+            SX_HIP(hipMemcpyAsync(st_host + slot, sh[0].st, sizeof(DevState), hipMemcpyDeviceToHost, s));
+            SX_HIP(hipEventRecord(poll_ev[slot], s));
+            if (k >= 1) {
+                SX_HIP(hipEventSynchronize(poll_ev[slot ^ 1]));
+                if (st_host[slot ^ 1].status != SX_NOT_ENDED) break;
+            }
+        }
+        DevState f = read_state();
+        if (pivots) *pivots = f.pivots;
+        return f.status;
+    }
+
+    double read_d0() {
+        double v = 0.0;
+        SX_HIP(hipMemcpyAsync(&v, sh[0].d, sizeof(double), hipMemcpyDeviceToHost, s));
+        SX_HIP(hipStreamSynchronize(s));
+        return v;
+    }
+
+    void read_base(int *out) {
+        SX_HIP(hipMemcpyAsync(out, sh[0].base, sizeof(int) * m, hipMemcpyDeviceToHost, s));
+        SX_HIP(hipStreamSynchronize(s));
+    }
+
+    void write_base(const int *in) {
+        for (auto &x : sh) SX_HIP(hipMemcpyAsync(x.base, in, sizeof(int) * m, hipMemcpyHostToDevice, s));
+        SX_HIP(hipStreamSynchronize(s));
+    }
+
+    // RHS column of all rows (for the solution, getSolution twoPhaseMethod.cu:116-128)
+    void read_rhs(std::vector<double> &out) {
+        out.assign(m, 0.0);
+        for (auto &x : sh) sx_launch_gather_rhs(x.T, x.rows, ld, x.rhs_local, s);
+        if (W > 1) {
+            allgather_doubles(&Shard::rhs_local, &Shard::rhs_all, rpr);
+            SX_HIP(hipMemcpyAsync(out.data(), sh[0].rhs_all, sizeof(double) * m, hipMemcpyDeviceToHost, s));
+        } else {
+            SX_HIP(hipMemcpyAsync(out.data(), sh[0].rhs_local, sizeof(double) * m, hipMemcpyDeviceToHost, s));
+        }
+        SX_HIP(hipStreamSynchronize(s));
+    }
+
+    // rows of the whole tableau (virtual or single shard only): for tests and printing
+    void download(double *T_host, size_t ld_host, int width, double *d_host) {
+        for (auto &x : sh)
+            if (x.rows > 0)
+                SX_HIP(hipMemcpy2DAsync(T_host + (size_t)x.row0 * ld_host, ld_host * sizeof(double), x.T,
+                                        ld * sizeof(double), width * sizeof(double), x.rows,
+                                        hipMemcpyDeviceToHost, s));
+        if (d_host) SX_HIP(hipMemcpyAsync(d_host, sh[0].d, sizeof(double) * width, hipMemcpyDeviceToHost, s));
+        SX_HIP(hipStreamSynchronize(s));
+    }
+
+    void upload(const double *T_host, size_t ld_host, int width, const double *d_host, const int *base_host) {
+        for (auto &x : sh) {
+            if (x.rows > 0)
+                SX_HIP(hipMemcpy2DAsync(x.T, ld * sizeof(double), T_host + (size_t)x.row0 * ld_host,
+                                        ld_host * sizeof(double), width * sizeof(double), x.rows,
+                                        hipMemcpyHostToDevice, s));
+            if (d_host) SX_HIP(hipMemcpyAsync(x.d, d_host, sizeof(double) * width, hipMemcpyHostToDevice, s));
+            if (base_host) SX_HIP(hipMemcpyAsync(x.base, base_host, sizeof(int) * m, hipMemcpyHostToDevice, s));
+        }
+        SX_HIP(hipStreamSynchronize(s));
+    }
+};
+
+// tabular_t <-> engine
+std::map<const tabular_t *, Engine *> g_tabs;
+
+// ------------------------------------------------------------------ the two-phase driver
+int two_phase(problem_t *P, double *solution, double *opt, int *base_out, long long *pivots_out,
+              long long max_pivots) {
+    const int n = P->vars, m = P->constraints;
+    Engine E(n, m);
+    long long p1 = 0, p2 = 0;
+    int status;
+    // phase1 (twoPhaseMethod.cu:225-283)
+    say("Phase 1: Filling Tableau");
+    E.build_phase1(P);
+    say("Phase 1: Resetting out-of-base variables");
+    E.update_objective(E.N1);
+    say("Phase 1: Solving auxiliary problem");
+    const int st1 = E.run_phase(E.N1, max_pivots, &p1);  // return value ignored by the reference (:258)
+    const double d0 = E.read_d0();
+    std::vector<int> base(m);
+    E.read_base(base.data());
+    if (st1 == SX_PIVOT_CAP) {
+        status = SX_PIVOT_CAP;
+    } else if (st1 == SX_NUMERIC_FAIL) {
+        status = SX_NUMERIC_FAIL;
+    } else if (compare(d0) < 0) {
+        status = INFEASIBLE;  // :265-268
+    } else {
+        status = FEASIBLE;  // checkDegeneracy (:206-223)
+        for (int i = 0; i < m; ++i)
+            if (base[i] >= n + m && base[i] < n + 2 * m) status = DEGENERATE;
+    }
+    if (status == FEASIBLE) {
+        // phase2 (:285-356): drop the artificial columns, costs -c / 0, d[0] kept
+        say("Phase 2: Filling costs vector with the original one");
+        E.phase2_costs();
+        say("Phase 2: Resetting out-of-base variables");
+        E.update_objective(E.N2);
+        say("Phase 2: Solving original problem");
+        status = E.run_phase(E.N2, max_pivots, &p2);
+        E.read_base(base.data());
+        if (status == FEASIBLE) {
+            // getSolutionHost (:370-383)
+            const double z = E.read_d0();
+            std::vector<double> rhs;
+            E.read_rhs(rhs);
+            if (opt) *opt = z;
+            if (solution) {
+                for (int j = 0; j < n; ++j) solution[j] = 0.0;
+                for (int i = 0; i < m; ++i)
+                    if (base[i] < n) solution[base[i]] = rhs[i];
+            }
+        }
+    }
+    if (base_out) std::memcpy(base_out, base.data(), sizeof(int) * m);
+    if (pivots_out) {
+        pivots_out[0] = p1;
+        pivots_out[1] = p2;
+    }
+    return status;
+}
+
+}  // namespace
+
+// ====================================================================== C-ABI
+extern "C" {
+
+int simplex_version(void) { return 1; }
+void simplex_set_verbose(int on) { g_cfg.verbose = on; }
+void simplex_set_update_rows(int rb) { g_cfg.update_rows = (rb == 4 || rb == 16) ? rb : 8; }
+void simplex_set_batch(int pivots) { g_cfg.batch = pivots > 0 ? pivots : 16; }
+void simplex_set_device(int device) {
+    g_cfg.device = device;
+    if (device >= 0) SX_HIP(hipSetDevice(device));
+}
+void simplex_set_virtual_ranks(int world) { g_cfg.virtual_ranks = world > 1 ? world : 1; }
+
+void enableBenchmarkMode(void) { g_cfg.benchmark = true; }
+void disableBenchmarkMode(void) { g_cfg.benchmark = false; }
+
+int simplex_dist_unique_id_size(void) { return (int)sizeof(ncclUniqueId); }
+
+int simplex_dist_get_unique_id(unsigned char *out) {
+    ncclUniqueId id;
+    SX_NCCL(ncclGetUniqueId(&id));
+    std::memcpy(out, &id, sizeof(id));
+    return 0;
+}
+
+int simplex_dist_init(int rank, int world, const unsigned char *unique_id, int device) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (device >= 0) {
+        g_cfg.device = device;
+        SX_HIP(hipSetDevice(device));
+    }
+    g_cfg.rank = rank;
+    g_cfg.world = world;
+    if (world > 1) {
+        ncclUniqueId id;
+        std::memcpy(&id, unique_id, sizeof(id));
+        SX_NCCL(ncclCommInitRank(&g_cfg.comm, world, id, rank));
+        g_cfg.dist = true;
+    }
+    return 0;
+}
+
+int simplex_dist_finalize(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_cfg.comm) {
+        ncclCommDestroy(g_cfg.comm);
+        g_cfg.comm = nullptr;
+    }
+    g_cfg.dist = false;
+    g_cfg.world = 1;
+    g_cfg.rank = 0;
+    return 0;
+}
+
+int twoPhaseMethod(problem_t *problem, TYPE *solution, TYPE *optimalValue) {
+    return two_phase(problem, solution, optimalValue, nullptr, nullptr, -1);
+}
+
+int twoPhaseMethodEx(problem_t *problem, double *solution, double *optimalValue, int *base_out,
+                     long long *pivots_out, long long max_pivots) {
+    return two_phase(problem, solution, optimalValue, base_out, pivots_out, max_pivots);
+}
+
+// ---------------------------------------------------------------- tabular_t API
+tabular_t *newTabular(problem_t *problem) {
+    Engine *E = new Engine(problem->vars, problem->constraints);
+    tabular_t *t = (tabular_t *)malloc(sizeof(tabular_t));
+    t->problem = problem;
+    t->cols = problem->constraints;
+    t->rows = E->N1;
+    t->pitch = E->ld * sizeof(double);
+    t->table = E->sh[0].T;
+    t->knownTermsVector = E->sh[0].T;
+    t->constraintsMatrix = E->sh[0].T + 1;
+    t->costsVector = E->sh[0].d;
+    g_tabs[t] = E;
+    return t;
+}
+
+void freeTabular(tabular_t *tabular) {
+    auto it = g_tabs.find(tabular);
+    if (it != g_tabs.end()) {
+        delete it->second;
+        g_tabs.erase(it);
+    }
+    free(tabular);
+}
+
+// solve(tabular_t*, int*) (solver.cu:128-149): the caller's base is copied in and out.
+int solve(tabular_t *tabular, int *base) {
+    auto it = g_tabs.find(tabular);
+    if (it == g_tabs.end()) SX_FATAL("solve: unknown tabular");
+    Engine *E = it->second;
+    E->write_base(base);
+    long long piv = 0;
+    int st = E->run_phase(tabular->rows, -1, &piv);
+    E->read_base(base);
+    return st;
+}
+
+// tabular.cu:41-98, reference (transposed) orientation
+void printTableauToStream(FILE *Stream, tabular_t *tabular, int *base) {
+    auto it = g_tabs.find(tabular);
+    if (it == g_tabs.end() || tabular->table == nullptr) return;
+    Engine *E = it->second;
+    const int width = tabular->rows, m = tabular->cols;
+    std::vector<double> T((size_t)m * width), d(width);
+    E->download(T.data(), width, width, d.data());
+    fprintf(Stream, "\n--------------- Tabular --------------\n");
+    for (int j = 0; j < width; ++j) {
+        for (int i = 0; i < m; ++i) fprintf(Stream, "%.2lf\t", T[(size_t)i * width + j]);
+        fprintf(Stream, "\t|\t %.11lf\n", d[j]);
+        if (j == 0) fprintf(Stream, "\n");
+    }
+    fprintf(Stream, "Base\n");
+    for (int i = 0; i < m; ++i) fprintf(Stream, "%d\t", base[i]);
+}
+
+// ---------------------------------------------------------------- bench sessions
+struct simplex_session {
+    Engine *E;
+    long long total = 0;
+    bool started = false;
+};
+
+simplex_session *simplex_session_open(problem_t *problem) {
+    simplex_session *S = new simplex_session;
+    S->E = new Engine(problem->vars, problem->constraints);
+    S->E->build_phase1(problem);
+    S->E->update_objective(S->E->N1);
+    S->E->N = S->E->N1;
+    S->E->reset_state(-1);
+    SX_HIP(hipStreamSynchronize(S->E->s));
+    return S;
+}
+
+int simplex_session_pivots(simplex_session *S, long long k, int time_updates, simplex_timing_t *out) {
+    Engine &E = *S->E;
+    std::vector<hipEvent_t> evs;
+    if (time_updates) {
+        evs.resize(2 * (size_t)k);
+        for (auto &e : evs) SX_HIP(hipEventCreate(&e));
+    }
+    hipEvent_t w0, w1;
+    SX_HIP(hipEventCreate(&w0));
+    SX_HIP(hipEventCreate(&w1));
+    const long long before = E.read_state().pivots;
+    SX_HIP(hipEventRecord(w0, E.s));
+    for (long long i = 0; i < k; ++i)
+        E.enqueue_pivot(time_updates ? evs[2 * i] : nullptr, time_updates ? evs[2 * i + 1] : nullptr);
+    SX_HIP(hipEventRecord(w1, E.s));
+    SX_HIP(hipEventSynchronize(w1));
+    DevState f = E.read_state();
+    simplex_timing_t t;
+    std::memset(&t, 0, sizeof(t));
+    float ms = 0.f;
+    SX_HIP(hipEventElapsedTime(&ms, w0, w1));
+    t.wall_ms = ms;
+    t.pivots = f.pivots - before;
+    t.status = f.status;
+    t.width = E.N;
+    long long rows = 0;
+    for (auto &x : E.sh) rows += x.rows;
+    t.local_rows = rows;
+    t.update_bytes = 16.0 * (double)(rows + 1) * (double)E.N;
+    if (time_updates) {
+        double sum = 0.0;
+        for (long long i = 0; i < k; ++i) {
+            float u = 0.f;
+            SX_HIP(hipEventElapsedTime(&u, evs[2 * i], evs[2 * i + 1]));
+            sum += u;
+        }
+        t.update_ms = sum;
+        t.update_launches = k;
+        for (auto &e : evs) (void)hipEventDestroy(e);
+    }
+    (void)hipEventDestroy(w0);
+    (void)hipEventDestroy(w1);
+    S->total = f.pivots;
+    if (out) *out = t;
+    return f.status;
+}
+
+double simplex_session_objective(simplex_session *S) { return S->E->read_d0(); }
+long long simplex_session_total_pivots(simplex_session *S) { return S->E->read_state().pivots; }
+
+void simplex_session_close(simplex_session *S) {
+    if (!S) return;
+    delete S->E;
+    delete S;
+}
+
+// ---------------------------------------------------------------- parity hooks
+long long simplex_dev_argmin(const double *v, long long L, double *vmin) {
+    hipStream_t s;
+    SX_HIP(hipStreamCreate(&s));
+    double *dv = dalloc<double>(L > 0 ? L : 1);
+    TilePart *parts = dalloc<TilePart>(SX_TILE);
+    int *di = dalloc<int>(1);
+    double *dvm = dalloc<double>(1);
+    if (L > 0) SX_HIP(hipMemcpyAsync(dv, v, sizeof(double) * L, hipMemcpyHostToDevice, s));
+    sx_launch_argmin_vector(dv, L, parts, di, dvm, s);
+    int idx = -1;
+    double mv = 0.0;
+    SX_HIP(hipMemcpyAsync(&idx, di, sizeof(int), hipMemcpyDeviceToHost, s));
+    SX_HIP(hipMemcpyAsync(&mv, dvm, sizeof(double), hipMemcpyDeviceToHost, s));
+    SX_HIP(hipStreamSynchronize(s));
+    (void)hipFree(dv);
+    (void)hipFree(parts);
+    (void)hipFree(di);
+    (void)hipFree(dvm);
+    (void)hipStreamDestroy(s);
+    if (vmin) *vmin = mv;
+    return idx;
+}
+
+int simplex_dev_pivots(double *T, long long m, long long N, long long ld, double *d, int *base, long long k,
+                       long long *done) {
+    // a scratch engine sized for width N: n + 2m + 1 >= N is all it needs
+    Engine E((int)(N - 1 - 2 * m) > 0 ? (int)(N - 1 - 2 * m) : 0, (int)m);
+    if ((long long)E.ld < N) SX_FATAL("simplex_dev_pivots: width exceeds engine stride");
+    E.upload(T, (size_t)ld, (int)N, d, base);
+    long long piv = 0;
+    const int st = E.run_phase((int)N, k, &piv);
+    E.download(T, (size_t)ld, (int)N, d);
+    E.read_base(base);
+    if (done) *done = piv;
+    return st == SX_PIVOT_CAP ? SIMPLEX_NOT_ENDED : st;
+}
+
+int simplex_dev_update_objective(const double *T, long long m, long long N, long long ld, const int *base,
+                                 double *d) {
+    Engine E((int)(N - 1 - 2 * m) > 0 ? (int)(N - 1 - 2 * m) : 0, (int)m);
+    if ((long long)E.ld < N) SX_FATAL("simplex_dev_update_objective: width exceeds engine stride");
+    E.upload(T, (size_t)ld, (int)N, d, base);
+    E.update_objective((int)N);
+    SX_HIP(hipStreamSynchronize(E.s));
+    SX_HIP(hipMemcpy(d, E.sh[0].d, sizeof(double) * N, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int simplex_dev_build_phase1(problem_t *problem, double *T, long long ld, double *d, int *base) {
+    Engine E(problem->vars, problem->constraints);
+    E.build_phase1(problem);
+    E.download(T, (size_t)ld, E.N1, d);
+    E.read_base(base);
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,521 @@
+// sx_kernels.hip -- CDNA4 (gfx950) kernels of the dense two-phase simplex pivot path.
+//
+// Layout: the tableau T is row-major in HBM, one row per constraint, row
+// stride ld doubles; column 0 = RHS b, column v+1 = variable v.  The objective row d is
+// a separate vector, replicated on every shard.  Shards own contiguous row ranges whose
+// starts are multiples of 512 (the reference's argmin tile).
+//
+// Every decision uses the reference's epsilon comparison (macro.h:28-42) and its exact
+// argmin combine tree (reduction.cu:10-104): a 32-lane shuffle-down tree per "warp",
+// then the 16 (pass 1, 512 threads) or 32 (pass 2, 1024 threads) warp winners combined
+// by the same 32-lane tree.  On wave64 a reference warp is one 32-lane half of a wave:
+// __shfl_down(x, off, 32) stays inside the half and returns the lane's own value past its
+// end, exactly like the CUDA shuffle.  Compiled with -ffp-contract=off; every fused
+// multiply-add of the reference is an explicit fma().
+
+#include <float.h>
+
+#include "sx_common.hpp"
+
+namespace {
+
+__device__ __forceinline__ int cmp_eps(double x, double y) {
+    if (fabs(x - y) < SX_EPS) return 0;
+    return x < y ? -1 : 1;
+}
+
+// warpReduceMin (reduction.cu:10-22) on one 32-lane half of a wave64.
+__device__ __forceinline__ void half_argmin(double &v, int &i) {
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) {
+        const double sv = __shfl_down(v, off, 32);
+        const int si = __shfl_down(i, off, 32);
+        if (cmp_eps(sv, v) < 0) {
+            v = sv;
+            i = si;
+        }
+    }
+}
+
+// blockReduceMin (reduction.cu:24-49) for a 512-thread block (8 waves = 16 halves).
+// Result valid in thread 0.  The same tree is the reference's 1024-thread pass 2 whenever
+// at most 512 partials exist: halves 16..31 of that block would hold only (DBL_MAX, -1),
+// which is exactly the padding the 512-thread final stage inserts.
+__device__ __forceinline__ void block_argmin512(double &v, int &i, double *s_v, int *s_i) {
+    half_argmin(v, i);
+    const int lane = threadIdx.x & 31;
+    const int h = threadIdx.x >> 5;
+    if (lane == 0) {
+        s_v[h] = v;
+        s_i[h] = i;
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        v = (threadIdx.x < 16) ? s_v[threadIdx.x] : DBL_MAX;
+        i = (threadIdx.x < 16) ? s_i[threadIdx.x] : -1;
+        half_argmin(v, i);
+    }
+}
+
+// Pass 2 (deviceReduceKernel<false><<<1,1024>>>, reduction.cu:239-241) over B <= 512 tile
+// winners.  A partial equal to DBL_MAX is not taken (compare(DBL_MAX, DBL_MAX) == 0), so
+// its index stays -1, as in the reference.
+__device__ __forceinline__ void stage2_512(const TilePart *parts, int B, double &v, int &i, double *s_v,
+                                           int *s_i) {
+    v = DBL_MAX;
+    i = -1;
+    if ((int)threadIdx.x < B) {
+        const double c = parts[threadIdx.x].v;
+        if (cmp_eps(c, v) < 0) {
+            v = c;
+            i = parts[threadIdx.x].idx;
+        }
+    }
+    block_argmin512(v, i, s_v, s_i);
+}
+
+// ---------------------------------------------------------------------------------------
+// K1: entering-variable pass 1 over d[1..N) (minElement(costs+1, rows-1), solver.cu:87).
+// Grid-stride exactly as the reference when L > 512*1024 (never for BASELINE sizes).
+__global__ __launch_bounds__(512) void k_argmin_pass1(const double *__restrict__ v, int L, TilePart *out,
+                                                      const DevState *st) {
+    if (st != nullptr && st->status != SX_NOT_ENDED) return;
+    __shared__ double s_v[16];
+    __shared__ int s_i[16];
+    double mv = DBL_MAX;
+    int mi = -1;
+    for (int i = blockIdx.x * SX_TILE + threadIdx.x; i < L; i += SX_TILE * gridDim.x) {
+        const double c = v[i];
+        if (cmp_eps(c, mv) < 0) {
+            mv = c;
+            mi = i;
+        }
+    }
+    block_argmin512(mv, mi, s_v, s_i);
+    if (threadIdx.x == 0) {
+        out[blockIdx.x].v = mv;
+        out[blockIdx.x].idx = mi;
+        out[blockIdx.x].elig = 0;
+    }
+}
+
+// Stand-alone pass 2 (used by the argmin test hook).
+__global__ __launch_bounds__(512) void k_argmin_pass2(const TilePart *parts, int B, int *out_idx, double *out_v) {
+    __shared__ double s_v[16];
+    __shared__ int s_i[16];
+    double v;
+    int i;
+    stage2_512(parts, B, v, i, s_v, s_i);
+    if (threadIdx.x == 0) {
+        *out_idx = i;
+        *out_v = v;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// K2: every block re-derives the entering variable from the pass-1 partials (a 512-thread
+// pass 2, cheap), stops the phase if compare(dmin) >= 0 (solver.cu:88), else builds the
+// ratio vector of its 512 rows (createIndicatorsVector, reduction.cu:106-114), saves the
+// pre-update entering column (the reference's rowPivot copy, solver.cu:90-94), and emits
+// the tile winner + "any entry >= eps" (isLessOrEqualThanZero, reduction.cu:186-201).
+__global__ __launch_bounds__(512) void k_ratio_partials(const double *__restrict__ T, int rows, int row0, size_t ld,
+                                                        const TilePart *__restrict__ enter_parts, int B1,
+                                                        TilePart *tiles_local, double *colE, DevState *st) {
+    if (st->status != SX_NOT_ENDED) return;
+    const bool leader = blockIdx.x == 0 && threadIdx.x == 0;
+    if (st->max_pivots >= 0 && st->pivots >= st->max_pivots) {
+        if (leader) st->status = SX_PIVOT_CAP;
+        return;
+    }
+    __shared__ double s_v[16];
+    __shared__ int s_i[16];
+    __shared__ double s_bv;
+    __shared__ int s_bi;
+    double v;
+    int e;
+    stage2_512(enter_parts, B1, v, e, s_v, s_i);
+    if (threadIdx.x == 0) {
+        s_bv = v;
+        s_bi = e;
+    }
+    __syncthreads();
+    v = s_bv;
+    e = s_bi;
+    if (!(cmp_eps(v, 0.0) < 0)) {
+        if (leader) st->status = SX_FEASIBLE;
+        return;
+    }
+    if (leader) {
+        st->e = e;
+        st->dmin = v;
+    }
+    const int li = blockIdx.x * SX_TILE + threadIdx.x;
+    double rv = DBL_MAX;
+    int ri = -1;
+    int elig = 0;
+    if (li < rows) {
+        const double *row = T + (size_t)li * ld;
+        const double a = row[1 + e];
+        const double b = row[0];
+        colE[li] = a;
+        elig = a >= SX_EPS;
+        const double ratio = cmp_eps(a, 0.0) > 0 ? b / a : DBL_MAX;
+        if (cmp_eps(ratio, rv) < 0) {
+            rv = ratio;
+            ri = row0 + li;
+        }
+    }
+    const int any = __syncthreads_or(elig);
+    block_argmin512(rv, ri, s_v, s_i);
+    if (threadIdx.x == 0) {
+        tiles_local[blockIdx.x].v = rv;
+        tiles_local[blockIdx.x].idx = ri;
+        tiles_local[blockIdx.x].elig = any;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// K3: every block re-derives the leaving row from the (gathered) tile winners, checks
+// the unbounded condition, and copies its chunk of the pre-update pivot row (the
+// reference's copyColumn, solver.cu:24-32, is a contiguous row here).  With several
+// shards only the owner contributes the row; the others contribute -0.0, the exact
+// additive identity, so a sum-allreduce reproduces the owner's row bit for bit.
+__global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T, int rows, int row0, size_t ld,
+                                                    int N, const TilePart *__restrict__ tiles_all, int B2,
+                                                    double *prow_out, int multi, int *base, DevState *st) {
+    if (st->status != SX_NOT_ENDED) return;
+    const bool leader = blockIdx.x == 0 && threadIdx.x == 0;
+    __shared__ double s_v[16];
+    __shared__ int s_i[16];
+    __shared__ int s_r;
+    const int elig = ((int)threadIdx.x < B2) ? tiles_all[threadIdx.x].elig : 0;
+    if (!__syncthreads_or(elig)) {
+        if (leader) st->status = SX_UNBOUNDED;  // solver.cu:96-102
+        return;
+    }
+    double v;
+    int r;
+    stage2_512(tiles_all, B2, v, r, s_v, s_i);
+    if (threadIdx.x == 0) s_r = r;
+    __syncthreads();
+    r = s_r;
+    if (r < 0) {
+        if (leader) st->status = SX_NUMERIC_FAIL;
+        return;
+    }
+    const bool own = r >= row0 && r < row0 + rows;
+    const double *src = T + (size_t)(own ? r - row0 : 0) * ld;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < N; j += gridDim.x * blockDim.x)
+        prow_out[j] = own ? src[j] : (multi ? -0.0 : 0.0);
+    if (leader) {
+        base[r] = st->e;  // solver.cu:105
+        st->r = r;
+        st->pivots += 1;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// K4: the rank-1 pivot update (updateContraintsMatrix + updateCostsVector, solver.cu:34-56)
+//   row r:       T[r][j] = prow[j] / p
+//   other rows:  T[i][j] = fma(-(a_ie / p), prow[j], T[i][j])   (factor hoisted per row:
+//                the reference recomputes the same division per element, bit-identical)
+//   objective:   d[j]    = fma(-(d_e / p),  prow[j], d[j])
+// prow and colE are pre-update copies, so the kernel reads only them and its own
+// element: no ordering between workgroups.  Each thread owns 2 adjacent columns (one
+// 16-byte load/store per row), a block covers 512 columns x RB rows; the RB loads of a
+// thread are issued before any use to keep 16 B x RB in flight per lane.
+template <int RB>
+__global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows, int row0, size_t ld, int N,
+                                                double *__restrict__ d, const double *__restrict__ prow,
+                                                const double *__restrict__ colE, const DevState *st) {
+    if (st->status != SX_NOT_ENDED) return;
+    const int e = st->e;
+    const int r = st->r - row0;
+    const double p = prow[1 + e];
+    __shared__ double s_f[RB];
+    const int i0 = blockIdx.y * RB;
+    if ((int)threadIdx.x < RB) {
+        const int i = i0 + threadIdx.x;
+        s_f[threadIdx.x] = (i < rows) ? -colE[i] / p : 0.0;
+    }
+    __syncthreads();
+    const int j = (blockIdx.x * 256 + threadIdx.x) * 2;
+    if (j >= N) return;
+    const int nrow = rows - i0 < RB ? rows - i0 : RB;
+    if (j + 1 < N) {
+        const double2 pr = *reinterpret_cast<const double2 *>(prow + j);
+        if (blockIdx.y == 0) {
+            const double fd = -st->dmin / p;
+            double2 x = *reinterpret_cast<double2 *>(d + j);
+            x.x = fma(fd, pr.x, x.x);
+            x.y = fma(fd, pr.y, x.y);
+            *reinterpret_cast<double2 *>(d + j) = x;
+        }
+        double *base = T + (size_t)i0 * ld + j;
+        if (nrow == RB) {
+            double2 x[RB];
+#pragma unroll
+            for (int k = 0; k < RB; ++k) x[k] = *reinterpret_cast<const double2 *>(base + (size_t)k * ld);
+#pragma unroll
+            for (int k = 0; k < RB; ++k) {
+                if (i0 + k == r) {
+                    x[k].x = pr.x / p;
+                    x[k].y = pr.y / p;
+                } else {
+                    const double f = s_f[k];
+                    x[k].x = fma(f, pr.x, x[k].x);
+                    x[k].y = fma(f, pr.y, x[k].y);
+                }
+                *reinterpret_cast<double2 *>(base + (size_t)k * ld) = x[k];
+            }
+        } else {
+            for (int k = 0; k < nrow; ++k) {
+                double2 x = *reinterpret_cast<const double2 *>(base + (size_t)k * ld);
+                if (i0 + k == r) {
+                    x.x = pr.x / p;
+                    x.y = pr.y / p;
+                } else {
+                    const double f = s_f[k];
+                    x.x = fma(f, pr.x, x.x);
+                    x.y = fma(f, pr.y, x.y);
+                }
+                *reinterpret_cast<double2 *>(base + (size_t)k * ld) = x;
+            }
+        }
+    } else {
+        // last (odd) column of the phase width: scalar path
+        const double pr = prow[j];
+        if (blockIdx.y == 0) d[j] = fma(-st->dmin / p, pr, d[j]);
+        for (int k = 0; k < nrow; ++k) {
+            double *x = T + (size_t)(i0 + k) * ld + j;
+            *x = (i0 + k == r) ? pr / p : fma(s_f[k], pr, *x);
+        }
+    }
+}
+
+// Virtual-rank "allreduce": out = sum of the shards' contributions in rank order.  Exact,
+// since all but one contribution are -0.0.
+__global__ void k_sum_rows(double *out, const double *const *srcs, int nsrc, int N) {
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < N; j += gridDim.x * blockDim.x) {
+        double s = srcs[0][j];
+        for (int k = 1; k < nsrc; ++k) s = s + srcs[k][j];
+        out[j] = s;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Objective canonicalisation (updateObjectiveFunction, gaussian.cu:132-162):
+//   coef[i] = d[1 + base[i]] (snapshot), then d[j] -= sum_i T[i][j] * coef[i].
+// The reference sums with fp64 atomics in arrival order (nondeterministic).  Here the
+// order is fixed: an fma chain over each 512-row block, then the block partials summed in
+// block order -- identical on 1 or W shards because shard boundaries are 512-aligned.
+__global__ void k_coef(const double *d, const int *base, int row0, int rows, double *coef) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < rows) coef[i] = d[1 + base[row0 + i]];
+}
+
+__global__ __launch_bounds__(256) void k_gemv_partials(const double *__restrict__ T, int rows, size_t ld, int N,
+                                                       const double *__restrict__ coef, double *partials) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int k = blockIdx.y;
+    if (j >= N) return;
+    const int i1 = (k + 1) * SX_TILE < rows ? (k + 1) * SX_TILE : rows;
+    double s = 0.0;
+    const double *col = T + j;
+    int i = k * SX_TILE;
+    for (; i + 4 <= i1; i += 4) {
+        const double t0 = col[(size_t)i * ld], t1 = col[(size_t)(i + 1) * ld];
+        const double t2 = col[(size_t)(i + 2) * ld], t3 = col[(size_t)(i + 3) * ld];
+        s = fma(t0, coef[i], s);
+        s = fma(t1, coef[i + 1], s);
+        s = fma(t2, coef[i + 2], s);
+        s = fma(t3, coef[i + 3], s);
+    }
+    for (; i < i1; ++i) s = fma(col[(size_t)i * ld], coef[i], s);
+    partials[(size_t)k * N + j] = s;
+}
+
+__global__ void k_gemv_apply(double *d, int N, const double *__restrict__ partials, int nblk) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= N) return;
+    double s = partials[j];
+    for (int k = 1; k < nblk; ++k) s = s + partials[(size_t)k * N + j];
+    d[j] = d[j] - s;
+}
+
+// ---------------------------------------------------------------------------------------
+// Tableau construction (fillTableu + checkColumns, twoPhaseMethod.cu:145-200, 86-111).
+// A_local is the shard's slice of the column-major A: A_local[j*rows + i] = A(row0+i, j).
+// 32x32 LDS transpose so both the read (along i) and the write (along j) are coalesced.
+__global__ __launch_bounds__(256) void k_fill_structural(double *T, int rows, size_t ld, int n,
+                                                         const double *__restrict__ A_local) {
+    __shared__ double tile[32][33];
+    const int i_base = blockIdx.x * 32, j_base = blockIdx.y * 32;
+    for (int jj = threadIdx.y; jj < 32; jj += 8) {
+        const int i = i_base + threadIdx.x, j = j_base + jj;
+        tile[jj][threadIdx.x] = (i < rows && j < n) ? A_local[(size_t)j * rows + i] : 0.0;
+    }
+    __syncthreads();
+    for (int ii = threadIdx.y; ii < 32; ii += 8) {
+        const int i = i_base + ii, j = j_base + threadIdx.x;
+        if (i < rows && j < n) T[(size_t)i * ld + 1 + j] = tile[threadIdx.x][ii];
+    }
+}
+
+// RHS, slack/artificial identities, and the b<0 quirk: a row with compare(b_i) < 0 is
+// negated across ALL its entries, slack and artificial included.
+__global__ void k_fill_rows(double *T, int rows, int row0, size_t ld, int n, int m, const double *b_full) {
+    const int i = blockIdx.y;
+    if (i >= rows) return;
+    const int gi = row0 + i;
+    const double bi = b_full[gi];
+    const bool neg = cmp_eps(bi, 0.0) < 0;
+    double *row = T + (size_t)i * ld;
+    const int N1 = 1 + n + 2 * m;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < N1; j += gridDim.x * blockDim.x) {
+        double x;
+        if (j == 0)
+            x = bi;
+        else if (j <= n)
+            x = row[j];
+        else
+            x = (j == 1 + n + gi || j == 1 + n + m + gi) ? 1.0 : 0.0;
+        row[j] = neg ? -x : x;
+    }
+}
+
+// d: phase-1 costs (0 for x and slacks, 1 for artificials, twoPhaseMethod.cu:152-157);
+// base[i] = n+m+i (fillBaseVector, :44-52).
+__global__ void k_init_vectors(double *d, int N1, int n, int m, int *base) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < N1) d[t] = (t <= n + m) ? 0.0 : 1.0;
+    if (t < m) base[t] = n + m + t;
+}
+
+// Phase-2 costs (twoPhaseMethod.cu:306-318): d[1..n] = -c, d[n+1..n+m] = 0, d[0] kept.
+__global__ void k_phase2_costs(double *d, int n, int m, const double *c) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) d[1 + t] = -c[t];
+    if (t < m) d[1 + n + t] = 0.0;
+}
+
+__global__ void k_gather_rhs(const double *T, int rows, size_t ld, double *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < rows) out[i] = T[(size_t)i * ld];
+}
+
+}  // namespace
+
+// =========================== launchers ===========================
+
+int sx_enter_blocks(int L) {
+    int g = (L + SX_TILE - 1) / SX_TILE;
+    if (g > 1024) g = 1024;
+    if (g < 1) g = 1;
+    return g;
+}
+
+void sx_launch_enter_partials(const double *d, int L, TilePart *out, const DevState *st, hipStream_t s) {
+    const int g = sx_enter_blocks(L);
+    if (g > SX_TILE) SX_FATAL("entering vector too long for the 512-thread pass 2");
+    k_argmin_pass1<<<g, SX_TILE, 0, s>>>(d + 1, L, out, st);
+}
+
+void sx_launch_ratio_partials(const double *T, int rows, int row0, size_t ld, const TilePart *enter_parts, int B1,
+                              TilePart *tiles_local, double *colE, DevState *st, hipStream_t s) {
+    int g = (rows + SX_TILE - 1) / SX_TILE;
+    if (g < 1) g = 1;  // a shard without rows still decides optimality for its own state
+    k_ratio_partials<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, enter_parts, B1, tiles_local, colE, st);
+}
+
+void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, int N, const TilePart *tiles_all, int B2,
+                          double *prow_out, bool multi, int *base, DevState *st, hipStream_t s) {
+    if (B2 > SX_TILE) SX_FATAL("too many ratio tiles for the 512-thread pass 2");
+    int g = (N + 4 * SX_TILE - 1) / (4 * SX_TILE);
+    if (g < 1) g = 1;
+    if (g > 64) g = 64;
+    k_select_row<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, N, tiles_all, B2, prow_out, multi ? 1 : 0, base, st);
+}
+
+void sx_launch_update(double *T, int rows, int row0, size_t ld, int N, double *d, const double *prow,
+                      const double *colE, const DevState *st, int rb, hipStream_t s) {
+    const int cols_blocks = (N + 511) / 512;
+    if (rows < 1) rows = 0;  // grid keeps one row-block so the objective row is updated
+    switch (rb) {
+    case 4: {
+        dim3 grid(cols_blocks, rows > 0 ? (rows + 3) / 4 : 1);
+        k_update<4><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow, colE, st);
+        break;
+    }
+    case 16: {
+        dim3 grid(cols_blocks, rows > 0 ? (rows + 15) / 16 : 1);
+        k_update<16><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow, colE, st);
+        break;
+    }
+    default: {
+        dim3 grid(cols_blocks, rows > 0 ? (rows + 7) / 8 : 1);
+        k_update<8><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow, colE, st);
+        break;
+    }
+    }
+}
+
+void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s) {
+    int g = (N + 255) / 256;
+    if (g > 1024) g = 1024;
+    k_sum_rows<<<g, 256, 0, s>>>(out, srcs, nsrc, N);
+}
+
+void sx_launch_coef(const double *d, const int *base, int row0, int rows, double *coef, hipStream_t s) {
+    if (rows <= 0) return;
+    k_coef<<<(rows + 255) / 256, 256, 0, s>>>(d, base, row0, rows, coef);
+}
+
+void sx_launch_gemv_partials(const double *T, int rows, size_t ld, int N, const double *coef, double *partials,
+                             hipStream_t s) {
+    const int nblk = (rows + SX_TILE - 1) / SX_TILE;
+    if (nblk == 0) return;
+    dim3 grid((N + 255) / 256, nblk);
+    k_gemv_partials<<<grid, 256, 0, s>>>(T, rows, ld, N, coef, partials);
+}
+
+void sx_launch_gemv_apply(double *d, int N, const double *partials, int nblk, hipStream_t s) {
+    k_gemv_apply<<<(N + 255) / 256, 256, 0, s>>>(d, N, partials, nblk);
+}
+
+void sx_launch_build_rows(double *T, int rows, int row0, size_t ld, int n, int m, const double *A_local,
+                          const double *b_full, hipStream_t s) {
+    if (rows <= 0) return;
+    dim3 tb(32, 8);
+    dim3 tg((rows + 31) / 32, (n + 31) / 32);
+    if (n > 0) k_fill_structural<<<tg, tb, 0, s>>>(T, rows, ld, n, A_local);
+    const int N1 = 1 + n + 2 * m;
+    int gx = (N1 + 255) / 256;
+    if (gx > 64) gx = 64;
+    dim3 rg(gx, rows);
+    k_fill_rows<<<rg, 256, 0, s>>>(T, rows, row0, ld, n, m, b_full);
+}
+
+void sx_launch_init_vectors(double *d, int N1, int n, int m, int *base, hipStream_t s) {
+    const int t = N1 > m ? N1 : m;
+    k_init_vectors<<<(t + 255) / 256, 256, 0, s>>>(d, N1, n, m, base);
+}
+
+void sx_launch_phase2_costs(double *d, int n, int m, const double *c, hipStream_t s) {
+    const int t = n > m ? n : m;
+    if (t == 0) return;
+    k_phase2_costs<<<(t + 255) / 256, 256, 0, s>>>(d, n, m, c);
+}
+
+void sx_launch_gather_rhs(const double *T, int rows, size_t ld, double *out, hipStream_t s) {
+    if (rows <= 0) return;
+    k_gather_rhs<<<(rows + 255) / 256, 256, 0, s>>>(T, rows, ld, out);
+}
+
+void sx_launch_argmin_vector(const double *v, long long L, TilePart *parts, int *out_idx, double *out_v,
+                             hipStream_t s) {
+    const int g = sx_enter_blocks((int)L);
+    if (g > SX_TILE) SX_FATAL("vector too long for the 512-thread pass 2");
+    k_argmin_pass1<<<g, SX_TILE, 0, s>>>(v, (int)L, parts, nullptr);
+    k_argmin_pass2<<<1, SX_TILE, 0, s>>>(parts, g, out_idx, out_v);
+}

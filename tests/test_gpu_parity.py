@@ -1,0 +1,192 @@
+"""HIP path vs CPU oracle, through the C-ABI (needs an MI355X).
+
+Bar: bit-exact on every tableau entry, objective entry, basis and pivot count -- the HIP
+kernels perform the same IEEE operations as the reference (fma, correctly rounded
+division) in the same order, and the argmin reproduces the reference's combine tree.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import simplexoncuda_amd as sx
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a, dtype=np.float64).view(np.uint64)
+
+
+def same(a, b):
+    return np.array_equal(bits(a), bits(b))
+
+
+# ------------------------------------------------------------------ argmin tree
+@pytest.mark.parametrize("L", [1, 2, 31, 32, 33, 511, 512, 513, 4097, 16384, 73728, 100000])
+def test_dev_argmin_matches_oracle(gpu, L):
+    rng = np.random.default_rng(L)
+    v = rng.integers(-4, 4, size=L).astype(np.float64)
+    v[rng.integers(0, L, size=max(1, L // 5))] += rng.choice([3e-10, -7e-10, 2e-9], size=max(1, L // 5))
+    assert sx.dev_argmin(v) == oracle.argmin(v)
+
+
+def test_dev_argmin_all_max(gpu):
+    big = np.finfo(np.float64).max
+    v = np.full(1000, big)
+    assert sx.dev_argmin(v)[0] == -1 == oracle.argmin(v)[0]
+
+
+# ------------------------------------------------------------------ tableau build + GEMV
+@pytest.mark.parametrize("n,m,lo,hi", [(20, 10, 1, 100), (37, 600, -100, 100), (300, 1100, 1, 100), (1, 1, -5, 5)])
+def test_build_phase1_bit_exact(gpu, n, m, lo, hi):
+    p = sx.generateRandomProblem(n, m, n * 100 + m, lo, hi)
+    A, b, c = p.arrays()
+    T, d, base = sx.dev_build_phase1(p)
+    To, do, bo = oracle.build_phase1(A, b)
+    assert same(T, To) and same(d, do) and np.array_equal(base, bo)
+
+
+@pytest.mark.parametrize("n,m", [(50, 40), (300, 1100)])
+def test_update_objective_bit_exact(gpu, n, m):
+    A, b, c = oracle.generate(n, m, 7 + n + m, -100, 100)
+    T, d, base = oracle.build_phase1(A, b)
+    d_gpu = d.copy()
+    sx.dev_update_objective(T, d_gpu, base)
+    oracle.update_objective(T, d, base)
+    assert same(d_gpu, d)
+
+
+# ------------------------------------------------------------------ pivots
+def _phase1_state(n, m, seed, lo=1, hi=100):
+    A, b, c = oracle.generate(n, m, seed, lo, hi)
+    T, d, base = oracle.build_phase1(A, b)
+    oracle.update_objective(T, d, base)
+    return T, d, base
+
+
+@pytest.mark.parametrize("n,m,k", [(20, 10, 5), (256, 256, 40), (333, 1025, 30), (2048, 1024, 25)])
+def test_pivots_bit_exact(gpu, n, m, k):
+    T, d, base = _phase1_state(n, m, n * 100 + m)
+    Tg, dg, bg = T.copy(), d.copy(), base.copy()
+    st_g, done_g = sx.dev_pivots(Tg, dg, bg, k)
+    st_o, done_o = oracle.solve(T, d, base, max_pivots=k)
+    assert done_g == done_o
+    assert (st_g == sx.NOT_ENDED) == (st_o == oracle.PIVOT_CAP)
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+def test_pivots_to_phase_end(gpu):
+    T, d, base = _phase1_state(64, 128, 6528)
+    Tg, dg, bg = T.copy(), d.copy(), base.copy()
+    st_g, done_g = sx.dev_pivots(Tg, dg, bg, 100000)
+    st_o, done_o = oracle.solve(T, d, base)
+    assert st_g == st_o == oracle.FEASIBLE and done_g == done_o
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+# ------------------------------------------------------------------ whole two-phase method
+def _check_two_phase(p):
+    got = sx.twoPhaseMethodEx(p)
+    A, b, c = p.arrays()
+    ref = oracle.two_phase(A, b, c)
+    assert got.status == ref["status"]
+    assert tuple(got.pivots) == ref["pivots"]
+    assert np.array_equal(got.base, ref["base"])
+    if got.status == sx.FEASIBLE:
+        assert same(got.optimal_value, ref["opt"])
+        assert same(got.solution, ref["x"])
+    return got, ref
+
+
+@pytest.mark.parametrize("name", ["smallProblem.txt", "infeasibleProblem.txt", "unboundedProblem.txt"])
+def test_examples(gpu, name):
+    p = sx.readProblemFromFile(os.path.join(GOLDEN, "examples", name))
+    got, _ = _check_two_phase(p)
+    expect = {"smallProblem.txt": (sx.FEASIBLE, (2, 2)), "infeasibleProblem.txt": (sx.INFEASIBLE, (2, 0)),
+              "unboundedProblem.txt": (sx.UNBOUNDED, (2, 0))}[name]
+    assert (got.status, tuple(got.pivots)) == expect
+    if got.status == sx.FEASIBLE:
+        assert got.optimal_value == pytest.approx(64.0) and list(got.solution) == pytest.approx([8, 0, 0])
+
+
+@pytest.mark.parametrize("n,m,seed,lo,hi", [
+    (20, 10, 2010, 1, 100), (20, 10, 2010, -100, 100), (25, 25, 99, -100, 100), (8, 6, 7, -100, 100),
+    (1, 1, 11, 1, 100), (3, 600, 5, 1, 100), (700, 3, 5, 1, 100), (129, 513, 77, -100, 100)])
+def test_two_phase_generated(gpu, n, m, seed, lo, hi):
+    _check_two_phase(sx.generateRandomProblem(n, m, seed, lo, hi))
+
+
+def test_two_phase_scipy_optima(gpu):
+    with open(os.path.join(GOLDEN, "scipy_optima.json")) as f:
+        for r in json.load(f):
+            got = sx.twoPhaseMethodEx(sx.generateRandomProblem(r["n"], r["m"], r["seed"], r["lo"], r["hi"]))
+            if r["highs_status"] == 0:
+                assert got.status == sx.FEASIBLE
+                assert got.optimal_value == pytest.approx(r["highs_opt"], rel=1e-6)
+            elif r["highs_status"] == 3:
+                assert got.status == sx.UNBOUNDED
+
+
+def _published(n, m):
+    with open(os.path.join(GOLDEN, "published_pivots.json")) as f:
+        return [x for x in json.load(f) if x["n"] == n and x["m"] == m and x["gpu"] == "rtx2070super"][0]
+
+
+@pytest.mark.parametrize("n,m", [(256, 256), (1024, 512), (2048, 1024), (8192, 512), (2048, 2048), (8192, 4096)])
+def test_published_pivot_counts_on_gpu(gpu, n, m):
+    rec = _published(n, m)
+    got = sx.twoPhaseMethodEx(sx.generateRandomProblem(n, m, rec["seed"], 1, 100))
+    assert got.status == sx.FEASIBLE
+    assert tuple(got.pivots) == (rec["p1_pivots"], rec["p2_pivots"])
+
+
+def test_config2_full_solve_bit_exact(gpu):
+    """configs[1]: n=2048, m=1024, seed 205824 -- every bit of the answer vs the oracle."""
+    got, ref = _check_two_phase(sx.generateRandomProblem(2048, 1024, 205824, 1, 100))
+    assert tuple(got.pivots) == (2003, 69)
+
+
+# ------------------------------------------------------------------ sharded path on one device
+@pytest.mark.parametrize("W", [2, 3, 4])
+def test_virtual_ranks_pivots_identical(gpu, W):
+    T, d, base = _phase1_state(200, 1500, 42)
+    ref = (T.copy(), d.copy(), base.copy())
+    sx.dev_pivots(*ref, 60)
+    try:
+        sx.set_virtual_ranks(W)
+        Tg, dg, bg = T.copy(), d.copy(), base.copy()
+        sx.dev_pivots(Tg, dg, bg, 60)
+    finally:
+        sx.set_virtual_ranks(1)
+    assert same(Tg, ref[0]) and same(dg, ref[1]) and np.array_equal(bg, ref[2])
+
+
+@pytest.mark.parametrize("W", [2, 8])
+def test_virtual_ranks_two_phase(gpu, W):
+    p = sx.generateRandomProblem(300, 1100, 300 * 100 + 1100, 1, 100)
+    base1 = sx.twoPhaseMethodEx(p)
+    try:
+        sx.set_virtual_ranks(W)
+        got = sx.twoPhaseMethodEx(p)
+    finally:
+        sx.set_virtual_ranks(1)
+    assert got.status == base1.status and tuple(got.pivots) == tuple(base1.pivots)
+    assert np.array_equal(got.base, base1.base)
+    assert same(got.optimal_value, base1.optimal_value) and same(got.solution, base1.solution)
+
+
+# ------------------------------------------------------------------ bench session
+def test_session_pivots(gpu):
+    p = sx.generateRandomProblem(2048, 1024, 205824, 1, 100)
+    s = sx.Session(p)
+    t = s.pivots(50, time_updates=True)
+    assert t.pivots == 50 and t.status == sx.NOT_ENDED and t.update_launches == 50
+    assert t.update_ms > 0 and t.wall_ms >= t.update_ms
+    assert t.update_bytes == 16.0 * (1024 + 1) * (1 + 2048 + 2 * 1024)
+    t2 = s.pivots(10000)
+    assert s.total_pivots() == 2003 and t2.status == sx.FEASIBLE
+    s.close()
