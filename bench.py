@@ -96,7 +96,8 @@ def main():
     ap.add_argument("--steps", type=int, default=1000, help="timed pivots")
     ap.add_argument("--warmup", type=int, default=50, help="untimed pivots before timing")
     ap.add_argument("--config", default="config3", choices=sorted(CONFIGS))
-    ap.add_argument("--update-rows", type=int, default=8)
+    ap.add_argument("--update-rows", type=int, default=0, help="rows per update workgroup (0 = auto)")
+    ap.add_argument("--snake", type=int, default=-1, help="alternate update sweep: -1 auto, 0 off, 1 on")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-file", default=None, help="per-launch HBM bytes from rocprofv3 --pmc (JSON)")
     args = ap.parse_args()
@@ -119,6 +120,7 @@ def main():
     else:
         sx.load().simplex_set_device(local_rank)
     sx.set_update_rows(args.update_rows)
+    sx.set_snake(args.snake)
 
     n, m, seed = CONFIGS[args.config]
     problem = sx.generateRandomProblem(n, m, seed, 1, 100)

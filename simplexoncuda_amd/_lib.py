@@ -80,6 +80,7 @@ SIGNATURES = {
     "simplex_version": (ctypes.c_int, []),
     "simplex_set_verbose": (None, [ctypes.c_int]),
     "simplex_set_update_rows": (None, [ctypes.c_int]),
+    "simplex_set_snake": (None, [ctypes.c_int]),
     "simplex_set_batch": (None, [ctypes.c_int]),
     "simplex_set_device": (None, [ctypes.c_int]),
     "simplex_dist_unique_id_size": (ctypes.c_int, []),

@@ -243,5 +243,9 @@ def set_update_rows(rb):
     _lib.load().simplex_set_update_rows(int(rb))
 
 
+def set_snake(mode):
+    _lib.load().simplex_set_snake(int(mode))
+
+
 def set_batch(p):
     _lib.load().simplex_set_batch(int(p))

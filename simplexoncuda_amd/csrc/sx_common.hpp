@@ -31,13 +31,15 @@ struct __attribute__((aligned(16))) TilePart {
 // Per-shard pivot state, resident in device memory (never read by the host inside a
 // batch of pivots).
 struct __attribute__((aligned(16))) DevState {
-    int status;         // SX_NOT_ENDED while the phase runs
-    int e;              // entering variable (0-based variable index; column e+1)
-    int r;              // leaving constraint row (global index)
-    int pad0;
-    double dmin;        // reduced cost of the entering variable (d[e+1] before update)
-    long long pivots;   // pivots applied in this phase
+    int status;            // SX_NOT_ENDED while the phase runs
+    int e;                 // entering variable (0-based variable index; column e+1)
+    int r;                 // leaving constraint row (global index) of the last pivot; its
+                           // new values sit in `rnew` until the next kernel writes them back
+    unsigned ticket;       // arrival counter of the ratio/select hand-off (zero between launches)
+    double dmin;           // reduced cost of the entering variable (d[e+1] before update)
+    long long pivots;      // pivots applied in this phase
     long long max_pivots;  // < 0: no cap (reference behaviour)
+    long long pad1;
 };
 
 // Error convention of the reference (error.cu:5-12): print "<msg> in <file> at line <n>"
@@ -48,18 +50,23 @@ void sx_fatal(const char *msg, const char *file, int line);
 #define SX_FATAL(msg) sx_fatal((msg), __FILE__, __LINE__)
 
 // ---- kernel launchers (sx_kernels.hip) ----
-struct LaunchCfg {
-    int update_rows;     // rows per update block (template RB)
+struct UpdateCfg {
+    int rows_per_block;  // 1, 2, 4 or 8
+    int snake;           // alternate the sweep direction every pivot
 };
 
-void sx_launch_enter_partials(const double *d, int L, TilePart *out, const DevState *st, hipStream_t s);
 int sx_enter_blocks(int L);
-void sx_launch_ratio_partials(const double *T, int rows, int row0, size_t ld, const TilePart *enter_parts,
-                              int B1, TilePart *tiles_local, double *colE, DevState *st, hipStream_t s);
-void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, int N, const TilePart *tiles_all,
-                          int B2, double *prow_out, bool multi, int *base, DevState *st, hipStream_t s);
-void sx_launch_update(double *T, int rows, int row0, size_t ld, int N, double *d, const double *prow,
-                      const double *colE, const DevState *st, int rb, hipStream_t s);
+void sx_launch_enter_partials(const double *d, int L, TilePart *out, const DevState *st, hipStream_t s);
+void sx_launch_ratio_select(double *T, int rows, int row0, size_t ld, int N, const TilePart *enter_parts, int B1,
+                            TilePart *tiles_local, double *colE, DevState *st, int *base, const double *rnew,
+                            bool select, hipStream_t s);
+void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, int N, const TilePart *tiles_all, int B2,
+                          double *prow_out, int *base, DevState *st, hipStream_t s);
+void sx_launch_update(double *T, int rows, int row0, size_t ld, int N, double *d, const double *prow_buf,
+                      const double *colE, const DevState *st, double *rnew, TilePart *enter_parts, UpdateCfg cfg,
+                      hipStream_t s);
+void sx_launch_flush_row(double *T, int rows, int row0, size_t ld, int N, const double *rnew, const DevState *st,
+                         hipStream_t s);
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s);
 
 void sx_launch_coef(const double *d, const int *base, int row0, int rows, double *coef, hipStream_t s);

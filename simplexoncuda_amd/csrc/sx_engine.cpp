@@ -8,6 +8,7 @@
 // stream; the host only polls a pinned status word once per batch of pivots.
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -46,7 +47,8 @@ namespace {
 
 struct Config {
     int verbose = 0;
-    int update_rows = 8;
+    int update_rows = 0;  // 0: auto (by tableau size)
+    int snake = -1;       // -1: auto, 0: off, 1: on
     int batch = 16;
     int device = -1;
     int virtual_ranks = 1;
@@ -88,6 +90,7 @@ struct Shard {
     double *colE = nullptr;
     double *prow = nullptr;
     double *prow_send = nullptr;
+    double *rnew = nullptr;
     double *coef = nullptr;
     double *gemv_local = nullptr;
     double *gemv_all = nullptr;
@@ -181,6 +184,7 @@ class Engine {
         x.colE = dalloc<double>(rows_alloc);
         x.prow = dalloc<double>(ld);
         if (W > 1) x.prow_send = dalloc<double>(ld);
+        x.rnew = dalloc<double>(ld);
         x.coef = dalloc<double>(rows_alloc);
         x.rhs_local = dalloc<double>(rpr);
         if (W > 1) x.rhs_all = dalloc<double>((size_t)W * rpr);
@@ -206,7 +210,7 @@ class Engine {
 
     void free_shard(Shard &x) {
         for (void *p : {(void *)x.T, (void *)x.d, (void *)x.colE, (void *)x.prow, (void *)x.prow_send,
-                        (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
+                        (void *)x.rnew, (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
                         (void *)x.rhs_all, (void *)x.base, (void *)x.enter_parts, (void *)x.tiles_local,
                         (void *)x.tiles_all, (void *)x.st})
             if (p) (void)hipFree(p);
@@ -292,23 +296,46 @@ class Engine {
     }
 
     // ---------------------------------------------------------------- one pivot
+    UpdateCfg update_cfg() const {
+        // measured on MI355X (tools/bench_update.hip): 2 rows per block is best up to ~1 GB
+        // per shard, 1 row above; reversing the sweep every other pivot pays once the shard's
+        // tableau outgrows the 256 MB Infinity Cache.
+        double bytes = 0.0;
+        for (auto &x : sh) bytes = std::max(bytes, 8.0 * (double)x.rows * (double)N);
+        UpdateCfg c;
+        c.rows_per_block = g_cfg.update_rows > 0 ? g_cfg.update_rows : (bytes > 2.0e9 ? 1 : 2);
+        c.snake = g_cfg.snake >= 0 ? g_cfg.snake : (bytes > 256.0 * 1024 * 1024 ? 1 : 0);
+        return c;
+    }
+
+    // pass 1 of the entering argmin for the first pivot of a phase (later pivots get it
+    // from the update kernel)
+    void enqueue_enter_partials() {
+        for (auto &x : sh) sx_launch_enter_partials(x.d, N - 1, x.enter_parts, x.st, s);
+    }
+
     void enqueue_pivot(hipEvent_t ev0, hipEvent_t ev1) {
-        const int L = N - 1;
-        const int B1 = sx_enter_blocks(L);
-        for (auto &x : sh) {
-            sx_launch_enter_partials(x.d, L, x.enter_parts, x.st, s);
-            sx_launch_ratio_partials(x.T, x.rows, x.row0, ld, x.enter_parts, B1, x.tiles_local, x.colE, x.st, s);
-        }
-        if (W > 1) allgather_tiles();
-        const int B2 = W * slots;
+        const int B1 = sx_enter_blocks(N - 1);
+        const UpdateCfg cfg = update_cfg();
         for (auto &x : sh)
-            sx_launch_select_row(x.T, x.rows, x.row0, ld, N, W > 1 ? x.tiles_all : x.tiles_local, B2,
-                                 W > 1 ? x.prow_send : x.prow, W > 1, x.base, x.st, s);
-        if (W > 1) allreduce_prow();
+            sx_launch_ratio_select(x.T, x.rows, x.row0, ld, N, x.enter_parts, B1, x.tiles_local, x.colE, x.st,
+                                   x.base, x.rnew, W == 1, s);
+        if (W > 1) {
+            allgather_tiles();
+            for (auto &x : sh)
+                sx_launch_select_row(x.T, x.rows, x.row0, ld, N, x.tiles_all, W * slots, x.prow_send, x.base, x.st, s);
+            allreduce_prow();
+        }
         if (ev0) SX_HIP(hipEventRecord(ev0, s));
         for (auto &x : sh)
-            sx_launch_update(x.T, x.rows, x.row0, ld, N, x.d, x.prow, x.colE, x.st, g_cfg.update_rows, s);
+            sx_launch_update(x.T, x.rows, x.row0, ld, N, x.d, W > 1 ? x.prow : nullptr, x.colE, x.st, x.rnew,
+                             x.enter_parts, cfg, s);
         if (ev1) SX_HIP(hipEventRecord(ev1, s));
+    }
+
+    // write the last pivot row back into T (it is deferred to the next pivot's first kernel)
+    void flush() {
+        for (auto &x : sh) sx_launch_flush_row(x.T, x.rows, x.row0, ld, N, x.rnew, x.st, s);
     }
 
     void reset_state(long long max_pivots) {
@@ -335,6 +362,7 @@ class Engine {
     int run_phase(int width, long long max_pivots, long long *pivots) {
         N = width;
         reset_state(max_pivots);
+        enqueue_enter_partials();
         const int batch = g_cfg.batch > 0 ? g_cfg.batch : 16;
         long long k = 0;
         for (;; ++k) {
@@ -347,6 +375,7 @@ class Engine {
                 if (st_host[slot ^ 1].status != SX_NOT_ENDED) break;
             }
         }
+        flush();
         DevState f = read_state();
         if (pivots) *pivots = f.pivots;
         return f.status;
@@ -474,7 +503,8 @@ extern "C" {
 
 int simplex_version(void) { return 1; }
 void simplex_set_verbose(int on) { g_cfg.verbose = on; }
-void simplex_set_update_rows(int rb) { g_cfg.update_rows = (rb == 4 || rb == 16) ? rb : 8; }
+void simplex_set_update_rows(int rb) { g_cfg.update_rows = (rb == 1 || rb == 2 || rb == 4 || rb == 8) ? rb : 0; }
+void simplex_set_snake(int mode) { g_cfg.snake = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_batch(int pivots) { g_cfg.batch = pivots > 0 ? pivots : 16; }
 void simplex_set_device(int device) {
     g_cfg.device = device;
@@ -601,6 +631,7 @@ simplex_session *simplex_session_open(problem_t *problem) {
     S->E->update_objective(S->E->N1);
     S->E->N = S->E->N1;
     S->E->reset_state(-1);
+    S->E->enqueue_enter_partials();
     SX_HIP(hipStreamSynchronize(S->E->s));
     return S;
 }

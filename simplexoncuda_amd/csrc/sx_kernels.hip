@@ -112,18 +112,57 @@ __global__ __launch_bounds__(512) void k_argmin_pass2(const TilePart *parts, int
     }
 }
 
+// sc1 (write-through, L1-bypassing) 8-byte accesses for the in-launch tile hand-off
+// (MI355X_MICROARCH.md "Valid forms", first row: sc1 stores + one agent-scope counter add
+// per storing workgroup; the last arriver, told by the add's return value, reads with sc1
+// loads).  No fences needed.
+__device__ __forceinline__ void store_tile_sc1(TilePart *t, double v, int idx, int elig) {
+    unsigned long long *w = reinterpret_cast<unsigned long long *>(t);
+    const unsigned long long lo = __double_as_longlong(v);
+    const unsigned long long hi = (unsigned long long)(unsigned)idx | ((unsigned long long)(unsigned)elig << 32);
+    __hip_atomic_store(w, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(w + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void load_tile_sc1(const TilePart *t, double &v, int &idx, int &elig) {
+    const unsigned long long *w = reinterpret_cast<const unsigned long long *>(t);
+    const unsigned long long lo = __hip_atomic_load(const_cast<unsigned long long *>(w), __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long hi = __hip_atomic_load(const_cast<unsigned long long *>(w + 1), __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+    v = __longlong_as_double(lo);
+    idx = (int)(unsigned)(hi & 0xffffffffull);
+    elig = (int)(unsigned)(hi >> 32);
+}
+
 // ---------------------------------------------------------------------------------------
-// K2: every block re-derives the entering variable from the pass-1 partials (a 512-thread
-// pass 2, cheap), stops the phase if compare(dmin) >= 0 (solver.cu:88), else builds the
-// ratio vector of its 512 rows (createIndicatorsVector, reduction.cu:106-114), saves the
-// pre-update entering column (the reference's rowPivot copy, solver.cu:90-94), and emits
-// the tile winner + "any entry >= eps" (isLessOrEqualThanZero, reduction.cu:186-201).
-__global__ __launch_bounds__(512) void k_ratio_partials(const double *__restrict__ T, int rows, int row0, size_t ld,
-                                                        const TilePart *__restrict__ enter_parts, int B1,
-                                                        TilePart *tiles_local, double *colE, DevState *st) {
+// K2: ratio test (+ row selection on a single shard).  Every block:
+//  1. writes back the previous pivot row (its new values were left in `rnew` by K4, so K4
+//     could read the old row in place without a copy),
+//  2. re-derives the entering variable from the pass-1 partials (a 512-thread pass 2) and
+//     ends the phase if compare(dmin) >= 0 (solver.cu:88),
+//  3. builds the ratio vector of its 512 rows (createIndicatorsVector, reduction.cu:106-114),
+//     saves the pre-update entering column (the reference's rowPivot copy, solver.cu:90-94)
+//     and reduces it to the tile winner + "any entry >= eps" (isLessOrEqualThanZero,
+//     reduction.cu:186-201).
+// With select != 0 the last block to arrive runs the pass-2 tree over the tile winners
+// (minElement(knownTerms, rowPivot), solver.cu:104), declares UNBOUNDED (:96-102) or records
+// the pivot: base[r] = e (:105).  With several shards the tile winners are allgathered
+// first and k_select_row does that step.
+__global__ __launch_bounds__(512) void k_ratio_select(double *__restrict__ T, int rows, int row0, size_t ld, int N,
+                                                      const TilePart *__restrict__ enter_parts, int B1,
+                                                      TilePart *tiles_local, double *colE, DevState *st, int *base,
+                                                      const double *__restrict__ rnew, int select) {
     if (st->status != SX_NOT_ENDED) return;
     const bool leader = blockIdx.x == 0 && threadIdx.x == 0;
-    if (st->max_pivots >= 0 && st->pivots >= st->max_pivots) {
+    const long long piv = st->pivots;
+    const int rp = piv > 0 ? st->r - row0 : -1;  // previous pivot row, local index
+    const bool fix = rp >= 0 && rp < rows;
+    if (fix) {
+        double *dst = T + (size_t)rp * ld;
+        for (int j = blockIdx.x * SX_TILE + threadIdx.x; j < N; j += gridDim.x * SX_TILE) dst[j] = rnew[j];
+    }
+    if (st->max_pivots >= 0 && piv >= st->max_pivots) {
         if (leader) st->status = SX_PIVOT_CAP;
         return;
     }
@@ -154,7 +193,7 @@ __global__ __launch_bounds__(512) void k_ratio_partials(const double *__restrict
     int ri = -1;
     int elig = 0;
     if (li < rows) {
-        const double *row = T + (size_t)li * ld;
+        const double *row = (fix && li == rp) ? rnew : T + (size_t)li * ld;
         const double a = row[1 + e];
         const double b = row[0];
         colE[li] = a;
@@ -167,22 +206,65 @@ __global__ __launch_bounds__(512) void k_ratio_partials(const double *__restrict
     }
     const int any = __syncthreads_or(elig);
     block_argmin512(rv, ri, s_v, s_i);
+    if (!select) {
+        if (threadIdx.x == 0) {
+            tiles_local[blockIdx.x].v = rv;
+            tiles_local[blockIdx.x].idx = ri;
+            tiles_local[blockIdx.x].elig = any;
+        }
+        return;
+    }
+    __shared__ int s_last;
     if (threadIdx.x == 0) {
-        tiles_local[blockIdx.x].v = rv;
-        tiles_local[blockIdx.x].idx = ri;
-        tiles_local[blockIdx.x].elig = any;
+        store_tile_sc1(tiles_local + blockIdx.x, rv, ri, any);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (t == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    const int B2 = gridDim.x;
+    double tv = DBL_MAX;
+    int ti = -1, te = 0;
+    if ((int)threadIdx.x < B2) {
+        double cv;
+        int ci;
+        load_tile_sc1(tiles_local + threadIdx.x, cv, ci, te);
+        if (cmp_eps(cv, tv) < 0) {
+            tv = cv;
+            ti = ci;
+        }
+    }
+    const int anyall = __syncthreads_or(te);
+    if (!anyall) {
+        if (threadIdx.x == 0) {
+            st->ticket = 0;
+            st->status = SX_UNBOUNDED;
+        }
+        return;
+    }
+    block_argmin512(tv, ti, s_v, s_i);
+    if (threadIdx.x == 0) {
+        st->ticket = 0;
+        if (ti < 0) {
+            st->status = SX_NUMERIC_FAIL;
+        } else {
+            base[ti] = e;
+            st->r = ti;
+            st->pivots = piv + 1;
+        }
     }
 }
 
 // ---------------------------------------------------------------------------------------
-// K3: every block re-derives the leaving row from the (gathered) tile winners, checks
-// the unbounded condition, and copies its chunk of the pre-update pivot row (the
-// reference's copyColumn, solver.cu:24-32, is a contiguous row here).  With several
-// shards only the owner contributes the row; the others contribute -0.0, the exact
-// additive identity, so a sum-allreduce reproduces the owner's row bit for bit.
+// K3 (several shards): every block re-derives the leaving row from the allgathered tile
+// winners, checks the unbounded condition, records the pivot, and copies its chunk of the
+// pre-update pivot row (the reference's copyColumn, solver.cu:24-32, is a contiguous row
+// here).  Only the owner contributes the row; the others contribute -0.0, the exact
+// additive identity, so the sum-allreduce reproduces the owner's row bit for bit.
 __global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T, int rows, int row0, size_t ld,
                                                     int N, const TilePart *__restrict__ tiles_all, int B2,
-                                                    double *prow_out, int multi, int *base, DevState *st) {
+                                                    double *prow_out, int *base, DevState *st) {
     if (st->status != SX_NOT_ENDED) return;
     const bool leader = blockIdx.x == 0 && threadIdx.x == 0;
     __shared__ double s_v[16];
@@ -206,7 +288,7 @@ __global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T
     const bool own = r >= row0 && r < row0 + rows;
     const double *src = T + (size_t)(own ? r - row0 : 0) * ld;
     for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < N; j += gridDim.x * blockDim.x)
-        prow_out[j] = own ? src[j] : (multi ? -0.0 : 0.0);
+        prow_out[j] = own ? src[j] : -0.0;
     if (leader) {
         base[r] = st->e;  // solver.cu:105
         st->r = r;
@@ -216,81 +298,151 @@ __global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T
 
 // ---------------------------------------------------------------------------------------
 // K4: the rank-1 pivot update (updateContraintsMatrix + updateCostsVector, solver.cu:34-56)
-//   row r:       T[r][j] = prow[j] / p
-//   other rows:  T[i][j] = fma(-(a_ie / p), prow[j], T[i][j])   (factor hoisted per row:
+//   row r:       rnew[j]  = prow[j] / p          (written back to T[r] by the next kernel)
+//   other rows:  T[i][j]  = fma(-(a_ie / p), prow[j], T[i][j])   (factor hoisted per row:
 //                the reference recomputes the same division per element, bit-identical)
-//   objective:   d[j]    = fma(-(d_e / p),  prow[j], d[j])
-// prow and colE are pre-update copies, so the kernel reads only them and its own
-// element: no ordering between workgroups.  Each thread owns 2 adjacent columns (one
-// 16-byte load/store per row), a block covers 512 columns x RB rows; the RB loads of a
-// thread are issued before any use to keep 16 B x RB in flight per lane.
-template <int RB>
+//   objective:   d[j]     = fma(-(d_e / p),  prow[j], d[j])
+// prow is the pre-update pivot row: read in place from T[r] on one shard (no block writes
+// T[r] during the launch), or the allreduced copy on several.  A thread owns 2 adjacent
+// columns (one 16-byte load/store per row); a block covers 512 columns x RB rows.  With
+// SNAKE the tile order is reversed on every other pivot, so the next sweep starts on the
+// lines the previous one wrote last -- still resident in the 256 MB Infinity Cache.
+// The last row of blocks updates d and emits the 512-tile winners of the NEXT pivot's
+// entering argmin (pass 1 of minElement(costs+1), reduction.cu:51-80).
+template <int RB, bool SNAKE>
 __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows, int row0, size_t ld, int N,
-                                                double *__restrict__ d, const double *__restrict__ prow,
-                                                const double *__restrict__ colE, const DevState *st) {
+                                                double *__restrict__ d, const double *__restrict__ prow_buf,
+                                                const double *__restrict__ colE, const DevState *st,
+                                                double *__restrict__ rnew, TilePart *enter_parts) {
     if (st->status != SX_NOT_ENDED) return;
     const int e = st->e;
-    const int r = st->r - row0;
+    const int rl = st->r - row0;
+    const double *prow = prow_buf ? prow_buf : T + (size_t)rl * ld;
     const double p = prow[1 + e];
+    const int rg = gridDim.y - 1;  // row groups of T; the last grid row handles d
+    if ((int)blockIdx.y == rg) {
+        // ---- objective row + next entering-argmin pass 1 (512 reference threads on 256)
+        __shared__ double s_v[16];
+        __shared__ int s_i[16];
+        const int L = N - 1;
+        if ((int)blockIdx.x * SX_TILE >= L) return;
+        const double fd = -st->dmin / p;
+        if (blockIdx.x == 0 && threadIdx.x == 0) d[0] = fma(fd, prow[0], d[0]);
+        double v0 = DBL_MAX, v1 = DBL_MAX;
+        int i0 = -1, i1 = -1;
+        const int ia = blockIdx.x * SX_TILE + threadIdx.x, ib = ia + 256;
+        if (ia < L) {
+            const double x = fma(fd, prow[1 + ia], d[1 + ia]);
+            d[1 + ia] = x;
+            if (cmp_eps(x, v0) < 0) {
+                v0 = x;
+                i0 = ia;
+            }
+        }
+        if (ib < L) {
+            const double x = fma(fd, prow[1 + ib], d[1 + ib]);
+            d[1 + ib] = x;
+            if (cmp_eps(x, v1) < 0) {
+                v1 = x;
+                i1 = ib;
+            }
+        }
+        half_argmin(v0, i0);  // reference warps 0..7
+        half_argmin(v1, i1);  // reference warps 8..15
+        const int lane = threadIdx.x & 31, h = threadIdx.x >> 5;
+        if (lane == 0) {
+            s_v[h] = v0;
+            s_i[h] = i0;
+            s_v[h + 8] = v1;
+            s_i[h + 8] = i1;
+        }
+        __syncthreads();
+        if (threadIdx.x < 32) {
+            double v = (threadIdx.x < 16) ? s_v[threadIdx.x] : DBL_MAX;
+            int i = (threadIdx.x < 16) ? s_i[threadIdx.x] : -1;
+            half_argmin(v, i);
+            if (threadIdx.x == 0) {
+                enter_parts[blockIdx.x].v = v;
+                enter_parts[blockIdx.x].idx = i;
+                enter_parts[blockIdx.x].elig = 0;
+            }
+        }
+        return;
+    }
+    int bx = blockIdx.x, by = blockIdx.y;
+    if (SNAKE && (st->pivots & 1)) {
+        bx = gridDim.x - 1 - bx;
+        by = rg - 1 - by;
+    }
     __shared__ double s_f[RB];
-    const int i0 = blockIdx.y * RB;
+    const int i0 = by * RB;
     if ((int)threadIdx.x < RB) {
         const int i = i0 + threadIdx.x;
         s_f[threadIdx.x] = (i < rows) ? -colE[i] / p : 0.0;
     }
     __syncthreads();
-    const int j = (blockIdx.x * 256 + threadIdx.x) * 2;
+    const int j = (bx * 256 + threadIdx.x) * 2;
     if (j >= N) return;
     const int nrow = rows - i0 < RB ? rows - i0 : RB;
     if (j + 1 < N) {
         const double2 pr = *reinterpret_cast<const double2 *>(prow + j);
-        if (blockIdx.y == 0) {
-            const double fd = -st->dmin / p;
-            double2 x = *reinterpret_cast<double2 *>(d + j);
-            x.x = fma(fd, pr.x, x.x);
-            x.y = fma(fd, pr.y, x.y);
-            *reinterpret_cast<double2 *>(d + j) = x;
-        }
         double *base = T + (size_t)i0 * ld + j;
         if (nrow == RB) {
             double2 x[RB];
 #pragma unroll
-            for (int k = 0; k < RB; ++k) x[k] = *reinterpret_cast<const double2 *>(base + (size_t)k * ld);
+            for (int k = 0; k < RB; ++k)
+                if (i0 + k != rl) x[k] = *reinterpret_cast<const double2 *>(base + (size_t)k * ld);
 #pragma unroll
             for (int k = 0; k < RB; ++k) {
-                if (i0 + k == r) {
-                    x[k].x = pr.x / p;
-                    x[k].y = pr.y / p;
+                if (i0 + k == rl) {
+                    double2 y;
+                    y.x = pr.x / p;
+                    y.y = pr.y / p;
+                    *reinterpret_cast<double2 *>(rnew + j) = y;
                 } else {
                     const double f = s_f[k];
                     x[k].x = fma(f, pr.x, x[k].x);
                     x[k].y = fma(f, pr.y, x[k].y);
+                    *reinterpret_cast<double2 *>(base + (size_t)k * ld) = x[k];
                 }
-                *reinterpret_cast<double2 *>(base + (size_t)k * ld) = x[k];
             }
         } else {
             for (int k = 0; k < nrow; ++k) {
-                double2 x = *reinterpret_cast<const double2 *>(base + (size_t)k * ld);
-                if (i0 + k == r) {
-                    x.x = pr.x / p;
-                    x.y = pr.y / p;
+                if (i0 + k == rl) {
+                    double2 y;
+                    y.x = pr.x / p;
+                    y.y = pr.y / p;
+                    *reinterpret_cast<double2 *>(rnew + j) = y;
                 } else {
+                    double2 x = *reinterpret_cast<const double2 *>(base + (size_t)k * ld);
                     const double f = s_f[k];
                     x.x = fma(f, pr.x, x.x);
                     x.y = fma(f, pr.y, x.y);
+                    *reinterpret_cast<double2 *>(base + (size_t)k * ld) = x;
                 }
-                *reinterpret_cast<double2 *>(base + (size_t)k * ld) = x;
             }
         }
     } else {
         // last (odd) column of the phase width: scalar path
         const double pr = prow[j];
-        if (blockIdx.y == 0) d[j] = fma(-st->dmin / p, pr, d[j]);
         for (int k = 0; k < nrow; ++k) {
-            double *x = T + (size_t)(i0 + k) * ld + j;
-            *x = (i0 + k == r) ? pr / p : fma(s_f[k], pr, *x);
+            if (i0 + k == rl) {
+                rnew[j] = pr / p;
+            } else {
+                double *x = T + (size_t)(i0 + k) * ld + j;
+                *x = fma(s_f[k], pr, *x);
+            }
         }
     }
+}
+
+// Phase end: write the last pivot row back from rnew (idempotent).
+__global__ void k_flush_row(double *T, int rows, int row0, size_t ld, int N, const double *rnew, const DevState *st) {
+    if (st->pivots <= 0) return;
+    const int rl = st->r - row0;
+    if (rl < 0 || rl >= rows) return;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < N; j += gridDim.x * blockDim.x)
+        T[(size_t)rl * ld + j] = rnew[j];
 }
 
 // Virtual-rank "allreduce": out = sum of the shards' contributions in rank order.  Exact,
@@ -421,43 +573,58 @@ void sx_launch_enter_partials(const double *d, int L, TilePart *out, const DevSt
     k_argmin_pass1<<<g, SX_TILE, 0, s>>>(d + 1, L, out, st);
 }
 
-void sx_launch_ratio_partials(const double *T, int rows, int row0, size_t ld, const TilePart *enter_parts, int B1,
-                              TilePart *tiles_local, double *colE, DevState *st, hipStream_t s) {
+void sx_launch_ratio_select(double *T, int rows, int row0, size_t ld, int N, const TilePart *enter_parts, int B1,
+                            TilePart *tiles_local, double *colE, DevState *st, int *base, const double *rnew,
+                            bool select, hipStream_t s) {
     int g = (rows + SX_TILE - 1) / SX_TILE;
     if (g < 1) g = 1;  // a shard without rows still decides optimality for its own state
-    k_ratio_partials<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, enter_parts, B1, tiles_local, colE, st);
+    if (select && g > SX_TILE) SX_FATAL("too many ratio tiles for the 512-thread pass 2");
+    k_ratio_select<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, N, enter_parts, B1, tiles_local, colE, st, base, rnew,
+                                         select ? 1 : 0);
 }
 
 void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, int N, const TilePart *tiles_all, int B2,
-                          double *prow_out, bool multi, int *base, DevState *st, hipStream_t s) {
+                          double *prow_out, int *base, DevState *st, hipStream_t s) {
     if (B2 > SX_TILE) SX_FATAL("too many ratio tiles for the 512-thread pass 2");
     int g = (N + 4 * SX_TILE - 1) / (4 * SX_TILE);
     if (g < 1) g = 1;
     if (g > 64) g = 64;
-    k_select_row<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, N, tiles_all, B2, prow_out, multi ? 1 : 0, base, st);
+    k_select_row<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, N, tiles_all, B2, prow_out, base, st);
 }
 
-void sx_launch_update(double *T, int rows, int row0, size_t ld, int N, double *d, const double *prow,
-                      const double *colE, const DevState *st, int rb, hipStream_t s) {
+template <int RB>
+static void launch_update_rb(dim3 grid, bool snake, double *T, int rows, int row0, size_t ld, int N, double *d,
+                             const double *prow_buf, const double *colE, const DevState *st, double *rnew,
+                             TilePart *enter_parts, hipStream_t s) {
+    if (snake)
+        k_update<RB, true><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, enter_parts);
+    else
+        k_update<RB, false><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, enter_parts);
+}
+
+void sx_launch_update(double *T, int rows, int row0, size_t ld, int N, double *d, const double *prow_buf,
+                      const double *colE, const DevState *st, double *rnew, TilePart *enter_parts, UpdateCfg cfg,
+                      hipStream_t s) {
     const int cols_blocks = (N + 511) / 512;
-    if (rows < 1) rows = 0;  // grid keeps one row-block so the objective row is updated
+    if (sx_enter_blocks(N - 1) > cols_blocks) SX_FATAL("update grid too narrow for the entering partials");
+    const int rb = cfg.rows_per_block;
+    const int rg = rows > 0 ? (rows + rb - 1) / rb : 0;
+    dim3 grid(cols_blocks, rg + 1);
+    const bool sn = cfg.snake != 0;
     switch (rb) {
-    case 4: {
-        dim3 grid(cols_blocks, rows > 0 ? (rows + 3) / 4 : 1);
-        k_update<4><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow, colE, st);
-        break;
+    case 1: launch_update_rb<1>(grid, sn, T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, enter_parts, s); break;
+    case 2: launch_update_rb<2>(grid, sn, T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, enter_parts, s); break;
+    case 4: launch_update_rb<4>(grid, sn, T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, enter_parts, s); break;
+    default: launch_update_rb<8>(grid, sn, T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, enter_parts, s); break;
     }
-    case 16: {
-        dim3 grid(cols_blocks, rows > 0 ? (rows + 15) / 16 : 1);
-        k_update<16><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow, colE, st);
-        break;
-    }
-    default: {
-        dim3 grid(cols_blocks, rows > 0 ? (rows + 7) / 8 : 1);
-        k_update<8><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow, colE, st);
-        break;
-    }
-    }
+}
+
+void sx_launch_flush_row(double *T, int rows, int row0, size_t ld, int N, const double *rnew, const DevState *st,
+                         hipStream_t s) {
+    if (rows <= 0) return;
+    int g = (N + 255) / 256;
+    if (g > 256) g = 256;
+    k_flush_row<<<g, 256, 0, s>>>(T, rows, row0, ld, N, rnew, st);
 }
 
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s) {
