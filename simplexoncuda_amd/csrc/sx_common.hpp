@@ -32,14 +32,19 @@ struct __attribute__((aligned(16))) TilePart {
 // batch of pivots).
 struct __attribute__((aligned(16))) DevState {
     int status;            // SX_NOT_ENDED while the phase runs
-    int e;                 // entering variable (0-based variable index; column e+1)
-    int r;                 // leaving constraint row (global index) of the last pivot; its
-                           // new values sit in `rnew` until the next kernel writes them back
-    unsigned ticket;       // arrival counter of the ratio/select hand-off (zero between launches)
+    int e;                 // entering variable of the current pivot (column e+1)
+    int r;                 // leaving row (global) of the current pivot; after the update its
+                           // new values sit in rnew[pivots & 1] until the next update writes
+                           // them back (the row is read in place as the pivot row meanwhile)
+    int r_prev;            // leaving row of the previous pivot
     double dmin;           // reduced cost of the entering variable (d[e+1] before update)
     long long pivots;      // pivots applied in this phase
     long long max_pivots;  // < 0: no cap (reference behaviour)
-    long long pad1;
+    int e_next;            // entering argmin of the updated objective row (next pivot)
+    unsigned ticket;       // arrival counter of the ratio/select hand-off (zero between launches)
+    double dmin_next;      // its value
+    unsigned ticket_d;     // arrival counter of the objective-row blocks of the update
+    int pad0;
 };
 
 // Error convention of the reference (error.cu:5-12): print "<msg> in <file> at line <n>"
@@ -56,17 +61,18 @@ struct UpdateCfg {
 };
 
 int sx_enter_blocks(int L);
-void sx_launch_enter_partials(const double *d, int L, TilePart *out, const DevState *st, hipStream_t s);
-void sx_launch_ratio_select(double *T, int rows, int row0, size_t ld, int N, const TilePart *enter_parts, int B1,
-                            TilePart *tiles_local, double *colE, DevState *st, int *base, const double *rnew,
-                            bool select, hipStream_t s);
+void sx_launch_enter(const double *d, int L, TilePart *parts, DevState *st, hipStream_t s);
+void sx_launch_ratio_select(const double *T, int rows, int row0, size_t ld, TilePart *tiles_local, double *colE,
+                            DevState *st, int *base, const double *rnew, size_t rnew_stride, bool select,
+                            hipStream_t s);
 void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, int N, const TilePart *tiles_all, int B2,
-                          double *prow_out, int *base, DevState *st, hipStream_t s);
+                          double *prow_out, int *base, DevState *st, const double *rnew, size_t rnew_stride,
+                          hipStream_t s);
 void sx_launch_update(double *T, int rows, int row0, size_t ld, int N, double *d, const double *prow_buf,
-                      const double *colE, const DevState *st, double *rnew, TilePart *enter_parts, UpdateCfg cfg,
-                      hipStream_t s);
-void sx_launch_flush_row(double *T, int rows, int row0, size_t ld, int N, const double *rnew, const DevState *st,
-                         hipStream_t s);
+                      const double *colE, DevState *st, double *rnew, size_t rnew_stride, TilePart *enter_parts,
+                      UpdateCfg cfg, hipStream_t s);
+void sx_launch_flush_row(double *T, int rows, int row0, size_t ld, int N, const double *rnew, size_t rnew_stride,
+                         const DevState *st, hipStream_t s);
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s);
 
 void sx_launch_coef(const double *d, const int *base, int row0, int rows, double *coef, hipStream_t s);

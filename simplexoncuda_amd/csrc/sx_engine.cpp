@@ -184,7 +184,7 @@ class Engine {
         x.colE = dalloc<double>(rows_alloc);
         x.prow = dalloc<double>(ld);
         if (W > 1) x.prow_send = dalloc<double>(ld);
-        x.rnew = dalloc<double>(ld);
+        x.rnew = dalloc<double>(2 * ld);
         x.coef = dalloc<double>(rows_alloc);
         x.rhs_local = dalloc<double>(rpr);
         if (W > 1) x.rhs_all = dalloc<double>((size_t)W * rpr);
@@ -311,31 +311,30 @@ class Engine {
     // pass 1 of the entering argmin for the first pivot of a phase (later pivots get it
     // from the update kernel)
     void enqueue_enter_partials() {
-        for (auto &x : sh) sx_launch_enter_partials(x.d, N - 1, x.enter_parts, x.st, s);
+        for (auto &x : sh) sx_launch_enter(x.d, N - 1, x.enter_parts, x.st, s);
     }
 
     void enqueue_pivot(hipEvent_t ev0, hipEvent_t ev1) {
-        const int B1 = sx_enter_blocks(N - 1);
         const UpdateCfg cfg = update_cfg();
         for (auto &x : sh)
-            sx_launch_ratio_select(x.T, x.rows, x.row0, ld, N, x.enter_parts, B1, x.tiles_local, x.colE, x.st,
-                                   x.base, x.rnew, W == 1, s);
+            sx_launch_ratio_select(x.T, x.rows, x.row0, ld, x.tiles_local, x.colE, x.st, x.base, x.rnew, ld, W == 1, s);
         if (W > 1) {
             allgather_tiles();
             for (auto &x : sh)
-                sx_launch_select_row(x.T, x.rows, x.row0, ld, N, x.tiles_all, W * slots, x.prow_send, x.base, x.st, s);
+                sx_launch_select_row(x.T, x.rows, x.row0, ld, N, x.tiles_all, W * slots, x.prow_send, x.base, x.st,
+                                     x.rnew, ld, s);
             allreduce_prow();
         }
         if (ev0) SX_HIP(hipEventRecord(ev0, s));
         for (auto &x : sh)
-            sx_launch_update(x.T, x.rows, x.row0, ld, N, x.d, W > 1 ? x.prow : nullptr, x.colE, x.st, x.rnew,
+            sx_launch_update(x.T, x.rows, x.row0, ld, N, x.d, W > 1 ? x.prow : nullptr, x.colE, x.st, x.rnew, ld,
                              x.enter_parts, cfg, s);
         if (ev1) SX_HIP(hipEventRecord(ev1, s));
     }
 
-    // write the last pivot row back into T (it is deferred to the next pivot's first kernel)
+    // write the last pivot row back into T (it is deferred to the next pivot's update)
     void flush() {
-        for (auto &x : sh) sx_launch_flush_row(x.T, x.rows, x.row0, ld, N, x.rnew, x.st, s);
+        for (auto &x : sh) sx_launch_flush_row(x.T, x.rows, x.row0, ld, N, x.rnew, ld, x.st, s);
     }
 
     void reset_state(long long max_pivots) {
@@ -344,6 +343,8 @@ class Engine {
         init.status = SX_NOT_ENDED;
         init.e = -1;
         init.r = -1;
+        init.r_prev = -1;
+        init.e_next = -1;
         init.max_pivots = max_pivots;
         for (auto &x : sh) SX_HIP(hipMemcpyAsync(x.st, &init, sizeof(init), hipMemcpyHostToDevice, s));
         SX_HIP(hipStreamSynchronize(s));

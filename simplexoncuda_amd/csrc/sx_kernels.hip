@@ -135,51 +135,52 @@ __device__ __forceinline__ void load_tile_sc1(const TilePart *t, double &v, int 
     elig = (int)(unsigned)(hi >> 32);
 }
 
+// Pass 2 of the entering argmin at the start of a phase (later pivots get it from the
+// update kernel): (e_next, dmin_next) from the pass-1 partials.
+__global__ __launch_bounds__(512) void k_enter_finish(const TilePart *parts, int B1, DevState *st) {
+    __shared__ double s_v[16];
+    __shared__ int s_i[16];
+    double v;
+    int i;
+    stage2_512(parts, B1, v, i, s_v, s_i);
+    if (threadIdx.x == 0) {
+        st->e_next = i;
+        st->dmin_next = v;
+    }
+}
+
+// The leaving row of the previous pivot is not yet written back to T: its current values
+// are rnew[pivots & 1].  Source row i of a shard for the pivot being selected:
+__device__ __forceinline__ const double *row_src(const double *T, size_t ld, int li, int pend,
+                                                 const double *rnew_cur) {
+    return li == pend ? rnew_cur : T + (size_t)li * ld;
+}
+
 // ---------------------------------------------------------------------------------------
-// K2: ratio test (+ row selection on a single shard).  Every block:
-//  1. writes back the previous pivot row (its new values were left in `rnew` by K4, so K4
-//     could read the old row in place without a copy),
-//  2. re-derives the entering variable from the pass-1 partials (a 512-thread pass 2) and
-//     ends the phase if compare(dmin) >= 0 (solver.cu:88),
-//  3. builds the ratio vector of its 512 rows (createIndicatorsVector, reduction.cu:106-114),
-//     saves the pre-update entering column (the reference's rowPivot copy, solver.cu:90-94)
-//     and reduces it to the tile winner + "any entry >= eps" (isLessOrEqualThanZero,
-//     reduction.cu:186-201).
+// K2: ratio test (+ row selection on a single shard).  The entering variable and its
+// reduced cost were produced by the previous update (or k_enter_finish).  Every block:
+//  - ends the phase if compare(dmin) >= 0 (solver.cu:88),
+//  - builds the ratio vector of its 512 rows (createIndicatorsVector, reduction.cu:106-114),
+//    saves the pre-update entering column (the reference's rowPivot copy, solver.cu:90-94)
+//    and reduces it to the tile winner + "any entry >= eps" (isLessOrEqualThanZero,
+//    reduction.cu:186-201).
 // With select != 0 the last block to arrive runs the pass-2 tree over the tile winners
 // (minElement(knownTerms, rowPivot), solver.cu:104), declares UNBOUNDED (:96-102) or records
 // the pivot: base[r] = e (:105).  With several shards the tile winners are allgathered
 // first and k_select_row does that step.
-__global__ __launch_bounds__(512) void k_ratio_select(double *__restrict__ T, int rows, int row0, size_t ld, int N,
-                                                      const TilePart *__restrict__ enter_parts, int B1,
+__global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__ T, int rows, int row0, size_t ld,
                                                       TilePart *tiles_local, double *colE, DevState *st, int *base,
-                                                      const double *__restrict__ rnew, int select) {
+                                                      const double *__restrict__ rnew, size_t rnew_stride,
+                                                      int select) {
     if (st->status != SX_NOT_ENDED) return;
     const bool leader = blockIdx.x == 0 && threadIdx.x == 0;
     const long long piv = st->pivots;
-    const int rp = piv > 0 ? st->r - row0 : -1;  // previous pivot row, local index
-    const bool fix = rp >= 0 && rp < rows;
-    if (fix) {
-        double *dst = T + (size_t)rp * ld;
-        for (int j = blockIdx.x * SX_TILE + threadIdx.x; j < N; j += gridDim.x * SX_TILE) dst[j] = rnew[j];
-    }
     if (st->max_pivots >= 0 && piv >= st->max_pivots) {
         if (leader) st->status = SX_PIVOT_CAP;
         return;
     }
-    __shared__ double s_v[16];
-    __shared__ int s_i[16];
-    __shared__ double s_bv;
-    __shared__ int s_bi;
-    double v;
-    int e;
-    stage2_512(enter_parts, B1, v, e, s_v, s_i);
-    if (threadIdx.x == 0) {
-        s_bv = v;
-        s_bi = e;
-    }
-    __syncthreads();
-    v = s_bv;
-    e = s_bi;
+    const double v = st->dmin_next;
+    const int e = st->e_next;
     if (!(cmp_eps(v, 0.0) < 0)) {
         if (leader) st->status = SX_FEASIBLE;
         return;
@@ -188,12 +189,16 @@ __global__ __launch_bounds__(512) void k_ratio_select(double *__restrict__ T, in
         st->e = e;
         st->dmin = v;
     }
+    const int pend = piv > 0 ? st->r - row0 : -1;
+    const double *rcur = rnew + (size_t)(piv & 1) * rnew_stride;
+    __shared__ double s_v[16];
+    __shared__ int s_i[16];
     const int li = blockIdx.x * SX_TILE + threadIdx.x;
     double rv = DBL_MAX;
     int ri = -1;
     int elig = 0;
     if (li < rows) {
-        const double *row = (fix && li == rp) ? rnew : T + (size_t)li * ld;
+        const double *row = row_src(T, ld, li, pend, rcur);
         const double a = row[1 + e];
         const double b = row[0];
         colE[li] = a;
@@ -250,6 +255,7 @@ __global__ __launch_bounds__(512) void k_ratio_select(double *__restrict__ T, in
             st->status = SX_NUMERIC_FAIL;
         } else {
             base[ti] = e;
+            st->r_prev = st->r;
             st->r = ti;
             st->pivots = piv + 1;
         }
@@ -264,7 +270,8 @@ __global__ __launch_bounds__(512) void k_ratio_select(double *__restrict__ T, in
 // additive identity, so the sum-allreduce reproduces the owner's row bit for bit.
 __global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T, int rows, int row0, size_t ld,
                                                     int N, const TilePart *__restrict__ tiles_all, int B2,
-                                                    double *prow_out, int *base, DevState *st) {
+                                                    double *prow_out, int *base, DevState *st,
+                                                    const double *__restrict__ rnew, size_t rnew_stride) {
     if (st->status != SX_NOT_ENDED) return;
     const bool leader = blockIdx.x == 0 && threadIdx.x == 0;
     __shared__ double s_v[16];
@@ -285,47 +292,65 @@ __global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T
         if (leader) st->status = SX_NUMERIC_FAIL;
         return;
     }
+    const long long piv = st->pivots;
+    const int pend = piv > 0 ? st->r - row0 : -1;
     const bool own = r >= row0 && r < row0 + rows;
-    const double *src = T + (size_t)(own ? r - row0 : 0) * ld;
+    const double *src = own ? row_src(T, ld, r - row0, pend, rnew + (size_t)(piv & 1) * rnew_stride) : T;
     for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < N; j += gridDim.x * blockDim.x)
         prow_out[j] = own ? src[j] : -0.0;
-    if (leader) {
-        base[r] = st->e;  // solver.cu:105
-        st->r = r;
-        st->pivots += 1;
+    // commit the pivot once every block has read the state above: the last block to
+    // arrive does it (the next kernel sees it after the launch boundary)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned t = __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == gridDim.x - 1) {
+            st->ticket = 0;
+            base[r] = st->e;  // solver.cu:105
+            st->r_prev = st->r;
+            st->r = r;
+            st->pivots = piv + 1;
+        }
     }
 }
 
 // ---------------------------------------------------------------------------------------
 // K4: the rank-1 pivot update (updateContraintsMatrix + updateCostsVector, solver.cu:34-56)
-//   row r:       rnew[j]  = prow[j] / p          (written back to T[r] by the next kernel)
-//   other rows:  T[i][j]  = fma(-(a_ie / p), prow[j], T[i][j])   (factor hoisted per row:
+//   row r:       rnew[q&1][j] = prow[j] / p     (q = pivot number; written back to T by the
+//                                                next update, which reads it as row r_prev)
+//   other rows:  T[i][j] = fma(-(a_ie / p), prow[j], T[i][j])   (factor hoisted per row:
 //                the reference recomputes the same division per element, bit-identical)
-//   objective:   d[j]     = fma(-(d_e / p),  prow[j], d[j])
-// prow is the pre-update pivot row: read in place from T[r] on one shard (no block writes
-// T[r] during the launch), or the allreduced copy on several.  A thread owns 2 adjacent
-// columns (one 16-byte load/store per row); a block covers 512 columns x RB rows.  With
-// SNAKE the tile order is reversed on every other pivot, so the next sweep starts on the
-// lines the previous one wrote last -- still resident in the 256 MB Infinity Cache.
-// The last row of blocks updates d and emits the 512-tile winners of the NEXT pivot's
-// entering argmin (pass 1 of minElement(costs+1), reduction.cu:51-80).
+//   objective:   d[j]    = fma(-(d_e / p),  prow[j], d[j])
+// prow is the pre-update pivot row, read in place on one shard (nothing writes row r
+// during the launch) or the allreduced copy on several.  Grid row 0 (dispatched first)
+// updates d and finishes the NEXT pivot's entering argmin: pass 1 per 512-tile
+// (reduction.cu:51-80), then the last block to arrive runs pass 2 and stores
+// (e_next, dmin_next).  Grid rows >= 1: a thread owns 2 adjacent columns (one 16-byte
+// load/store per row), a block covers 512 columns x RB rows.  With SNAKE the tile order
+// is reversed on every other pivot, so a sweep starts on the lines the previous one wrote
+// last -- still resident in the 256 MB Infinity Cache.
 template <int RB, bool SNAKE>
 __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows, int row0, size_t ld, int N,
                                                 double *__restrict__ d, const double *__restrict__ prow_buf,
-                                                const double *__restrict__ colE, const DevState *st,
-                                                double *__restrict__ rnew, TilePart *enter_parts) {
+                                                const double *__restrict__ colE, DevState *st,
+                                                double *__restrict__ rnew, size_t rnew_stride,
+                                                TilePart *enter_parts) {
     if (st->status != SX_NOT_ENDED) return;
+    const long long q = st->pivots;
     const int e = st->e;
     const int rl = st->r - row0;
-    const double *prow = prow_buf ? prow_buf : T + (size_t)rl * ld;
+    const int pl = (q >= 2 && st->r_prev != st->r) ? st->r_prev - row0 : -1;  // pending row, local
+    const double *rprev = rnew + (size_t)((q - 1) & 1) * rnew_stride;
+    double *rout = rnew + (size_t)(q & 1) * rnew_stride;
+    const double *prow = prow_buf ? prow_buf : ((q >= 2 && st->r_prev == st->r) ? rprev : T + (size_t)rl * ld);
     const double p = prow[1 + e];
-    const int rg = gridDim.y - 1;  // row groups of T; the last grid row handles d
-    if ((int)blockIdx.y == rg) {
-        // ---- objective row + next entering-argmin pass 1 (512 reference threads on 256)
+    if (blockIdx.y == 0) {
+        // ---- objective row + next entering argmin (512 reference threads on 256)
         __shared__ double s_v[16];
         __shared__ int s_i[16];
+        __shared__ int s_last;
         const int L = N - 1;
-        if ((int)blockIdx.x * SX_TILE >= L) return;
+        const int B1 = (L + SX_TILE - 1) / SX_TILE;
+        if ((int)blockIdx.x >= B1) return;
         const double fd = -st->dmin / p;
         if (blockIdx.x == 0 && threadIdx.x == 0) d[0] = fma(fd, prow[0], d[0]);
         double v0 = DBL_MAX, v1 = DBL_MAX;
@@ -362,15 +387,49 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows
             int i = (threadIdx.x < 16) ? s_i[threadIdx.x] : -1;
             half_argmin(v, i);
             if (threadIdx.x == 0) {
-                enter_parts[blockIdx.x].v = v;
-                enter_parts[blockIdx.x].idx = i;
-                enter_parts[blockIdx.x].elig = 0;
+                store_tile_sc1(enter_parts + blockIdx.x, v, i, 0);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const unsigned t = __hip_atomic_fetch_add(&st->ticket_d, 1u, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                s_last = (t == (unsigned)B1 - 1);
+            }
+        }
+        __syncthreads();
+        if (!s_last) return;
+        // last objective block: pass 2 (reference pass-2 tree; B1 <= 256 here)
+        double v = DBL_MAX;
+        int i = -1;
+        if ((int)threadIdx.x < B1) {
+            double cv;
+            int ci, ce;
+            load_tile_sc1(enter_parts + threadIdx.x, cv, ci, ce);
+            if (cmp_eps(cv, v) < 0) {
+                v = cv;
+                i = ci;
+            }
+        }
+        half_argmin(v, i);
+        __syncthreads();
+        if (lane == 0) {
+            s_v[h] = v;
+            s_i[h] = i;
+        }
+        __syncthreads();
+        if (threadIdx.x < 32) {
+            v = (threadIdx.x < 8) ? s_v[threadIdx.x] : DBL_MAX;
+            i = (threadIdx.x < 8) ? s_i[threadIdx.x] : -1;
+            half_argmin(v, i);
+            if (threadIdx.x == 0) {
+                st->e_next = i;
+                st->dmin_next = v;
+                st->ticket_d = 0;
             }
         }
         return;
     }
-    int bx = blockIdx.x, by = blockIdx.y;
-    if (SNAKE && (st->pivots & 1)) {
+    const int rg = gridDim.y - 1;  // row groups of T
+    int bx = blockIdx.x, by = blockIdx.y - 1;
+    if (SNAKE && (q & 1)) {
         bx = gridDim.x - 1 - bx;
         by = rg - 1 - by;
     }
@@ -391,14 +450,15 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows
             double2 x[RB];
 #pragma unroll
             for (int k = 0; k < RB; ++k)
-                if (i0 + k != rl) x[k] = *reinterpret_cast<const double2 *>(base + (size_t)k * ld);
+                if (i0 + k != rl)
+                    x[k] = *reinterpret_cast<const double2 *>(i0 + k == pl ? rprev + j : base + (size_t)k * ld);
 #pragma unroll
             for (int k = 0; k < RB; ++k) {
                 if (i0 + k == rl) {
                     double2 y;
                     y.x = pr.x / p;
                     y.y = pr.y / p;
-                    *reinterpret_cast<double2 *>(rnew + j) = y;
+                    *reinterpret_cast<double2 *>(rout + j) = y;
                 } else {
                     const double f = s_f[k];
                     x[k].x = fma(f, pr.x, x[k].x);
@@ -412,9 +472,9 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows
                     double2 y;
                     y.x = pr.x / p;
                     y.y = pr.y / p;
-                    *reinterpret_cast<double2 *>(rnew + j) = y;
+                    *reinterpret_cast<double2 *>(rout + j) = y;
                 } else {
-                    double2 x = *reinterpret_cast<const double2 *>(base + (size_t)k * ld);
+                    double2 x = *reinterpret_cast<const double2 *>(i0 + k == pl ? rprev + j : base + (size_t)k * ld);
                     const double f = s_f[k];
                     x.x = fma(f, pr.x, x.x);
                     x.y = fma(f, pr.y, x.y);
@@ -427,22 +487,26 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows
         const double pr = prow[j];
         for (int k = 0; k < nrow; ++k) {
             if (i0 + k == rl) {
-                rnew[j] = pr / p;
+                rout[j] = pr / p;
             } else {
                 double *x = T + (size_t)(i0 + k) * ld + j;
-                *x = fma(s_f[k], pr, *x);
+                const double old = (i0 + k == pl) ? rprev[j] : *x;
+                *x = fma(s_f[k], pr, old);
             }
         }
     }
 }
 
-// Phase end: write the last pivot row back from rnew (idempotent).
-__global__ void k_flush_row(double *T, int rows, int row0, size_t ld, int N, const double *rnew, const DevState *st) {
-    if (st->pivots <= 0) return;
+// Phase end: write the last pivot row back from rnew[pivots & 1] (idempotent).
+__global__ void k_flush_row(double *T, int rows, int row0, size_t ld, int N, const double *rnew, size_t rnew_stride,
+                            const DevState *st) {
+    const long long q = st->pivots;
+    if (q <= 0) return;
     const int rl = st->r - row0;
     if (rl < 0 || rl >= rows) return;
+    const double *src = rnew + (size_t)(q & 1) * rnew_stride;
     for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < N; j += gridDim.x * blockDim.x)
-        T[(size_t)rl * ld + j] = rnew[j];
+        T[(size_t)rl * ld + j] = src[j];
 }
 
 // Virtual-rank "allreduce": out = sum of the shards' contributions in rank order.  Exact,
@@ -567,64 +631,69 @@ int sx_enter_blocks(int L) {
     return g;
 }
 
-void sx_launch_enter_partials(const double *d, int L, TilePart *out, const DevState *st, hipStream_t s) {
+void sx_launch_enter(const double *d, int L, TilePart *parts, DevState *st, hipStream_t s) {
     const int g = sx_enter_blocks(L);
     if (g > SX_TILE) SX_FATAL("entering vector too long for the 512-thread pass 2");
-    k_argmin_pass1<<<g, SX_TILE, 0, s>>>(d + 1, L, out, st);
+    k_argmin_pass1<<<g, SX_TILE, 0, s>>>(d + 1, L, parts, nullptr);
+    k_enter_finish<<<1, SX_TILE, 0, s>>>(parts, g, st);
 }
 
-void sx_launch_ratio_select(double *T, int rows, int row0, size_t ld, int N, const TilePart *enter_parts, int B1,
-                            TilePart *tiles_local, double *colE, DevState *st, int *base, const double *rnew,
-                            bool select, hipStream_t s) {
+void sx_launch_ratio_select(const double *T, int rows, int row0, size_t ld, TilePart *tiles_local, double *colE,
+                            DevState *st, int *base, const double *rnew, size_t rnew_stride, bool select,
+                            hipStream_t s) {
     int g = (rows + SX_TILE - 1) / SX_TILE;
     if (g < 1) g = 1;  // a shard without rows still decides optimality for its own state
     if (select && g > SX_TILE) SX_FATAL("too many ratio tiles for the 512-thread pass 2");
-    k_ratio_select<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, N, enter_parts, B1, tiles_local, colE, st, base, rnew,
+    k_ratio_select<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, tiles_local, colE, st, base, rnew, rnew_stride,
                                          select ? 1 : 0);
 }
 
 void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, int N, const TilePart *tiles_all, int B2,
-                          double *prow_out, int *base, DevState *st, hipStream_t s) {
+                          double *prow_out, int *base, DevState *st, const double *rnew, size_t rnew_stride,
+                          hipStream_t s) {
     if (B2 > SX_TILE) SX_FATAL("too many ratio tiles for the 512-thread pass 2");
     int g = (N + 4 * SX_TILE - 1) / (4 * SX_TILE);
     if (g < 1) g = 1;
     if (g > 64) g = 64;
-    k_select_row<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, N, tiles_all, B2, prow_out, base, st);
+    k_select_row<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, N, tiles_all, B2, prow_out, base, st, rnew, rnew_stride);
 }
 
 template <int RB>
 static void launch_update_rb(dim3 grid, bool snake, double *T, int rows, int row0, size_t ld, int N, double *d,
-                             const double *prow_buf, const double *colE, const DevState *st, double *rnew,
-                             TilePart *enter_parts, hipStream_t s) {
+                             const double *prow_buf, const double *colE, DevState *st, double *rnew,
+                             size_t rnew_stride, TilePart *enter_parts, hipStream_t s) {
     if (snake)
-        k_update<RB, true><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, enter_parts);
+        k_update<RB, true><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, rnew_stride,
+                                                enter_parts);
     else
-        k_update<RB, false><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, enter_parts);
+        k_update<RB, false><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, rnew_stride,
+                                                 enter_parts);
 }
 
 void sx_launch_update(double *T, int rows, int row0, size_t ld, int N, double *d, const double *prow_buf,
-                      const double *colE, const DevState *st, double *rnew, TilePart *enter_parts, UpdateCfg cfg,
-                      hipStream_t s) {
+                      const double *colE, DevState *st, double *rnew, size_t rnew_stride, TilePart *enter_parts,
+                      UpdateCfg cfg, hipStream_t s) {
     const int cols_blocks = (N + 511) / 512;
-    if (sx_enter_blocks(N - 1) > cols_blocks) SX_FATAL("update grid too narrow for the entering partials");
+    const int B1 = (N - 1 + SX_TILE - 1) / SX_TILE;
+    if (B1 > cols_blocks || B1 > 256) SX_FATAL("update grid too narrow for the entering partials");
     const int rb = cfg.rows_per_block;
     const int rg = rows > 0 ? (rows + rb - 1) / rb : 0;
     dim3 grid(cols_blocks, rg + 1);
     const bool sn = cfg.snake != 0;
     switch (rb) {
-    case 1: launch_update_rb<1>(grid, sn, T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, enter_parts, s); break;
-    case 2: launch_update_rb<2>(grid, sn, T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, enter_parts, s); break;
-    case 4: launch_update_rb<4>(grid, sn, T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, enter_parts, s); break;
-    default: launch_update_rb<8>(grid, sn, T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, enter_parts, s); break;
+    case 1: launch_update_rb<1>(grid, sn, T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, rnew_stride, enter_parts, s); break;
+    case 2: launch_update_rb<2>(grid, sn, T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, rnew_stride, enter_parts, s); break;
+    case 4: launch_update_rb<4>(grid, sn, T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, rnew_stride, enter_parts, s); break;
+    default: launch_update_rb<8>(grid, sn, T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, rnew_stride, enter_parts, s); break;
     }
 }
 
-void sx_launch_flush_row(double *T, int rows, int row0, size_t ld, int N, const double *rnew, const DevState *st,
-                         hipStream_t s) {
+void sx_launch_flush_row(double *T, int rows, int row0, size_t ld, int N, const double *rnew, size_t rnew_stride,
+                         const DevState *st, hipStream_t s) {
     if (rows <= 0) return;
     int g = (N + 255) / 256;
     if (g > 256) g = 256;
-    k_flush_row<<<g, 256, 0, s>>>(T, rows, row0, ld, N, rnew, st);
+    k_flush_row<<<g, 256, 0, s>>>(T, rows, row0, ld, N, rnew, rnew_stride, st);
 }
 
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s) {
