@@ -99,6 +99,8 @@ def main():
     ap.add_argument("--update-rows", type=int, default=0, help="rows per update workgroup (0 = auto)")
     ap.add_argument("--snake", type=int, default=-1, help="alternate update sweep: -1 auto, 0 off, 1 on")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--update-events", type=int, default=8,
+                    help="bracket every k-th update launch with HIP events (0 = none)")
     ap.add_argument("--pmc-file", default=None, help="per-launch HBM bytes from rocprofv3 --pmc (JSON)")
     args = ap.parse_args()
 
@@ -135,7 +137,7 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    tim = sess.pivots(args.steps, time_updates=True)
+    tim = sess.pivots(args.steps, time_updates=args.update_events)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -146,7 +148,7 @@ def main():
 
     pivots = tim.pivots
     avg_update_s = tim.update_ms / 1e3 / max(tim.update_launches, 1)
-    achieved = tim.update_bytes / avg_update_s / 1e9
+    achieved = tim.update_bytes / avg_update_s / 1e9 if tim.update_launches else None
     traffic = None
     if args.pmc_file and os.path.exists(args.pmc_file):
         with open(args.pmc_file) as f:
@@ -176,7 +178,7 @@ def main():
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
+            "frac": achieved / HBM_PEAK_GBS if achieved else None,
             "traffic": traffic,
             "kernel": "k_update (rank-1 pivot update, rank 0)",
             "algorithmic_bytes_per_launch": tim.update_bytes,

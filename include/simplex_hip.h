@@ -54,7 +54,7 @@ void simplex_free_problem_struct(problem_t *problem);
 /* ---- benchmark session: a resident phase-1 tableau and timed pivots ---- */
 typedef struct {
     double wall_ms;            /* device time of the whole call (events on the engine stream) */
-    double update_ms;          /* sum of rank-1 update kernel durations (events around each launch) */
+    double update_ms;          /* sum of the timed rank-1 update kernel durations (HIP events) */
     long long pivots;          /* pivots applied during the call */
     long long update_launches; /* update kernel launches timed */
     int status;                /* phase status after the call (SIMPLEX_NOT_ENDED while running) */
@@ -65,6 +65,7 @@ typedef struct {
 
 typedef struct simplex_session simplex_session;
 simplex_session *simplex_session_open(problem_t *problem); /* builds phase 1 + canonicalises d */
+/* k pivots; time_updates = s > 0 brackets every s-th update launch with HIP events */
 int simplex_session_pivots(simplex_session *s, long long k, int time_updates, simplex_timing_t *out);
 double simplex_session_objective(simplex_session *s);   /* d[0] */
 long long simplex_session_total_pivots(simplex_session *s);

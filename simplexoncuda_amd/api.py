@@ -171,9 +171,10 @@ class Session:
         if not self._h:
             raise RuntimeError("simplex_session_open failed")
 
-    def pivots(self, k, time_updates=False):
+    def pivots(self, k, time_updates=0):
+        """k pivots; time_updates = s > 0 times every s-th update launch with HIP events."""
         t = _lib.TimingT()
-        self._lib.simplex_session_pivots(self._h, k, 1 if time_updates else 0, ctypes.byref(t))
+        self._lib.simplex_session_pivots(self._h, k, int(time_updates), ctypes.byref(t))
         return t
 
     def objective(self):
