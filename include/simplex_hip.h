@@ -35,6 +35,10 @@ int simplex_dist_finalize(void);
 /* single-process emulation of W row-block shards on the current device (collectives are
  * device copies); used to test the sharded path on one GPU. 0 or 1 disables. */
 void simplex_set_virtual_ranks(int world);
+/* run the multi-shard exchange path (tile allgather + pivot-row allreduce) even with a
+ * single shard; with simplex_dist_init(.., world=1, ..) it goes through a 1-rank RCCL
+ * communicator.  Test hook. */
+void simplex_set_force_exchange(int on);
 
 /* ---- extended drop-in entry ---- */
 /* twoPhaseMethod + final basis (base_out[m]) and per-phase pivot counts (pivots_out[2]);

@@ -3,7 +3,8 @@
 Each rank drives its row block through libsimplex_hip.so; the per-pivot allgather and
 allreduce go over the library's own RCCL communicator.  Rank 0 checks the answer against
 the CPU oracle bit for bit.  On a 1-GPU box the ranks share device 0 (--same-device).
-usage: torchrun --nproc-per-node W scripts/dist_selftest.py [--same-device]
+usage: torchrun --nproc-per-node W scripts/dist_selftest.py [--same-device] [--force-rccl]
+(--force-rccl: run the exchange path over a real RCCL communicator even at W=1)
 """
 import os
 import sys
@@ -29,7 +30,7 @@ def main():
     import simplexoncuda_amd as sx
     from simplexoncuda_amd import dist as sxdist
 
-    sxdist.init_from_torch(dev)
+    sxdist.init_from_torch(dev, force_rccl="--force-rccl" in sys.argv)
     cases = [(300, 1100, 41100, 1, 100), (129, 1513, 77, -100, 100), (2048, 1024, 205824, 1, 100)]
     ok = True
     for n, m, seed, lo, hi in cases:

@@ -236,6 +236,10 @@ def set_virtual_ranks(w):
     _lib.load().simplex_set_virtual_ranks(int(w))
 
 
+def set_force_exchange(on):
+    _lib.load().simplex_set_force_exchange(1 if on else 0)
+
+
 def set_verbose(on):
     _lib.load().simplex_set_verbose(1 if on else 0)
 

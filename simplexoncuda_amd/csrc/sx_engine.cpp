@@ -52,6 +52,7 @@ struct Config {
     int batch = 16;
     int device = -1;
     int virtual_ranks = 1;
+    int force_exchange = 0;  // run the multi-shard exchange path even with one shard
     bool benchmark = false;
     // distributed
     bool dist = false;
@@ -108,6 +109,7 @@ class Engine {
     int n = 0, m = 0;
     int W = 1;             // total shards (ranks)
     bool rccl = false;     // true: one shard per process, collectives over RCCL
+    bool xchg = false;     // exchange path: tile allgather + pivot-row allreduce per pivot
     int N1 = 0, N2 = 0, N = 0;
     size_t ld = 0;         // row stride in doubles
     int rpr = 0;           // rows per rank (multiple of 512)
@@ -126,12 +128,13 @@ class Engine {
         N2 = 1 + n + m;
         N = N1;
         ld = round_up((size_t)N1, 16);
-        if (g_cfg.dist && g_cfg.world > 1) {
+        if (g_cfg.dist && g_cfg.comm) {
             rccl = true;
             W = g_cfg.world;
         } else if (g_cfg.virtual_ranks > 1) {
             W = g_cfg.virtual_ranks;
         }
+        xchg = W > 1 || g_cfg.force_exchange;
         int dev = 0;
         if (g_cfg.device >= 0) SX_HIP(hipSetDevice(g_cfg.device));
         SX_HIP(hipGetDevice(&dev));
@@ -156,7 +159,7 @@ class Engine {
             alloc_shard(x);
             sh.push_back(x);
         }
-        if (!rccl && W > 1) {
+        if (!rccl && xchg) {
             std::vector<const double *> ptrs;
             for (auto &x : sh) ptrs.push_back(x.prow_send);
             sum_srcs = dalloc<const double *>(W);
@@ -183,15 +186,15 @@ class Engine {
         x.d = dalloc<double>(ld);
         x.colE = dalloc<double>(rows_alloc);
         x.prow = dalloc<double>(ld);
-        if (W > 1) x.prow_send = dalloc<double>(ld);
+        if (xchg) x.prow_send = dalloc<double>(ld);
         x.rnew = dalloc<double>(2 * ld);
         x.coef = dalloc<double>(rows_alloc);
         x.rhs_local = dalloc<double>(rpr);
-        if (W > 1) x.rhs_all = dalloc<double>((size_t)W * rpr);
+        if (xchg) x.rhs_all = dalloc<double>((size_t)W * rpr);
         x.base = dalloc<int>(m);
         x.enter_parts = dalloc<TilePart>(SX_TILE);
         x.tiles_local = dalloc<TilePart>(slots);
-        if (W > 1) x.tiles_all = dalloc<TilePart>((size_t)W * slots);
+        if (xchg) x.tiles_all = dalloc<TilePart>((size_t)W * slots);
         x.st = dalloc<DevState>(1);
         SX_HIP(hipMemsetAsync(x.T, 0, rows_alloc * ld * sizeof(double), s));
         SX_HIP(hipMemsetAsync(x.d, 0, ld * sizeof(double), s));
@@ -204,7 +207,7 @@ class Engine {
             t.elig = 0;
         }
         SX_HIP(hipMemcpy(x.tiles_local, pad.data(), sizeof(TilePart) * slots, hipMemcpyHostToDevice));
-        if (W > 1)
+        if (xchg)
             SX_HIP(hipMemcpy(x.tiles_all, pad.data(), sizeof(TilePart) * pad.size(), hipMemcpyHostToDevice));
     }
 
@@ -281,14 +284,14 @@ class Engine {
         const size_t part = (size_t)slots * width;
         for (auto &x : sh) {
             if (!x.gemv_local) x.gemv_local = dalloc<double>((size_t)slots * N1);
-            if (W > 1 && !x.gemv_all) x.gemv_all = dalloc<double>((size_t)W * slots * N1);
+            if (xchg && !x.gemv_all) x.gemv_all = dalloc<double>((size_t)W * slots * N1);
             SX_HIP(hipMemsetAsync(x.gemv_local, 0, part * sizeof(double), s));
             sx_launch_coef(x.d, x.base, x.row0, x.rows, x.coef, s);
             sx_launch_gemv_partials(x.T, x.rows, ld, width, x.coef, x.gemv_local, s);
         }
-        if (W > 1) allgather_doubles(&Shard::gemv_local, &Shard::gemv_all, part);
+        if (xchg) allgather_doubles(&Shard::gemv_local, &Shard::gemv_all, part);
         const int nblk = (m + SX_TILE - 1) / SX_TILE;
-        for (auto &x : sh) sx_launch_gemv_apply(x.d, width, W > 1 ? x.gemv_all : x.gemv_local, nblk, s);
+        for (auto &x : sh) sx_launch_gemv_apply(x.d, width, xchg ? x.gemv_all : x.gemv_local, nblk, s);
     }
 
     void phase2_costs() {
@@ -317,8 +320,8 @@ class Engine {
     void enqueue_pivot(hipEvent_t ev0, hipEvent_t ev1) {
         const UpdateCfg cfg = update_cfg();
         for (auto &x : sh)
-            sx_launch_ratio_select(x.T, x.rows, x.row0, ld, x.tiles_local, x.colE, x.st, x.base, x.rnew, ld, W == 1, s);
-        if (W > 1) {
+            sx_launch_ratio_select(x.T, x.rows, x.row0, ld, x.tiles_local, x.colE, x.st, x.base, x.rnew, ld, !xchg, s);
+        if (xchg) {
             allgather_tiles();
             for (auto &x : sh)
                 sx_launch_select_row(x.T, x.rows, x.row0, ld, N, x.tiles_all, W * slots, x.prow_send, x.base, x.st,
@@ -327,7 +330,7 @@ class Engine {
         }
         if (ev0) SX_HIP(hipEventRecord(ev0, s));
         for (auto &x : sh)
-            sx_launch_update(x.T, x.rows, x.row0, ld, N, x.d, W > 1 ? x.prow : nullptr, x.colE, x.st, x.rnew, ld,
+            sx_launch_update(x.T, x.rows, x.row0, ld, N, x.d, xchg ? x.prow : nullptr, x.colE, x.st, x.rnew, ld,
                              x.enter_parts, cfg, s);
         if (ev1) SX_HIP(hipEventRecord(ev1, s));
     }
@@ -403,7 +406,7 @@ class Engine {
     void read_rhs(std::vector<double> &out) {
         out.assign(m, 0.0);
         for (auto &x : sh) sx_launch_gather_rhs(x.T, x.rows, ld, x.rhs_local, s);
-        if (W > 1) {
+        if (xchg) {
             allgather_doubles(&Shard::rhs_local, &Shard::rhs_all, rpr);
             SX_HIP(hipMemcpyAsync(out.data(), sh[0].rhs_all, sizeof(double) * m, hipMemcpyDeviceToHost, s));
         } else {
@@ -512,6 +515,7 @@ void simplex_set_device(int device) {
     if (device >= 0) SX_HIP(hipSetDevice(device));
 }
 void simplex_set_virtual_ranks(int world) { g_cfg.virtual_ranks = world > 1 ? world : 1; }
+void simplex_set_force_exchange(int on) { g_cfg.force_exchange = on ? 1 : 0; }
 
 void enableBenchmarkMode(void) { g_cfg.benchmark = true; }
 void disableBenchmarkMode(void) { g_cfg.benchmark = false; }
@@ -533,7 +537,7 @@ int simplex_dist_init(int rank, int world, const unsigned char *unique_id, int d
     }
     g_cfg.rank = rank;
     g_cfg.world = world;
-    if (world > 1) {
+    if (world > 1 || g_cfg.force_exchange) {
         ncclUniqueId id;
         std::memcpy(&id, unique_id, sizeof(id));
         SX_NCCL(ncclCommInitRank(&g_cfg.comm, world, id, rank));

@@ -9,14 +9,17 @@ import ctypes
 from . import _lib
 
 
-def init_from_torch(local_rank):
+def init_from_torch(local_rank, force_rccl=False):
+    """force_rccl: build the RCCL communicator (and the exchange path) even at world size 1."""
     import torch.distributed as dist
 
     lib = _lib.load()
+    if force_rccl:
+        lib.simplex_set_force_exchange(1)
     rank, world = dist.get_rank(), dist.get_world_size()
     size = lib.simplex_dist_unique_id_size()
     uid = b""
-    if world > 1:
+    if world > 1 or force_rccl:
         if rank == 0:
             buf = ctypes.create_string_buffer(size)
             lib.simplex_dist_get_unique_id(buf)

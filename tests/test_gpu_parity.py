@@ -207,3 +207,18 @@ def test_update_configs_bit_exact(gpu, rb, snake):
         sx.set_snake(-1)
     oracle.solve(T, d, base, max_pivots=21)
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+@pytest.mark.parametrize("W", [1, 2])
+def test_exchange_path_bit_exact(gpu, W):
+    """the multi-shard kernels (tile allgather, select+row copy, -0.0 allreduce, update from the
+    exchanged row) on virtual shards -- W=1 runs them with a single shard"""
+    p = sx.generateRandomProblem(300, 1100, 300 * 100 + 1100, 1, 100)
+    try:
+        sx.set_virtual_ranks(W)
+        sx.set_force_exchange(1)
+        got, _ = _check_two_phase(p)
+    finally:
+        sx.set_force_exchange(0)
+        sx.set_virtual_ranks(1)
+    assert got.status == sx.FEASIBLE
