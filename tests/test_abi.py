@@ -87,3 +87,25 @@ def test_print_problem(tmp_path):
     txt = out.read_text()
     assert txt.startswith("max + 8.00 X1 + 10.00 X2 + 7.00 X3 \nsubject to \n")
     assert "+ 1.00 X1 + 3.00 X2 + 2.00 X3 <= 10.00" in txt
+
+
+def _build_c_caller(tmp_path, compiler, std):
+    import subprocess
+    exe = tmp_path / f"drop_in_{compiler}"
+    lib_dir = os.path.join(ROOT, "simplexoncuda_amd")
+    cmd = [compiler, f"-std={std}", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "tests", "c", "drop_in_main.c"), "-L", lib_dir, "-lsimplex_hip",
+           f"-Wl,-rpath,{lib_dir}", "-o", str(exe)]
+    if compiler == "g++":
+        cmd[1:1] = ["-x", "c++"]
+    subprocess.run(cmd, check=True)
+    return exe
+
+
+@pytest.mark.parametrize("compiler,std", [("gcc", "c99"), ("g++", "c++17")])
+def test_headers_compile_and_link_as_c_and_cxx(tmp_path, compiler, std):
+    import subprocess
+    exe = _build_c_caller(tmp_path, compiler, std)
+    out = subprocess.run([str(exe), "host"], check=True, capture_output=True, text=True).stdout
+    assert out.startswith("max + ") and "subject to" in out
+    assert "compare(1e-10)=0 compare(-1)=-1" in out

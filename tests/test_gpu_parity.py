@@ -222,3 +222,14 @@ def test_exchange_path_bit_exact(gpu, W):
         sx.set_force_exchange(0)
         sx.set_virtual_ranks(1)
     assert got.status == sx.FEASIBLE
+
+
+def test_c_caller_drop_in(gpu, tmp_path):
+    """a reference-style C program linked against libsimplex_hip.so solves smallProblem.txt"""
+    import subprocess
+    from test_abi import _build_c_caller
+    exe = _build_c_caller(tmp_path, "gcc", "c99")
+    r = subprocess.run([str(exe), "solve", os.path.join(GOLDEN, "examples", "smallProblem.txt")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "status 0 z 64.000000 x0 8.000000" in r.stdout
