@@ -101,7 +101,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--update-events", type=int, default=8,
                     help="bracket every k-th update launch with HIP events (0 = none)")
-    ap.add_argument("--pmc-file", default=None, help="per-launch HBM bytes from rocprofv3 --pmc (JSON)")
+    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_update_config3.json"),
+                    help="per-launch HBM bytes of the update kernel from rocprofv3 --pmc (JSON)")
+    ap.add_argument("--secondary", default="config5",
+                    help="second workload timed in the same run ('' to skip): the m=32768 scaling problem")
+    ap.add_argument("--secondary-steps", type=int, default=40)
+    ap.add_argument("--secondary-warmup", type=int, default=3)
     args = ap.parse_args()
 
     import torch
@@ -124,31 +129,38 @@ def main():
     sx.set_update_rows(args.update_rows)
     sx.set_snake(args.snake)
 
-    n, m, seed = CONFIGS[args.config]
-    problem = sx.generateRandomProblem(n, m, seed, 1, 100)
-    sess = sx.Session(problem)
-    if args.warmup > 0:
-        sess.pivots(args.warmup)
-
     def barrier():
         if world > 1:
             dist.barrier()
 
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    tim = sess.pivots(args.steps, time_updates=args.update_events)
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    def measure(config, steps, warmup, events):
+        """W untimed + K timed phase-1 pivots of `config`; returns timing + roofline."""
+        n, m, seed = CONFIGS[config]
+        problem = sx.generateRandomProblem(n, m, seed, 1, 100)
+        sess = sx.Session(problem)
+        del problem
+        if warmup > 0:
+            sess.pivots(warmup)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tim = sess.pivots(steps, time_updates=events)
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = float(tt.item())
+        sess.close()
+        avg_update_s = tim.update_ms / 1e3 / max(tim.update_launches, 1)
+        achieved = tim.update_bytes / avg_update_s / 1e9 if tim.update_launches else None
+        return {"n": n, "m": m, "seed": seed, "tim": tim, "elapsed": elapsed, "pivots": tim.pivots,
+                "avg_update_s": avg_update_s, "achieved": achieved}
 
-    pivots = tim.pivots
-    avg_update_s = tim.update_ms / 1e3 / max(tim.update_launches, 1)
-    achieved = tim.update_bytes / avg_update_s / 1e9 if tim.update_launches else None
+    r = measure(args.config, args.steps, args.warmup, args.update_events)
+    n, m, seed, tim, elapsed, pivots = r["n"], r["m"], r["seed"], r["tim"], r["elapsed"], r["pivots"]
+    avg_update_s, achieved = r["avg_update_s"], r["achieved"]
     traffic = None
     if args.pmc_file and os.path.exists(args.pmc_file):
         with open(args.pmc_file) as f:
@@ -183,12 +195,25 @@ def main():
             "kernel": "k_update (rank-1 pivot update, rank 0)",
             "algorithmic_bytes_per_launch": tim.update_bytes,
             "avg_launch_us": avg_update_s * 1e6,
+            "timed_launches": tim.update_launches,
         },
         "cpu_baseline": None,
     }
+    if args.secondary and args.secondary != args.config:
+        r2 = measure(args.secondary, args.secondary_steps, args.secondary_warmup, args.update_events)
+        t2 = r2["tim"]
+        out["secondary"] = {
+            "workload": f"{args.secondary}: phase-1 pivots, {r2['m']}x{1 + r2['n'] + 2 * r2['m']} fp64 tableau "
+                        f"(m={r2['m']}, n={r2['n']}, seed={r2['seed']})",
+            "value": r2["pivots"] / r2["elapsed"], "unit": "pivots/s",
+            "ms_per_step": r2["elapsed"] * 1e3 / max(r2["pivots"], 1),
+            "steps": args.secondary_steps, "warmup": args.secondary_warmup, "pivots_timed": r2["pivots"],
+            "rows_per_gpu_rank0": t2.local_rows,
+            "update_GBps_rank0": r2["achieved"], "update_frac_of_peak": r2["achieved"] / HBM_PEAK_GBS
+            if r2["achieved"] else None, "avg_update_us": r2["avg_update_s"] * 1e6,
+        }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, m, seed, CPU_SAMPLE[args.config], sx)
-    sess.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

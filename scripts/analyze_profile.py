@@ -5,7 +5,7 @@
       traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes -- gfx950 FETCH_SIZE counts half
       the bytes of a wide coalesced stream (MI355X_MICROARCH.md §HBM); WRITE_SIZE is exact
       for 16-B-per-lane streaming stores.
-usage: python scripts/analyze_profile.py <prof_dir> <tag> [kernel_substring]
+usage: python scripts/analyze_profile.py <prof_dir> <tag> [kernel_substring] [publish_as.json]
 """
 import collections
 import csv
@@ -47,8 +47,12 @@ def main():
             res.update({"pmc_kernel": k, "launches": len(fetch[k]), "FETCH_SIZE_KB_avg": fs, "WRITE_SIZE_KB_avg": ws,
                         "hbm_bytes_per_launch": (2 * fs + ws) * 1024.0,
                         "correction": "traffic = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count)"})
+    res["tag"] = tag
     with open(os.path.join(out, f"{tag}_pmc_update.json"), "w") as f:
         json.dump(res, f, indent=1)
+    if len(sys.argv) > 4:  # also publish as the file bench.py reads for roofline.traffic
+        with open(os.path.join(out, sys.argv[4]), "w") as f:
+            json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))
 
 
