@@ -26,6 +26,9 @@ void simplex_set_update_rows(int rb);        /* rows per update workgroup: 1, 2,
 void simplex_set_snake(int mode);            /* alternate update sweep direction: -1 auto, 0, 1 */
 void simplex_set_batch(int pivots);          /* pivots enqueued between status polls */
 void simplex_set_device(int device);
+/* write the reference's -D TIMER CSV (chrono.cu) into `dir` (NULL or "" = off; env
+ * SIMPLEX_TIMER_DIR also enables it); benchmark mode names it benchmark_<n>_<m>.txt */
+void simplex_set_timer_dir(const char *dir);
 
 /* ---- multi-GPU: one process per GPU, RCCL communicator over xGMI ---- */
 int simplex_dist_unique_id_size(void);

@@ -83,6 +83,7 @@ SIGNATURES = {
     "simplex_set_snake": (None, [ctypes.c_int]),
     "simplex_set_batch": (None, [ctypes.c_int]),
     "simplex_set_device": (None, [ctypes.c_int]),
+    "simplex_set_timer_dir": (None, [ctypes.c_char_p]),
     "simplex_dist_unique_id_size": (ctypes.c_int, []),
     "simplex_dist_get_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "simplex_dist_init": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),

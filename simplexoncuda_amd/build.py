@@ -41,6 +41,20 @@ def build_lib(force=False, verbose=False):
     return LIB
 
 
+CLI = os.path.join(PKG, "simplex_cli")
+
+
+def build_cli(force=False):
+    """simplex_cli: the reference's main.cu front end, linked against the library."""
+    src = os.path.join(CSRC, "sx_cli.cpp")
+    if not force and not _stale(CLI, [src, LIB]):
+        return CLI
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-I", os.path.join(ROOT, "include"), src, "-L", PKG,
+           "-lsimplex_hip", "-Wl,-rpath,$ORIGIN", "-o", CLI]
+    subprocess.run(cmd, check=True)
+    return CLI
+
+
 def build_oracle(force=False):
     args = ["make", "-s", "-C", os.path.join(ROOT, "oracle")]
     if force:
@@ -51,4 +65,5 @@ def build_oracle(force=False):
 
 if __name__ == "__main__":
     build_lib(force="--force" in sys.argv, verbose=True)
+    build_cli(force="--force" in sys.argv)
     build_oracle()

@@ -10,7 +10,9 @@
 
 #include <algorithm>
 #include <cstring>
+#include <ctime>
 #include <map>
+#include <string>
 #include <mutex>
 #include <vector>
 
@@ -53,6 +55,7 @@ struct Config {
     int device = -1;
     int virtual_ranks = 1;
     int force_exchange = 0;  // run the multi-shard exchange path even with one shard
+    std::string timer_dir;   // non-empty: write the reference's TIMER CSV there
     bool benchmark = false;
     // distributed
     bool dist = false;
@@ -80,6 +83,64 @@ T *dalloc(size_t count) {
     SX_HIP(hipMalloc(reinterpret_cast<void **>(&p), count * sizeof(T)));
     return p;
 }
+
+// ------------------------------------------------------------------ TIMER CSV (chrono.cu:8-57)
+// Same file names and format as the reference's -D TIMER build: header
+// "vars,contraints,operation,elapsed_time", one row "rows,cols,op,us" per timed operation
+// (rows = tableau width in the reference's counting, cols = m), one "solve" row per
+// iteration of the pivot loop including the terminating one.  Enabled by
+// simplex_set_timer_dir() or SIMPLEX_TIMER_DIR.
+struct Chrono {
+    FILE *f = nullptr;
+    hipEvent_t a = nullptr, b = nullptr;
+
+    bool on() const { return f != nullptr; }
+
+    void open(int n, int m) {
+        std::string dir = g_cfg.timer_dir;
+        if (dir.empty()) {
+            const char *e = getenv("SIMPLEX_TIMER_DIR");
+            if (e) dir = e;
+        }
+        if (dir.empty()) return;
+        char name[96];
+        if (g_cfg.benchmark) {
+            snprintf(name, sizeof(name), "/benchmark_%d_%d.txt", n, m);
+        } else {
+            time_t t = time(nullptr);
+            char ts[32];
+            strftime(ts, sizeof(ts), "%Y%m%d%H%M%S.%d", localtime(&t));
+            snprintf(name, sizeof(name), "/times_%s.txt", ts);
+        }
+        f = openFile((dir + name).c_str(), "w");
+        fprintf(f, "vars,contraints,operation,elapsed_time\n");
+        SX_HIP(hipEventCreate(&a));
+        SX_HIP(hipEventCreate(&b));
+    }
+    void start(hipStream_t s, int rows, int cols, const char *op) {
+        if (!f) return;
+        fprintf(f, "%d,%d,%s,", rows, cols, op);
+        SX_HIP(hipEventRecord(a, s));
+    }
+    void stop(hipStream_t s) {
+        if (!f) return;
+        SX_HIP(hipEventRecord(b, s));
+        SX_HIP(hipEventSynchronize(b));
+        float ms = 0.f;
+        SX_HIP(hipEventElapsedTime(&ms, a, b));
+        fprintf(f, "%f\n", ms * 1000.0f);
+    }
+    void row(int rows, int cols, const char *op, float ms) {
+        if (f) fprintf(f, "%d,%d,%s,%f\n", rows, cols, op, ms * 1000.0f);
+    }
+    ~Chrono() {
+        if (f) {
+            fclose(f);
+            (void)hipEventDestroy(a);
+            (void)hipEventDestroy(b);
+        }
+    }
+};
 
 // ------------------------------------------------------------------ shard + engine
 struct Shard {
@@ -363,14 +424,29 @@ class Engine {
     // solve (solver.cu:128-149): pivots until the phase ends.  Batches of pivots are
     // enqueued back to back; the host polls the status of the batch before the last one,
     // so the device never waits on the host.  Kernels of a finished phase return at once.
-    int run_phase(int width, long long max_pivots, long long *pivots) {
+    int run_phase(int width, long long max_pivots, long long *pivots, Chrono *ch = nullptr) {
         N = width;
         reset_state(max_pivots);
         enqueue_enter_partials();
         const int batch = g_cfg.batch > 0 ? g_cfg.batch : 16;
+        const bool timed = ch && ch->on();
+        std::vector<hipEvent_t> it_ev;  // TIMER CSV: one event pair per loop iteration
         long long k = 0;
         for (;; ++k) {
-            for (int b = 0; b < batch; ++b) enqueue_pivot(nullptr, nullptr);
+            for (int b = 0; b < batch; ++b) {
+                if (timed) {
+                    hipEvent_t e0, e1;
+                    SX_HIP(hipEventCreate(&e0));
+                    SX_HIP(hipEventCreate(&e1));
+                    SX_HIP(hipEventRecord(e0, s));
+                    enqueue_pivot(nullptr, nullptr);
+                    SX_HIP(hipEventRecord(e1, s));
+                    it_ev.push_back(e0);
+                    it_ev.push_back(e1);
+                } else {
+                    enqueue_pivot(nullptr, nullptr);
+                }
+            }
             const int slot = (int)(k & 1);
             SX_HIP(hipMemcpyAsync(st_host + slot, sh[0].st, sizeof(DevState), hipMemcpyDeviceToHost, s));
             SX_HIP(hipEventRecord(poll_ev[slot], s));
@@ -381,6 +457,15 @@ class Engine {
         }
         flush();
         DevState f = read_state();
+        if (timed) {
+            const size_t iters = std::min(it_ev.size() / 2, (size_t)f.pivots + 1);
+            for (size_t i = 0; i < iters; ++i) {
+                float ms = 0.f;
+                SX_HIP(hipEventElapsedTime(&ms, it_ev[2 * i], it_ev[2 * i + 1]));
+                ch->row(width, m, "solve", ms);
+            }
+            for (auto e : it_ev) (void)hipEventDestroy(e);
+        }
         if (pivots) *pivots = f.pivots;
         return f.status;
     }
@@ -447,18 +532,23 @@ int two_phase(problem_t *P, double *solution, double *opt, int *base_out, long l
               long long max_pivots) {
     const int n = P->vars, m = P->constraints;
     Engine E(n, m);
+    Chrono ch;
+    ch.open(n, m);
     long long p1 = 0, p2 = 0;
     int status;
     // phase1 (twoPhaseMethod.cu:225-283)
     say("Phase 1: Filling Tableau");
+    ch.start(E.s, E.N1, m, "fillTableau");
     E.build_phase1(P);
+    ch.stop(E.s);
     say("Phase 1: Resetting out-of-base variables");
+    ch.start(E.s, E.N1, m, "gauss1");
     E.update_objective(E.N1);
+    ch.stop(E.s);
     say("Phase 1: Solving auxiliary problem");
-    const int st1 = E.run_phase(E.N1, max_pivots, &p1);  // return value ignored by the reference (:258)
+    const int st1 = E.run_phase(E.N1, max_pivots, &p1, &ch);  // return value ignored by the reference (:258)
     const double d0 = E.read_d0();
     std::vector<int> base(m);
-    E.read_base(base.data());
     if (st1 == SX_PIVOT_CAP) {
         status = SX_PIVOT_CAP;
     } else if (st1 == SX_NUMERIC_FAIL) {
@@ -466,21 +556,30 @@ int two_phase(problem_t *P, double *solution, double *opt, int *base_out, long l
     } else if (compare(d0) < 0) {
         status = INFEASIBLE;  // :265-268
     } else {
+        ch.start(E.s, E.N1, m, "checkDegeneracy");
+        E.read_base(base.data());
         status = FEASIBLE;  // checkDegeneracy (:206-223)
         for (int i = 0; i < m; ++i)
             if (base[i] >= n + m && base[i] < n + 2 * m) status = DEGENERATE;
+        ch.stop(E.s);
     }
+    E.read_base(base.data());
     if (status == FEASIBLE) {
         // phase2 (:285-356): drop the artificial columns, costs -c / 0, d[0] kept
         say("Phase 2: Filling costs vector with the original one");
+        ch.start(E.s, E.N2, m, "costsVector");
         E.phase2_costs();
+        ch.stop(E.s);
         say("Phase 2: Resetting out-of-base variables");
+        ch.start(E.s, E.N2, m, "gauss2");
         E.update_objective(E.N2);
+        ch.stop(E.s);
         say("Phase 2: Solving original problem");
-        status = E.run_phase(E.N2, max_pivots, &p2);
+        status = E.run_phase(E.N2, max_pivots, &p2, &ch);
         E.read_base(base.data());
         if (status == FEASIBLE) {
             // getSolutionHost (:370-383)
+            ch.start(E.s, E.N2, m, "solution");
             const double z = E.read_d0();
             std::vector<double> rhs;
             E.read_rhs(rhs);
@@ -490,6 +589,7 @@ int two_phase(problem_t *P, double *solution, double *opt, int *base_out, long l
                 for (int i = 0; i < m; ++i)
                     if (base[i] < n) solution[base[i]] = rhs[i];
             }
+            ch.stop(E.s);
         }
     }
     if (base_out) std::memcpy(base_out, base.data(), sizeof(int) * m);
@@ -516,6 +616,7 @@ void simplex_set_device(int device) {
 }
 void simplex_set_virtual_ranks(int world) { g_cfg.virtual_ranks = world > 1 ? world : 1; }
 void simplex_set_force_exchange(int on) { g_cfg.force_exchange = on ? 1 : 0; }
+void simplex_set_timer_dir(const char *dir) { g_cfg.timer_dir = dir ? dir : ""; }
 
 void enableBenchmarkMode(void) { g_cfg.benchmark = true; }
 void disableBenchmarkMode(void) { g_cfg.benchmark = false; }

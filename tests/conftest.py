@@ -16,10 +16,11 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session", autouse=True)
 def _built():
-    from simplexoncuda_amd.build import build_lib, build_oracle
+    from simplexoncuda_amd.build import build_cli, build_lib, build_oracle
 
     build_oracle()
     build_lib()
+    build_cli()
 
 
 @pytest.fixture(scope="session")
