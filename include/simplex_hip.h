@@ -42,6 +42,9 @@ void simplex_set_virtual_ranks(int world);
  * single shard; with simplex_dist_init(.., world=1, ..) it goes through a 1-rank RCCL
  * communicator.  Test hook. */
 void simplex_set_force_exchange(int on);
+/* per-pivot exchange between shards: 0 auto, 1 tile-winner allgather + pivot-row allreduce,
+ * 2 one allgather of tile winners together with their rows (auto: when <= 1 MiB per rank) */
+void simplex_set_exchange_mode(int mode);
 
 /* ---- extended drop-in entry ---- */
 /* twoPhaseMethod + final basis (base_out[m]) and per-phase pivot counts (pivots_out[2]);

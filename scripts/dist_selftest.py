@@ -33,7 +33,8 @@ def main():
     sxdist.init_from_torch(dev, force_rccl="--force-rccl" in sys.argv)
     cases = [(300, 1100, 41100, 1, 100), (129, 1513, 77, -100, 100), (2048, 1024, 205824, 1, 100)]
     ok = True
-    for n, m, seed, lo, hi in cases:
+    for mode, (n, m, seed, lo, hi) in [(md, c) for md in (1, 2) for c in cases]:
+        sx.set_exchange_mode(mode)
         p = sx.generateRandomProblem(n, m, seed, lo, hi)
         t0 = time.time()
         got = sx.twoPhaseMethodEx(p)
@@ -49,8 +50,9 @@ def main():
                 good = good and np.float64(got.optimal_value).view(np.uint64) == np.float64(ref["opt"]).view(np.uint64)
                 good = good and np.array_equal(got.solution.view(np.uint64), ref["x"].view(np.uint64))
             ok = ok and good
-            print(f"world={world} n={n} m={m}: status {got.status} pivots {got.pivots} "
+            print(f"world={world} exchange_mode={mode} n={n} m={m}: status {got.status} pivots {got.pivots} "
                   f"{'BIT-EXACT' if good else 'MISMATCH'} vs oracle ({dt:.2f}s)", flush=True)
+    sx.set_exchange_mode(0)
     # a timed session on the config-2 instance
     p = sx.generateRandomProblem(2048, 1024, 205824, 1, 100)
     s = sx.Session(p)

@@ -90,6 +90,7 @@ SIGNATURES = {
     "simplex_dist_finalize": (ctypes.c_int, []),
     "simplex_set_virtual_ranks": (None, [ctypes.c_int]),
     "simplex_set_force_exchange": (None, [ctypes.c_int]),
+    "simplex_set_exchange_mode": (None, [ctypes.c_int]),
     "twoPhaseMethodEx": (ctypes.c_int, [P_PROBLEM, c_double_p, c_double_p, c_int_p, c_ll_p, ctypes.c_longlong]),
     "simplex_problem_from_arrays": (P_PROBLEM, [ctypes.c_int, ctypes.c_int, c_double_p, c_double_p, c_double_p]),
     "simplex_generate_problem_ex": (P_PROBLEM, [ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_int,

@@ -64,13 +64,15 @@ int sx_enter_blocks(int L);
 void sx_launch_enter(const double *d, int L, TilePart *parts, DevState *st, hipStream_t s);
 void sx_launch_ratio_select(const double *T, int rows, int row0, size_t ld, TilePart *tiles_local, double *colE,
                             DevState *st, int *base, const double *rnew, size_t rnew_stride, bool select,
-                            hipStream_t s);
+                            double *slots, size_t slot_stride, int N, hipStream_t s);
+void sx_launch_select_gathered(const double *slots, size_t slot_stride, int B2, int *base, DevState *st,
+                               hipStream_t s);
 void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, int N, const TilePart *tiles_all, int B2,
                           double *prow_out, int *base, DevState *st, const double *rnew, size_t rnew_stride,
                           hipStream_t s);
 void sx_launch_update(double *T, int rows, int row0, size_t ld, int N, double *d, const double *prow_buf,
-                      const double *colE, DevState *st, double *rnew, size_t rnew_stride, TilePart *enter_parts,
-                      UpdateCfg cfg, hipStream_t s);
+                      size_t prow_stride, const double *colE, DevState *st, double *rnew, size_t rnew_stride,
+                      TilePart *enter_parts, UpdateCfg cfg, hipStream_t s);
 void sx_launch_flush_row(double *T, int rows, int row0, size_t ld, int N, const double *rnew, size_t rnew_stride,
                          const DevState *st, hipStream_t s);
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s);

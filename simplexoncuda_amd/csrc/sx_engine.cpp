@@ -56,6 +56,7 @@ struct Config {
     int virtual_ranks = 1;
     int force_exchange = 0;  // run the multi-shard exchange path even with one shard
     std::string timer_dir;   // non-empty: write the reference's TIMER CSV there
+    int exchange_mode = 0;   // 0 auto, 1 tile allgather + row allreduce, 2 row-gather
     bool benchmark = false;
     // distributed
     bool dist = false;
@@ -152,6 +153,8 @@ struct Shard {
     double *colE = nullptr;
     double *prow = nullptr;
     double *prow_send = nullptr;
+    double *slot_send = nullptr;  // row-gather: per tile [TilePart header | winner row]
+    double *slot_all = nullptr;
     double *rnew = nullptr;
     double *coef = nullptr;
     double *gemv_local = nullptr;
@@ -171,6 +174,8 @@ class Engine {
     int W = 1;             // total shards (ranks)
     bool rccl = false;     // true: one shard per process, collectives over RCCL
     bool xchg = false;     // exchange path: tile allgather + pivot-row allreduce per pivot
+    bool rowgather = false;  // exchange path variant: one allgather of tile winners with their rows
+    size_t slot_stride = 0;  // doubles per row-gather slot (16-byte header + ld)
     int N1 = 0, N2 = 0, N = 0;
     size_t ld = 0;         // row stride in doubles
     int rpr = 0;           // rows per rank (multiple of 512)
@@ -196,6 +201,7 @@ class Engine {
             W = g_cfg.virtual_ranks;
         }
         xchg = W > 1 || g_cfg.force_exchange;
+        slot_stride = ld + 2;
         int dev = 0;
         if (g_cfg.device >= 0) SX_HIP(hipSetDevice(g_cfg.device));
         SX_HIP(hipGetDevice(&dev));
@@ -205,6 +211,9 @@ class Engine {
         if (rpr == 0) rpr = SX_TILE;
         slots = rpr / SX_TILE;
         if ((long long)W * slots > SX_TILE) SX_FATAL("too many constraint tiles for the exact argmin tree");
+        // one allgather of (tile winner, row) beats two collectives while the rows are small
+        const double slot_bytes = 8.0 * (double)slots * (double)slot_stride;
+        rowgather = xchg && (g_cfg.exchange_mode == 2 || (g_cfg.exchange_mode == 0 && slot_bytes <= 1048576.0));
         std::vector<int> ranks;
         if (rccl)
             ranks.push_back(g_cfg.rank);
@@ -248,6 +257,18 @@ class Engine {
         x.colE = dalloc<double>(rows_alloc);
         x.prow = dalloc<double>(ld);
         if (xchg) x.prow_send = dalloc<double>(ld);
+        if (rowgather) {
+            x.slot_send = dalloc<double>((size_t)slots * slot_stride);
+            x.slot_all = dalloc<double>((size_t)W * slots * slot_stride);
+            std::vector<double> init((size_t)slots * slot_stride, 0.0);
+            for (int k = 0; k < slots; ++k) {
+                TilePart *h = reinterpret_cast<TilePart *>(init.data() + (size_t)k * slot_stride);
+                h->v = 1.7976931348623157e308;
+                h->idx = -1;
+                h->elig = 0;
+            }
+            SX_HIP(hipMemcpy(x.slot_send, init.data(), sizeof(double) * init.size(), hipMemcpyHostToDevice));
+        }
         x.rnew = dalloc<double>(2 * ld);
         x.coef = dalloc<double>(rows_alloc);
         x.rhs_local = dalloc<double>(rpr);
@@ -274,7 +295,7 @@ class Engine {
 
     void free_shard(Shard &x) {
         for (void *p : {(void *)x.T, (void *)x.d, (void *)x.colE, (void *)x.prow, (void *)x.prow_send,
-                        (void *)x.rnew, (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
+                        (void *)x.slot_send, (void *)x.slot_all, (void *)x.rnew, (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
                         (void *)x.rhs_all, (void *)x.base, (void *)x.enter_parts, (void *)x.tiles_local,
                         (void *)x.tiles_all, (void *)x.st})
             if (p) (void)hipFree(p);
@@ -316,6 +337,19 @@ class Engine {
             for (auto &src : sh)
                 SX_HIP(hipMemcpyAsync(dst.tiles_all + (size_t)src.rank * slots, src.tiles_local,
                                       sizeof(TilePart) * slots, hipMemcpyDeviceToDevice, s));
+    }
+
+    void allgather_slots() {
+        const size_t count = (size_t)slots * slot_stride;
+        if (rccl) {
+            Shard &x = sh[0];
+            SX_NCCL(ncclAllGather(x.slot_send, x.slot_all, count, ncclDouble, g_cfg.comm, s));
+            return;
+        }
+        for (auto &dst : sh)
+            for (auto &src : sh)
+                SX_HIP(hipMemcpyAsync(dst.slot_all + (size_t)src.rank * count, src.slot_send, sizeof(double) * count,
+                                      hipMemcpyDeviceToDevice, s));
     }
 
     void allreduce_prow() {
@@ -381,8 +415,12 @@ class Engine {
     void enqueue_pivot(hipEvent_t ev0, hipEvent_t ev1) {
         const UpdateCfg cfg = update_cfg();
         for (auto &x : sh)
-            sx_launch_ratio_select(x.T, x.rows, x.row0, ld, x.tiles_local, x.colE, x.st, x.base, x.rnew, ld, !xchg, s);
-        if (xchg) {
+            sx_launch_ratio_select(x.T, x.rows, x.row0, ld, x.tiles_local, x.colE, x.st, x.base, x.rnew, ld, !xchg,
+                                   rowgather ? x.slot_send : nullptr, slot_stride, N, s);
+        if (rowgather) {
+            allgather_slots();
+            for (auto &x : sh) sx_launch_select_gathered(x.slot_all, slot_stride, W * slots, x.base, x.st, s);
+        } else if (xchg) {
             allgather_tiles();
             for (auto &x : sh)
                 sx_launch_select_row(x.T, x.rows, x.row0, ld, N, x.tiles_all, W * slots, x.prow_send, x.base, x.st,
@@ -390,9 +428,11 @@ class Engine {
             allreduce_prow();
         }
         if (ev0) SX_HIP(hipEventRecord(ev0, s));
-        for (auto &x : sh)
-            sx_launch_update(x.T, x.rows, x.row0, ld, N, x.d, xchg ? x.prow : nullptr, x.colE, x.st, x.rnew, ld,
-                             x.enter_parts, cfg, s);
+        for (auto &x : sh) {
+            const double *pb = rowgather ? x.slot_all : (xchg ? x.prow : nullptr);
+            sx_launch_update(x.T, x.rows, x.row0, ld, N, x.d, pb, rowgather ? slot_stride : 0, x.colE, x.st, x.rnew,
+                             ld, x.enter_parts, cfg, s);
+        }
         if (ev1) SX_HIP(hipEventRecord(ev1, s));
     }
 
@@ -616,6 +656,7 @@ void simplex_set_device(int device) {
 }
 void simplex_set_virtual_ranks(int world) { g_cfg.virtual_ranks = world > 1 ? world : 1; }
 void simplex_set_force_exchange(int on) { g_cfg.force_exchange = on ? 1 : 0; }
+void simplex_set_exchange_mode(int mode) { g_cfg.exchange_mode = (mode >= 0 && mode <= 2) ? mode : 0; }
 void simplex_set_timer_dir(const char *dir) { g_cfg.timer_dir = dir ? dir : ""; }
 
 void enableBenchmarkMode(void) { g_cfg.benchmark = true; }

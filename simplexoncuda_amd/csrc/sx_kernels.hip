@@ -171,7 +171,7 @@ __device__ __forceinline__ const double *row_src(const double *T, size_t ld, int
 __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__ T, int rows, int row0, size_t ld,
                                                       TilePart *tiles_local, double *colE, DevState *st, int *base,
                                                       const double *__restrict__ rnew, size_t rnew_stride,
-                                                      int select) {
+                                                      int select, double *slots, size_t slot_stride, int N) {
     if (st->status != SX_NOT_ENDED) return;
     const bool leader = blockIdx.x == 0 && threadIdx.x == 0;
     const long long piv = st->pivots;
@@ -212,10 +212,30 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
     const int any = __syncthreads_or(elig);
     block_argmin512(rv, ri, s_v, s_i);
     if (!select) {
+        if (slots == nullptr) {
+            if (threadIdx.x == 0) {
+                tiles_local[blockIdx.x].v = rv;
+                tiles_local[blockIdx.x].idx = ri;
+                tiles_local[blockIdx.x].elig = any;
+            }
+            return;
+        }
+        // row-gather exchange: the slot carries the tile winner and that row's current
+        // values, so one allgather hands every rank the pivot row whichever tile wins
+        __shared__ int s_ri;
+        double *slot = slots + (size_t)blockIdx.x * slot_stride;
         if (threadIdx.x == 0) {
-            tiles_local[blockIdx.x].v = rv;
-            tiles_local[blockIdx.x].idx = ri;
-            tiles_local[blockIdx.x].elig = any;
+            TilePart *h = reinterpret_cast<TilePart *>(slot);
+            h->v = rv;
+            h->idx = ri;
+            h->elig = any;
+            s_ri = ri;
+        }
+        __syncthreads();
+        const int wl = s_ri - row0;
+        if (s_ri >= 0) {
+            const double *src = row_src(T, ld, wl, pend, rcur);
+            for (int j = threadIdx.x; j < N; j += SX_TILE) slot[2 + j] = src[j];
         }
         return;
     }
@@ -313,6 +333,42 @@ __global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T
     }
 }
 
+// K3 (row-gather exchange): one block picks the leaving row among the gathered tile
+// winners (the reference's pass-2 tree), checks the unbounded condition and records the
+// pivot; the update then reads the pivot row from the winning slot.
+__global__ __launch_bounds__(512) void k_select_gathered(const double *__restrict__ slots, size_t slot_stride, int B2,
+                                                         int *base, DevState *st) {
+    if (st->status != SX_NOT_ENDED) return;
+    __shared__ double s_v[16];
+    __shared__ int s_i[16];
+    double v = DBL_MAX;
+    int r = -1, elig = 0;
+    if ((int)threadIdx.x < B2) {
+        const TilePart *h = reinterpret_cast<const TilePart *>(slots + (size_t)threadIdx.x * slot_stride);
+        elig = h->elig;
+        const double c = h->v;
+        if (cmp_eps(c, v) < 0) {
+            v = c;
+            r = h->idx;
+        }
+    }
+    if (!__syncthreads_or(elig)) {
+        if (threadIdx.x == 0) st->status = SX_UNBOUNDED;  // solver.cu:96-102
+        return;
+    }
+    block_argmin512(v, r, s_v, s_i);
+    if (threadIdx.x == 0) {
+        if (r < 0) {
+            st->status = SX_NUMERIC_FAIL;
+        } else {
+            base[r] = st->e;  // solver.cu:105
+            st->r_prev = st->r;
+            st->r = r;
+            st->pivots += 1;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // K4: the rank-1 pivot update (updateContraintsMatrix + updateCostsVector, solver.cu:34-56)
 //   row r:       rnew[q&1][j] = prow[j] / p     (q = pivot number; written back to T by the
@@ -331,7 +387,7 @@ __global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T
 template <int RB, bool SNAKE>
 __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows, int row0, size_t ld, int N,
                                                 double *__restrict__ d, const double *__restrict__ prow_buf,
-                                                const double *__restrict__ colE, DevState *st,
+                                                size_t prow_stride, const double *__restrict__ colE, DevState *st,
                                                 double *__restrict__ rnew, size_t rnew_stride,
                                                 TilePart *enter_parts) {
     if (st->status != SX_NOT_ENDED) return;
@@ -341,7 +397,8 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows
     const int pl = (q >= 2 && st->r_prev != st->r) ? st->r_prev - row0 : -1;  // pending row, local
     const double *rprev = rnew + (size_t)((q - 1) & 1) * rnew_stride;
     double *rout = rnew + (size_t)(q & 1) * rnew_stride;
-    const double *prow = prow_buf ? prow_buf : ((q >= 2 && st->r_prev == st->r) ? rprev : T + (size_t)rl * ld);
+    const double *prow = prow_buf ? (prow_stride ? prow_buf + (size_t)(st->r / SX_TILE) * prow_stride + 2 : prow_buf)
+                                  : ((q >= 2 && st->r_prev == st->r) ? rprev : T + (size_t)rl * ld);
     const double p = prow[1 + e];
     if (blockIdx.y == 0) {
         // ---- objective row + next entering argmin (512 reference threads on 256)
@@ -640,12 +697,18 @@ void sx_launch_enter(const double *d, int L, TilePart *parts, DevState *st, hipS
 
 void sx_launch_ratio_select(const double *T, int rows, int row0, size_t ld, TilePart *tiles_local, double *colE,
                             DevState *st, int *base, const double *rnew, size_t rnew_stride, bool select,
-                            hipStream_t s) {
+                            double *slots, size_t slot_stride, int N, hipStream_t s) {
     int g = (rows + SX_TILE - 1) / SX_TILE;
     if (g < 1) g = 1;  // a shard without rows still decides optimality for its own state
     if (select && g > SX_TILE) SX_FATAL("too many ratio tiles for the 512-thread pass 2");
     k_ratio_select<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, tiles_local, colE, st, base, rnew, rnew_stride,
-                                         select ? 1 : 0);
+                                         select ? 1 : 0, slots, slot_stride, N);
+}
+
+void sx_launch_select_gathered(const double *slots, size_t slot_stride, int B2, int *base, DevState *st,
+                               hipStream_t s) {
+    if (B2 > SX_TILE) SX_FATAL("too many ratio tiles for the 512-thread pass 2");
+    k_select_gathered<<<1, SX_TILE, 0, s>>>(slots, slot_stride, B2, base, st);
 }
 
 void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, int N, const TilePart *tiles_all, int B2,
@@ -660,19 +723,19 @@ void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, int N,
 
 template <int RB>
 static void launch_update_rb(dim3 grid, bool snake, double *T, int rows, int row0, size_t ld, int N, double *d,
-                             const double *prow_buf, const double *colE, DevState *st, double *rnew,
-                             size_t rnew_stride, TilePart *enter_parts, hipStream_t s) {
+                             const double *prow_buf, size_t prow_stride, const double *colE, DevState *st,
+                             double *rnew, size_t rnew_stride, TilePart *enter_parts, hipStream_t s) {
     if (snake)
-        k_update<RB, true><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, rnew_stride,
-                                                enter_parts);
+        k_update<RB, true><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew,
+                                                rnew_stride, enter_parts);
     else
-        k_update<RB, false><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, rnew_stride,
-                                                 enter_parts);
+        k_update<RB, false><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew,
+                                                 rnew_stride, enter_parts);
 }
 
 void sx_launch_update(double *T, int rows, int row0, size_t ld, int N, double *d, const double *prow_buf,
-                      const double *colE, DevState *st, double *rnew, size_t rnew_stride, TilePart *enter_parts,
-                      UpdateCfg cfg, hipStream_t s) {
+                      size_t prow_stride, const double *colE, DevState *st, double *rnew, size_t rnew_stride,
+                      TilePart *enter_parts, UpdateCfg cfg, hipStream_t s) {
     const int cols_blocks = (N + 511) / 512;
     const int B1 = (N - 1 + SX_TILE - 1) / SX_TILE;
     if (B1 > cols_blocks || B1 > 256) SX_FATAL("update grid too narrow for the entering partials");
@@ -681,10 +744,10 @@ void sx_launch_update(double *T, int rows, int row0, size_t ld, int N, double *d
     dim3 grid(cols_blocks, rg + 1);
     const bool sn = cfg.snake != 0;
     switch (rb) {
-    case 1: launch_update_rb<1>(grid, sn, T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, rnew_stride, enter_parts, s); break;
-    case 2: launch_update_rb<2>(grid, sn, T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, rnew_stride, enter_parts, s); break;
-    case 4: launch_update_rb<4>(grid, sn, T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, rnew_stride, enter_parts, s); break;
-    default: launch_update_rb<8>(grid, sn, T, rows, row0, ld, N, d, prow_buf, colE, st, rnew, rnew_stride, enter_parts, s); break;
+    case 1: launch_update_rb<1>(grid, sn, T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, rnew_stride, enter_parts, s); break;
+    case 2: launch_update_rb<2>(grid, sn, T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, rnew_stride, enter_parts, s); break;
+    case 4: launch_update_rb<4>(grid, sn, T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, rnew_stride, enter_parts, s); break;
+    default: launch_update_rb<8>(grid, sn, T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, rnew_stride, enter_parts, s); break;
     }
 }
 

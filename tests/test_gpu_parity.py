@@ -209,16 +209,20 @@ def test_update_configs_bit_exact(gpu, rb, snake):
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 
-@pytest.mark.parametrize("W", [1, 2])
-def test_exchange_path_bit_exact(gpu, W):
-    """the multi-shard kernels (tile allgather, select+row copy, -0.0 allreduce, update from the
-    exchanged row) on virtual shards -- W=1 runs them with a single shard"""
+@pytest.mark.parametrize("W", [1, 2, 3])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_exchange_path_bit_exact(gpu, W, mode):
+    """the multi-shard kernels on virtual shards (W=1 runs them with a single shard):
+    mode 1 = tile allgather + select/row copy + -0.0 allreduce; mode 2 = one allgather of
+    tile winners with their rows + single-block select"""
     p = sx.generateRandomProblem(300, 1100, 300 * 100 + 1100, 1, 100)
     try:
         sx.set_virtual_ranks(W)
         sx.set_force_exchange(1)
+        sx.set_exchange_mode(mode)
         got, _ = _check_two_phase(p)
     finally:
+        sx.set_exchange_mode(0)
         sx.set_force_exchange(0)
         sx.set_virtual_ranks(1)
     assert got.status == sx.FEASIBLE
