@@ -181,7 +181,7 @@ def main():
         "data": f"synthetic: generateRandomProblem(n={n}, m={m}, seed={seed}, [1,100]) (generator.cu/cuRAND-XORWOW restatement)",
         "config": {
             "workload": f"{args.config}: phase-1 pivots, {m}x{N1} fp64 tableau (m={m}, n={n})",
-            "m": m, "n": n, "seed": seed, "tableau_width": tim.width,
+            "m": m, "n": n, "seed": seed, "tableau_width": tim.width, "stored_width": tim.stored_width,
             "rows_per_gpu_rank0": tim.local_rows, "parallelism": f"row-block x{world}",
             "pivots_timed": pivots, "status_after": tim.status,
         },

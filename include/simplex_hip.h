@@ -45,6 +45,8 @@ void simplex_set_force_exchange(int on);
 /* per-pivot exchange between shards: 0 auto, 1 tile-winner allgather + pivot-row allreduce,
  * 2 one allgather of tile winners together with their rows (auto: when <= 1 MiB per rank) */
 void simplex_set_exchange_mode(int mode);
+/* store each phase-1 artificial column as its (bit-identical) slack column: 1 on (default), 0 off */
+void simplex_set_alias(int on);
 
 /* ---- extended drop-in entry ---- */
 /* twoPhaseMethod + final basis (base_out[m]) and per-phase pivot counts (pivots_out[2]);
@@ -68,9 +70,10 @@ typedef struct {
     long long pivots;          /* pivots applied during the call */
     long long update_launches; /* update kernel launches timed */
     int status;                /* phase status after the call (SIMPLEX_NOT_ENDED while running) */
-    int width;                 /* tableau width N of the phase */
+    int width;                 /* tableau width N of the phase (reference counting) */
+    int stored_width;          /* columns actually stored and swept (artificials alias slacks in phase 1) */
     long long local_rows;      /* constraint rows owned by this process */
-    double update_bytes;       /* algorithmic bytes per update launch: 16 * (local_rows + 1) * N */
+    double update_bytes;       /* algorithmic bytes per update launch: 16 * local_rows * stored_width + 16 * N */
 } simplex_timing_t;
 
 typedef struct simplex_session simplex_session;

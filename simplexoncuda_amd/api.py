@@ -244,6 +244,10 @@ def set_exchange_mode(mode):
     _lib.load().simplex_set_exchange_mode(int(mode))
 
 
+def set_alias(on):
+    _lib.load().simplex_set_alias(1 if on else 0)
+
+
 def set_verbose(on):
     _lib.load().simplex_set_verbose(1 if on else 0)
 

@@ -54,6 +54,18 @@ void sx_handle_error(hipError_t err, const char *file, int line);
 void sx_fatal(const char *msg, const char *file, int line);
 #define SX_FATAL(msg) sx_fatal((msg), __FILE__, __LINE__)
 
+// Logical vs stored tableau columns.  In phase 1 every artificial column n+m+k starts equal
+// to its slack column n+k (both unit vectors, both negated by the b<0 quirk) and receives
+// exactly the same IEEE operations at every pivot, so the two stay bit-identical: only
+// Ns = 1+n+m columns are stored and logical column j >= art0 reads stored column j - shift.
+struct Cols {
+    int N;      // logical columns of the phase (reference width: 1+n+2m or 1+n+m)
+    int Ns;     // stored columns (swept by the update)
+    int art0;   // first aliased logical column, or INT_MAX
+    int shift;  // alias distance (m)
+    __host__ __device__ __forceinline__ int map(int j) const { return j >= art0 ? j - shift : j; }
+};
+
 // ---- kernel launchers (sx_kernels.hip) ----
 struct UpdateCfg {
     int rows_per_block;  // 1, 2, 4 or 8
@@ -64,25 +76,25 @@ int sx_enter_blocks(int L);
 void sx_launch_enter(const double *d, int L, TilePart *parts, DevState *st, hipStream_t s);
 void sx_launch_ratio_select(const double *T, int rows, int row0, size_t ld, TilePart *tiles_local, double *colE,
                             DevState *st, int *base, const double *rnew, size_t rnew_stride, bool select,
-                            double *slots, size_t slot_stride, int N, hipStream_t s);
+                            double *slots, size_t slot_stride, Cols c, hipStream_t s);
 void sx_launch_select_gathered(const double *slots, size_t slot_stride, int B2, int *base, DevState *st,
                                hipStream_t s);
-void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, int N, const TilePart *tiles_all, int B2,
+void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, Cols c, const TilePart *tiles_all, int B2,
                           double *prow_out, int *base, DevState *st, const double *rnew, size_t rnew_stride,
                           hipStream_t s);
-void sx_launch_update(double *T, int rows, int row0, size_t ld, int N, double *d, const double *prow_buf,
+void sx_launch_update(double *T, int rows, int row0, size_t ld, Cols c, double *d, const double *prow_buf,
                       size_t prow_stride, const double *colE, DevState *st, double *rnew, size_t rnew_stride,
                       TilePart *enter_parts, UpdateCfg cfg, hipStream_t s);
-void sx_launch_flush_row(double *T, int rows, int row0, size_t ld, int N, const double *rnew, size_t rnew_stride,
+void sx_launch_flush_row(double *T, int rows, int row0, size_t ld, int Ns, const double *rnew, size_t rnew_stride,
                          const DevState *st, hipStream_t s);
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s);
 
 void sx_launch_coef(const double *d, const int *base, int row0, int rows, double *coef, hipStream_t s);
-void sx_launch_gemv_partials(const double *T, int rows, size_t ld, int N, const double *coef, double *partials,
+void sx_launch_gemv_partials(const double *T, int rows, size_t ld, int Ns, const double *coef, double *partials,
                              hipStream_t s);
-void sx_launch_gemv_apply(double *d, int N, const double *partials, int nblk, hipStream_t s);
+void sx_launch_gemv_apply(double *d, Cols c, const double *partials, int nblk, hipStream_t s);
 
-void sx_launch_build_rows(double *T, int rows, int row0, size_t ld, int n, int m, const double *A_local,
+void sx_launch_build_rows(double *T, int rows, int row0, size_t ld, int n, int m, int Ns, const double *A_local,
                           const double *b_full, hipStream_t s);
 void sx_launch_init_vectors(double *d, int N1, int n, int m, int *base, hipStream_t s);
 void sx_launch_phase2_costs(double *d, int n, int m, const double *c, hipStream_t s);

@@ -57,6 +57,7 @@ struct Config {
     int force_exchange = 0;  // run the multi-shard exchange path even with one shard
     std::string timer_dir;   // non-empty: write the reference's TIMER CSV there
     int exchange_mode = 0;   // 0 auto, 1 tile allgather + row allreduce, 2 row-gather
+    int alias = 1;           // store phase-1 artificial columns as their slack columns
     bool benchmark = false;
     // distributed
     bool dist = false;
@@ -177,6 +178,8 @@ class Engine {
     bool rowgather = false;  // exchange path variant: one allgather of tile winners with their rows
     size_t slot_stride = 0;  // doubles per row-gather slot (16-byte header + ld)
     int N1 = 0, N2 = 0, N = 0;
+    bool alias = false;    // phase-1 artificial columns stored as their slack columns (sx_common.hpp Cols)
+    int Ns1 = 0;           // stored columns in phase 1
     size_t ld = 0;         // row stride in doubles
     int rpr = 0;           // rows per rank (multiple of 512)
     int slots = 0;         // argmin tiles / GEMV blocks per rank
@@ -189,11 +192,13 @@ class Engine {
     double *c_dev = nullptr;            // objective coefficients c (phase 2)
     long long phase_pivots[2] = {0, 0};
 
-    Engine(int n_, int m_) : n(n_), m(m_) {
+    Engine(int n_, int m_, bool alias_ = true) : n(n_), m(m_) {
         N1 = 1 + n + 2 * m;
         N2 = 1 + n + m;
         N = N1;
-        ld = round_up((size_t)N1, 16);
+        alias = alias_ && g_cfg.alias && m > 0;
+        Ns1 = alias ? N2 : N1;
+        ld = round_up((size_t)Ns1, 16);
         if (g_cfg.dist && g_cfg.comm) {
             rccl = true;
             W = g_cfg.world;
@@ -253,7 +258,7 @@ class Engine {
     void alloc_shard(Shard &x) {
         const size_t rows_alloc = x.rows > 0 ? (size_t)x.rows : 1;
         x.T = dalloc<double>(rows_alloc * ld);
-        x.d = dalloc<double>(ld);
+        x.d = dalloc<double>(round_up((size_t)N1, 16));
         x.colE = dalloc<double>(rows_alloc);
         x.prow = dalloc<double>(ld);
         if (xchg) x.prow_send = dalloc<double>(ld);
@@ -279,7 +284,7 @@ class Engine {
         if (xchg) x.tiles_all = dalloc<TilePart>((size_t)W * slots);
         x.st = dalloc<DevState>(1);
         SX_HIP(hipMemsetAsync(x.T, 0, rows_alloc * ld * sizeof(double), s));
-        SX_HIP(hipMemsetAsync(x.d, 0, ld * sizeof(double), s));
+        SX_HIP(hipMemsetAsync(x.d, 0, round_up((size_t)N1, 16) * sizeof(double), s));
         SX_HIP(hipMemsetAsync(x.prow, 0, ld * sizeof(double), s));
         // padding tile entries must read (DBL_MAX, -1, not eligible)
         std::vector<TilePart> pad((size_t)W * slots);
@@ -313,7 +318,7 @@ class Engine {
                 SX_HIP(hipMemcpy2DAsync(A_local, sizeof(double) * x.rows, P->constraintsMatrix + x.row0,
                                         sizeof(double) * m, sizeof(double) * x.rows, n, hipMemcpyHostToDevice, s));
             }
-            sx_launch_build_rows(x.T, x.rows, x.row0, ld, n, m, A_local, b_dev, s);
+            sx_launch_build_rows(x.T, x.rows, x.row0, ld, n, m, Ns1, A_local, b_dev, s);
             sx_launch_init_vectors(x.d, N1, n, m, x.base, s);
             SX_HIP(hipStreamSynchronize(s));
             if (A_local) (void)hipFree(A_local);
@@ -355,10 +360,10 @@ class Engine {
     void allreduce_prow() {
         if (rccl) {
             Shard &x = sh[0];
-            SX_NCCL(ncclAllReduce(x.prow_send, x.prow, N, ncclDouble, ncclSum, g_cfg.comm, s));
+            SX_NCCL(ncclAllReduce(x.prow_send, x.prow, cols(N).Ns, ncclDouble, ncclSum, g_cfg.comm, s));
             return;
         }
-        for (auto &dst : sh) sx_launch_sum_rows(dst.prow, sum_srcs, W, N, s);
+        for (auto &dst : sh) sx_launch_sum_rows(dst.prow, sum_srcs, W, cols(N).Ns, s);
     }
 
     void allgather_doubles(double *Shard::*local, double *Shard::*all, size_t count) {
@@ -376,21 +381,33 @@ class Engine {
     // ---------------------------------------------------------------- objective GEMV
     // updateObjectiveFunction (gaussian.cu:132-162), deterministic blocked order.
     void update_objective(int width) {
-        const size_t part = (size_t)slots * width;
+        const Cols c = cols(width);
+        const size_t part = (size_t)slots * c.Ns;
         for (auto &x : sh) {
-            if (!x.gemv_local) x.gemv_local = dalloc<double>((size_t)slots * N1);
-            if (xchg && !x.gemv_all) x.gemv_all = dalloc<double>((size_t)W * slots * N1);
+            if (!x.gemv_local) x.gemv_local = dalloc<double>((size_t)slots * Ns1);
+            if (xchg && !x.gemv_all) x.gemv_all = dalloc<double>((size_t)W * slots * Ns1);
             SX_HIP(hipMemsetAsync(x.gemv_local, 0, part * sizeof(double), s));
             sx_launch_coef(x.d, x.base, x.row0, x.rows, x.coef, s);
-            sx_launch_gemv_partials(x.T, x.rows, ld, width, x.coef, x.gemv_local, s);
+            sx_launch_gemv_partials(x.T, x.rows, ld, c.Ns, x.coef, x.gemv_local, s);
         }
         if (xchg) allgather_doubles(&Shard::gemv_local, &Shard::gemv_all, part);
         const int nblk = (m + SX_TILE - 1) / SX_TILE;
-        for (auto &x : sh) sx_launch_gemv_apply(x.d, width, xchg ? x.gemv_all : x.gemv_local, nblk, s);
+        for (auto &x : sh) sx_launch_gemv_apply(x.d, c, xchg ? x.gemv_all : x.gemv_local, nblk, s);
     }
 
     void phase2_costs() {
         for (auto &x : sh) sx_launch_phase2_costs(x.d, n, m, c_dev, s);
+    }
+
+    // logical width of a phase -> stored columns
+    Cols cols(int width) const {
+        Cols c;
+        c.N = width;
+        const bool a = alias && width == N1;
+        c.Ns = a ? Ns1 : width;
+        c.art0 = a ? 1 + n + m : 0x7fffffff;
+        c.shift = m;
+        return c;
     }
 
     // ---------------------------------------------------------------- one pivot
@@ -399,7 +416,7 @@ class Engine {
         // per shard, 1 row above; reversing the sweep every other pivot pays once the shard's
         // tableau outgrows the 256 MB Infinity Cache.
         double bytes = 0.0;
-        for (auto &x : sh) bytes = std::max(bytes, 8.0 * (double)x.rows * (double)N);
+        for (auto &x : sh) bytes = std::max(bytes, 8.0 * (double)x.rows * (double)cols(N).Ns);
         UpdateCfg c;
         c.rows_per_block = g_cfg.update_rows > 0 ? g_cfg.update_rows : (bytes > 2.0e9 ? 1 : 2);
         c.snake = g_cfg.snake >= 0 ? g_cfg.snake : (bytes > 256.0 * 1024 * 1024 ? 1 : 0);
@@ -414,23 +431,24 @@ class Engine {
 
     void enqueue_pivot(hipEvent_t ev0, hipEvent_t ev1) {
         const UpdateCfg cfg = update_cfg();
+        const Cols c = cols(N);
         for (auto &x : sh)
             sx_launch_ratio_select(x.T, x.rows, x.row0, ld, x.tiles_local, x.colE, x.st, x.base, x.rnew, ld, !xchg,
-                                   rowgather ? x.slot_send : nullptr, slot_stride, N, s);
+                                   rowgather ? x.slot_send : nullptr, slot_stride, c, s);
         if (rowgather) {
             allgather_slots();
             for (auto &x : sh) sx_launch_select_gathered(x.slot_all, slot_stride, W * slots, x.base, x.st, s);
         } else if (xchg) {
             allgather_tiles();
             for (auto &x : sh)
-                sx_launch_select_row(x.T, x.rows, x.row0, ld, N, x.tiles_all, W * slots, x.prow_send, x.base, x.st,
+                sx_launch_select_row(x.T, x.rows, x.row0, ld, c, x.tiles_all, W * slots, x.prow_send, x.base, x.st,
                                      x.rnew, ld, s);
             allreduce_prow();
         }
         if (ev0) SX_HIP(hipEventRecord(ev0, s));
         for (auto &x : sh) {
             const double *pb = rowgather ? x.slot_all : (xchg ? x.prow : nullptr);
-            sx_launch_update(x.T, x.rows, x.row0, ld, N, x.d, pb, rowgather ? slot_stride : 0, x.colE, x.st, x.rnew,
+            sx_launch_update(x.T, x.rows, x.row0, ld, c, x.d, pb, rowgather ? slot_stride : 0, x.colE, x.st, x.rnew,
                              ld, x.enter_parts, cfg, s);
         }
         if (ev1) SX_HIP(hipEventRecord(ev1, s));
@@ -438,7 +456,7 @@ class Engine {
 
     // write the last pivot row back into T (it is deferred to the next pivot's update)
     void flush() {
-        for (auto &x : sh) sx_launch_flush_row(x.T, x.rows, x.row0, ld, N, x.rnew, ld, x.st, s);
+        for (auto &x : sh) sx_launch_flush_row(x.T, x.rows, x.row0, ld, cols(N).Ns, x.rnew, ld, x.st, s);
     }
 
     void reset_state(long long max_pivots) {
@@ -540,22 +558,35 @@ class Engine {
         SX_HIP(hipStreamSynchronize(s));
     }
 
-    // rows of the whole tableau (virtual or single shard only): for tests and printing
+    // rows of the whole tableau (virtual or single shard only), logical columns: for tests
+    // and printing (aliased artificial columns are expanded from their slack columns)
     void download(double *T_host, size_t ld_host, int width, double *d_host) {
-        for (auto &x : sh)
-            if (x.rows > 0)
-                SX_HIP(hipMemcpy2DAsync(T_host + (size_t)x.row0 * ld_host, ld_host * sizeof(double), x.T,
-                                        ld * sizeof(double), width * sizeof(double), x.rows,
-                                        hipMemcpyDeviceToHost, s));
+        const Cols c = cols(width);
+        std::vector<double> tmp;
+        for (auto &x : sh) {
+            if (x.rows <= 0) continue;
+            tmp.assign((size_t)x.rows * c.Ns, 0.0);
+            SX_HIP(hipMemcpy2DAsync(tmp.data(), c.Ns * sizeof(double), x.T, ld * sizeof(double), c.Ns * sizeof(double),
+                                    x.rows, hipMemcpyDeviceToHost, s));
+            SX_HIP(hipStreamSynchronize(s));
+            for (int i = 0; i < x.rows; ++i) {
+                double *dst = T_host + (size_t)(x.row0 + i) * ld_host;
+                const double *src = tmp.data() + (size_t)i * c.Ns;
+                for (int j = 0; j < width; ++j) dst[j] = src[c.map(j)];
+            }
+        }
         if (d_host) SX_HIP(hipMemcpyAsync(d_host, sh[0].d, sizeof(double) * width, hipMemcpyDeviceToHost, s));
         SX_HIP(hipStreamSynchronize(s));
     }
 
+    // logical columns in; with aliasing only the stored columns are taken (the caller's
+    // artificial columns must equal the slack columns, checked by the callers below)
     void upload(const double *T_host, size_t ld_host, int width, const double *d_host, const int *base_host) {
+        const Cols c = cols(width);
         for (auto &x : sh) {
             if (x.rows > 0)
                 SX_HIP(hipMemcpy2DAsync(x.T, ld * sizeof(double), T_host + (size_t)x.row0 * ld_host,
-                                        ld_host * sizeof(double), width * sizeof(double), x.rows,
+                                        ld_host * sizeof(double), c.Ns * sizeof(double), x.rows,
                                         hipMemcpyHostToDevice, s));
             if (d_host) SX_HIP(hipMemcpyAsync(x.d, d_host, sizeof(double) * width, hipMemcpyHostToDevice, s));
             if (base_host) SX_HIP(hipMemcpyAsync(x.base, base_host, sizeof(int) * m, hipMemcpyHostToDevice, s));
@@ -563,6 +594,18 @@ class Engine {
         SX_HIP(hipStreamSynchronize(s));
     }
 };
+
+// true when a caller's phase-1-width tableau has every artificial column bit-identical to
+// its slack column (so the aliased storage represents it exactly)
+static bool artificial_equals_slack(const double *T, long long m, long long N, long long ld) {
+    const long long n = N - 1 - 2 * m;
+    if (n < 0 || m <= 0) return false;
+    for (long long i = 0; i < m; ++i) {
+        const double *row = T + i * ld;
+        if (std::memcmp(row + 1 + n, row + 1 + n + m, sizeof(double) * (size_t)m) != 0) return false;
+    }
+    return true;
+}
 
 // tabular_t <-> engine
 std::map<const tabular_t *, Engine *> g_tabs;
@@ -656,6 +699,7 @@ void simplex_set_device(int device) {
 }
 void simplex_set_virtual_ranks(int world) { g_cfg.virtual_ranks = world > 1 ? world : 1; }
 void simplex_set_force_exchange(int on) { g_cfg.force_exchange = on ? 1 : 0; }
+void simplex_set_alias(int on) { g_cfg.alias = on ? 1 : 0; }
 void simplex_set_exchange_mode(int mode) { g_cfg.exchange_mode = (mode >= 0 && mode <= 2) ? mode : 0; }
 void simplex_set_timer_dir(const char *dir) { g_cfg.timer_dir = dir ? dir : ""; }
 
@@ -814,7 +858,8 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
     long long rows = 0;
     for (auto &x : E.sh) rows += x.rows;
     t.local_rows = rows;
-    t.update_bytes = 16.0 * (double)(rows + 1) * (double)E.N;
+    t.stored_width = E.cols(E.N).Ns;
+    t.update_bytes = 16.0 * (double)rows * (double)t.stored_width + 16.0 * (double)E.N;
     double sum = 0.0;
     for (long long i = 0; i < nt; ++i) {
         float u = 0.f;
@@ -866,9 +911,10 @@ long long simplex_dev_argmin(const double *v, long long L, double *vmin) {
 
 int simplex_dev_pivots(double *T, long long m, long long N, long long ld, double *d, int *base, long long k,
                        long long *done) {
-    // a scratch engine sized for width N: n + 2m + 1 >= N is all it needs
-    Engine E((int)(N - 1 - 2 * m) > 0 ? (int)(N - 1 - 2 * m) : 0, (int)m);
-    if ((long long)E.ld < N) SX_FATAL("simplex_dev_pivots: width exceeds engine stride");
+    // a scratch engine sized for width N: n + 2m + 1 >= N is all it needs; aliased storage
+    // only when the caller's tableau satisfies the invariant
+    Engine E((int)(N - 1 - 2 * m) > 0 ? (int)(N - 1 - 2 * m) : 0, (int)m, artificial_equals_slack(T, m, N, ld));
+    if ((long long)E.cols((int)N).Ns > (long long)E.ld) SX_FATAL("simplex_dev_pivots: width exceeds engine stride");
     E.upload(T, (size_t)ld, (int)N, d, base);
     long long piv = 0;
     const int st = E.run_phase((int)N, k, &piv);
@@ -880,8 +926,8 @@ int simplex_dev_pivots(double *T, long long m, long long N, long long ld, double
 
 int simplex_dev_update_objective(const double *T, long long m, long long N, long long ld, const int *base,
                                  double *d) {
-    Engine E((int)(N - 1 - 2 * m) > 0 ? (int)(N - 1 - 2 * m) : 0, (int)m);
-    if ((long long)E.ld < N) SX_FATAL("simplex_dev_update_objective: width exceeds engine stride");
+    Engine E((int)(N - 1 - 2 * m) > 0 ? (int)(N - 1 - 2 * m) : 0, (int)m, artificial_equals_slack(T, m, N, ld));
+    if ((long long)E.cols((int)N).Ns > (long long)E.ld) SX_FATAL("simplex_dev_update_objective: width exceeds engine stride");
     E.upload(T, (size_t)ld, (int)N, d, base);
     E.update_objective((int)N);
     SX_HIP(hipStreamSynchronize(E.s));

@@ -171,7 +171,7 @@ __device__ __forceinline__ const double *row_src(const double *T, size_t ld, int
 __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__ T, int rows, int row0, size_t ld,
                                                       TilePart *tiles_local, double *colE, DevState *st, int *base,
                                                       const double *__restrict__ rnew, size_t rnew_stride,
-                                                      int select, double *slots, size_t slot_stride, int N) {
+                                                      int select, double *slots, size_t slot_stride, Cols c) {
     if (st->status != SX_NOT_ENDED) return;
     const bool leader = blockIdx.x == 0 && threadIdx.x == 0;
     const long long piv = st->pivots;
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
     int elig = 0;
     if (li < rows) {
         const double *row = row_src(T, ld, li, pend, rcur);
-        const double a = row[1 + e];
+        const double a = row[c.map(1 + e)];
         const double b = row[0];
         colE[li] = a;
         elig = a >= SX_EPS;
@@ -235,7 +235,7 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
         const int wl = s_ri - row0;
         if (s_ri >= 0) {
             const double *src = row_src(T, ld, wl, pend, rcur);
-            for (int j = threadIdx.x; j < N; j += SX_TILE) slot[2 + j] = src[j];
+            for (int j = threadIdx.x; j < c.Ns; j += SX_TILE) slot[2 + j] = src[j];
         }
         return;
     }
@@ -289,7 +289,7 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
 // here).  Only the owner contributes the row; the others contribute -0.0, the exact
 // additive identity, so the sum-allreduce reproduces the owner's row bit for bit.
 __global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T, int rows, int row0, size_t ld,
-                                                    int N, const TilePart *__restrict__ tiles_all, int B2,
+                                                    int Ns, const TilePart *__restrict__ tiles_all, int B2,
                                                     double *prow_out, int *base, DevState *st,
                                                     const double *__restrict__ rnew, size_t rnew_stride) {
     if (st->status != SX_NOT_ENDED) return;
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T
     const int pend = piv > 0 ? st->r - row0 : -1;
     const bool own = r >= row0 && r < row0 + rows;
     const double *src = own ? row_src(T, ld, r - row0, pend, rnew + (size_t)(piv & 1) * rnew_stride) : T;
-    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < N; j += gridDim.x * blockDim.x)
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < Ns; j += gridDim.x * blockDim.x)
         prow_out[j] = own ? src[j] : -0.0;
     // commit the pivot once every block has read the state above: the last block to
     // arrive does it (the next kernel sees it after the launch boundary)
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(512) void k_select_gathered(const double *__restric
 // is reversed on every other pivot, so a sweep starts on the lines the previous one wrote
 // last -- still resident in the 256 MB Infinity Cache.
 template <int RB, bool SNAKE>
-__global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows, int row0, size_t ld, int N,
+__global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows, int row0, size_t ld, Cols c,
                                                 double *__restrict__ d, const double *__restrict__ prow_buf,
                                                 size_t prow_stride, const double *__restrict__ colE, DevState *st,
                                                 double *__restrict__ rnew, size_t rnew_stride,
@@ -399,13 +399,13 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows
     double *rout = rnew + (size_t)(q & 1) * rnew_stride;
     const double *prow = prow_buf ? (prow_stride ? prow_buf + (size_t)(st->r / SX_TILE) * prow_stride + 2 : prow_buf)
                                   : ((q >= 2 && st->r_prev == st->r) ? rprev : T + (size_t)rl * ld);
-    const double p = prow[1 + e];
+    const double p = prow[c.map(1 + e)];
     if (blockIdx.y == 0) {
         // ---- objective row + next entering argmin (512 reference threads on 256)
         __shared__ double s_v[16];
         __shared__ int s_i[16];
         __shared__ int s_last;
-        const int L = N - 1;
+        const int L = c.N - 1;
         const int B1 = (L + SX_TILE - 1) / SX_TILE;
         if ((int)blockIdx.x >= B1) return;
         const double fd = -st->dmin / p;
@@ -414,7 +414,7 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows
         int i0 = -1, i1 = -1;
         const int ia = blockIdx.x * SX_TILE + threadIdx.x, ib = ia + 256;
         if (ia < L) {
-            const double x = fma(fd, prow[1 + ia], d[1 + ia]);
+            const double x = fma(fd, prow[c.map(1 + ia)], d[1 + ia]);
             d[1 + ia] = x;
             if (cmp_eps(x, v0) < 0) {
                 v0 = x;
@@ -422,7 +422,7 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows
             }
         }
         if (ib < L) {
-            const double x = fma(fd, prow[1 + ib], d[1 + ib]);
+            const double x = fma(fd, prow[c.map(1 + ib)], d[1 + ib]);
             d[1 + ib] = x;
             if (cmp_eps(x, v1) < 0) {
                 v1 = x;
@@ -485,9 +485,12 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows
         return;
     }
     const int rg = gridDim.y - 1;  // row groups of T
+    const int N = c.Ns;            // stored columns
+    const int cb = (N + 511) / 512;
+    if ((int)blockIdx.x >= cb) return;
     int bx = blockIdx.x, by = blockIdx.y - 1;
     if (SNAKE && (q & 1)) {
-        bx = gridDim.x - 1 - bx;
+        bx = cb - 1 - bx;
         by = rg - 1 - by;
     }
     __shared__ double s_f[RB];
@@ -555,14 +558,14 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows
 }
 
 // Phase end: write the last pivot row back from rnew[pivots & 1] (idempotent).
-__global__ void k_flush_row(double *T, int rows, int row0, size_t ld, int N, const double *rnew, size_t rnew_stride,
+__global__ void k_flush_row(double *T, int rows, int row0, size_t ld, int Ns, const double *rnew, size_t rnew_stride,
                             const DevState *st) {
     const long long q = st->pivots;
     if (q <= 0) return;
     const int rl = st->r - row0;
     if (rl < 0 || rl >= rows) return;
     const double *src = rnew + (size_t)(q & 1) * rnew_stride;
-    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < N; j += gridDim.x * blockDim.x)
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < Ns; j += gridDim.x * blockDim.x)
         T[(size_t)rl * ld + j] = src[j];
 }
 
@@ -608,11 +611,12 @@ __global__ __launch_bounds__(256) void k_gemv_partials(const double *__restrict_
     partials[(size_t)k * N + j] = s;
 }
 
-__global__ void k_gemv_apply(double *d, int N, const double *__restrict__ partials, int nblk) {
+__global__ void k_gemv_apply(double *d, Cols c, const double *__restrict__ partials, int nblk) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= N) return;
-    double s = partials[j];
-    for (int k = 1; k < nblk; ++k) s = s + partials[(size_t)k * N + j];
+    if (j >= c.N) return;
+    const int js = c.map(j);  // an artificial column's sum is its slack column's (identical columns)
+    double s = partials[js];
+    for (int k = 1; k < nblk; ++k) s = s + partials[(size_t)k * c.Ns + js];
     d[j] = d[j] - s;
 }
 
@@ -637,15 +641,14 @@ __global__ __launch_bounds__(256) void k_fill_structural(double *T, int rows, si
 
 // RHS, slack/artificial identities, and the b<0 quirk: a row with compare(b_i) < 0 is
 // negated across ALL its entries, slack and artificial included.
-__global__ void k_fill_rows(double *T, int rows, int row0, size_t ld, int n, int m, const double *b_full) {
+__global__ void k_fill_rows(double *T, int rows, int row0, size_t ld, int n, int m, int Ns, const double *b_full) {
     const int i = blockIdx.y;
     if (i >= rows) return;
     const int gi = row0 + i;
     const double bi = b_full[gi];
     const bool neg = cmp_eps(bi, 0.0) < 0;
     double *row = T + (size_t)i * ld;
-    const int N1 = 1 + n + 2 * m;
-    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < N1; j += gridDim.x * blockDim.x) {
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < Ns; j += gridDim.x * blockDim.x) {
         double x;
         if (j == 0)
             x = bi;
@@ -697,12 +700,12 @@ void sx_launch_enter(const double *d, int L, TilePart *parts, DevState *st, hipS
 
 void sx_launch_ratio_select(const double *T, int rows, int row0, size_t ld, TilePart *tiles_local, double *colE,
                             DevState *st, int *base, const double *rnew, size_t rnew_stride, bool select,
-                            double *slots, size_t slot_stride, int N, hipStream_t s) {
+                            double *slots, size_t slot_stride, Cols c, hipStream_t s) {
     int g = (rows + SX_TILE - 1) / SX_TILE;
     if (g < 1) g = 1;  // a shard without rows still decides optimality for its own state
     if (select && g > SX_TILE) SX_FATAL("too many ratio tiles for the 512-thread pass 2");
     k_ratio_select<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, tiles_local, colE, st, base, rnew, rnew_stride,
-                                         select ? 1 : 0, slots, slot_stride, N);
+                                         select ? 1 : 0, slots, slot_stride, c);
 }
 
 void sx_launch_select_gathered(const double *slots, size_t slot_stride, int B2, int *base, DevState *st,
@@ -711,10 +714,11 @@ void sx_launch_select_gathered(const double *slots, size_t slot_stride, int B2, 
     k_select_gathered<<<1, SX_TILE, 0, s>>>(slots, slot_stride, B2, base, st);
 }
 
-void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, int N, const TilePart *tiles_all, int B2,
+void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, Cols c, const TilePart *tiles_all, int B2,
                           double *prow_out, int *base, DevState *st, const double *rnew, size_t rnew_stride,
                           hipStream_t s) {
     if (B2 > SX_TILE) SX_FATAL("too many ratio tiles for the 512-thread pass 2");
+    const int N = c.Ns;
     int g = (N + 4 * SX_TILE - 1) / (4 * SX_TILE);
     if (g < 1) g = 1;
     if (g > 64) g = 64;
@@ -722,7 +726,7 @@ void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, int N,
 }
 
 template <int RB>
-static void launch_update_rb(dim3 grid, bool snake, double *T, int rows, int row0, size_t ld, int N, double *d,
+static void launch_update_rb(dim3 grid, bool snake, double *T, int rows, int row0, size_t ld, Cols N, double *d,
                              const double *prow_buf, size_t prow_stride, const double *colE, DevState *st,
                              double *rnew, size_t rnew_stride, TilePart *enter_parts, hipStream_t s) {
     if (snake)
@@ -733,12 +737,13 @@ static void launch_update_rb(dim3 grid, bool snake, double *T, int rows, int row
                                                  rnew_stride, enter_parts);
 }
 
-void sx_launch_update(double *T, int rows, int row0, size_t ld, int N, double *d, const double *prow_buf,
+void sx_launch_update(double *T, int rows, int row0, size_t ld, Cols N, double *d, const double *prow_buf,
                       size_t prow_stride, const double *colE, DevState *st, double *rnew, size_t rnew_stride,
                       TilePart *enter_parts, UpdateCfg cfg, hipStream_t s) {
-    const int cols_blocks = (N + 511) / 512;
-    const int B1 = (N - 1 + SX_TILE - 1) / SX_TILE;
-    if (B1 > cols_blocks || B1 > 256) SX_FATAL("update grid too narrow for the entering partials");
+    const int B1 = (N.N - 1 + SX_TILE - 1) / SX_TILE;
+    if (B1 > 256) SX_FATAL("entering vector too long for the update's pass 2");
+    int cols_blocks = (N.Ns + 511) / 512;
+    if (cols_blocks < B1) cols_blocks = B1;
     const int rb = cfg.rows_per_block;
     const int rg = rows > 0 ? (rows + rb - 1) / rb : 0;
     dim3 grid(cols_blocks, rg + 1);
@@ -751,12 +756,12 @@ void sx_launch_update(double *T, int rows, int row0, size_t ld, int N, double *d
     }
 }
 
-void sx_launch_flush_row(double *T, int rows, int row0, size_t ld, int N, const double *rnew, size_t rnew_stride,
+void sx_launch_flush_row(double *T, int rows, int row0, size_t ld, int Ns, const double *rnew, size_t rnew_stride,
                          const DevState *st, hipStream_t s) {
     if (rows <= 0) return;
-    int g = (N + 255) / 256;
+    int g = (Ns + 255) / 256;
     if (g > 256) g = 256;
-    k_flush_row<<<g, 256, 0, s>>>(T, rows, row0, ld, N, rnew, rnew_stride, st);
+    k_flush_row<<<g, 256, 0, s>>>(T, rows, row0, ld, Ns, rnew, rnew_stride, st);
 }
 
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s) {
@@ -778,21 +783,20 @@ void sx_launch_gemv_partials(const double *T, int rows, size_t ld, int N, const 
     k_gemv_partials<<<grid, 256, 0, s>>>(T, rows, ld, N, coef, partials);
 }
 
-void sx_launch_gemv_apply(double *d, int N, const double *partials, int nblk, hipStream_t s) {
-    k_gemv_apply<<<(N + 255) / 256, 256, 0, s>>>(d, N, partials, nblk);
+void sx_launch_gemv_apply(double *d, Cols c, const double *partials, int nblk, hipStream_t s) {
+    k_gemv_apply<<<(c.N + 255) / 256, 256, 0, s>>>(d, c, partials, nblk);
 }
 
-void sx_launch_build_rows(double *T, int rows, int row0, size_t ld, int n, int m, const double *A_local,
+void sx_launch_build_rows(double *T, int rows, int row0, size_t ld, int n, int m, int Ns, const double *A_local,
                           const double *b_full, hipStream_t s) {
     if (rows <= 0) return;
     dim3 tb(32, 8);
     dim3 tg((rows + 31) / 32, (n + 31) / 32);
     if (n > 0) k_fill_structural<<<tg, tb, 0, s>>>(T, rows, ld, n, A_local);
-    const int N1 = 1 + n + 2 * m;
-    int gx = (N1 + 255) / 256;
+    int gx = (Ns + 255) / 256;
     if (gx > 64) gx = 64;
     dim3 rg(gx, rows);
-    k_fill_rows<<<rg, 256, 0, s>>>(T, rows, row0, ld, n, m, b_full);
+    k_fill_rows<<<rg, 256, 0, s>>>(T, rows, row0, ld, n, m, Ns, b_full);
 }
 
 void sx_launch_init_vectors(double *d, int N1, int n, int m, int *base, hipStream_t s) {

@@ -186,7 +186,8 @@ def test_session_pivots(gpu):
     t = s.pivots(50, time_updates=True)
     assert t.pivots == 50 and t.status == sx.NOT_ENDED and t.update_launches == 50
     assert t.update_ms > 0 and t.wall_ms >= t.update_ms
-    assert t.update_bytes == 16.0 * (1024 + 1) * (1 + 2048 + 2 * 1024)
+    assert t.stored_width == 1 + 2048 + 1024 and t.width == 1 + 2048 + 2 * 1024
+    assert t.update_bytes == 16.0 * 1024 * t.stored_width + 16.0 * t.width
     t2 = s.pivots(10000)
     assert s.total_pivots() == 2003 and t2.status == sx.FEASIBLE
     s.close()
@@ -237,3 +238,31 @@ def test_c_caller_drop_in(gpu, tmp_path):
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "status 0 z 64.000000 x0 8.000000" in r.stdout
+
+
+@pytest.mark.parametrize("alias", [0, 1])
+def test_alias_storage_on_off(gpu, alias):
+    """phase-1 artificial columns stored as their slack columns (default) or explicitly:
+    identical bits either way"""
+    p = sx.generateRandomProblem(129, 513, 77, -100, 100)
+    try:
+        sx.set_alias(alias)
+        _check_two_phase(p)
+        T, d, base = _phase1_state(200, 700, 5)
+        Tg, dg, bg = T.copy(), d.copy(), base.copy()
+        sx.dev_pivots(Tg, dg, bg, 40)
+        oracle.solve(T, d, base, max_pivots=40)
+        assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+    finally:
+        sx.set_alias(1)
+
+
+def test_pivots_without_alias_invariant(gpu):
+    """a tableau whose artificial columns differ from the slack columns is stored in full"""
+    T, d, base = _phase1_state(100, 300, 9)
+    n, m = 100, 300
+    T[5, 1 + n + m + 7] += 0.25  # break the artificial == slack invariant
+    Tg, dg, bg = T.copy(), d.copy(), base.copy()
+    sx.dev_pivots(Tg, dg, bg, 30)
+    oracle.solve(T, d, base, max_pivots=30)
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
