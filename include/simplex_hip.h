@@ -24,6 +24,7 @@ int simplex_version(void);
 void simplex_set_verbose(int on);            /* reference progress lines on stdout */
 void simplex_set_update_rows(int rb);        /* rows per update workgroup: 1, 2, 4, 8; 0 = auto */
 void simplex_set_snake(int mode);            /* alternate update sweep direction: -1 auto, 0, 1 */
+void simplex_set_store_sc1(int mode);        /* write-through tableau stores: -1 auto, 0, 1 */
 void simplex_set_batch(int pivots);          /* pivots enqueued between status polls */
 void simplex_set_device(int device);
 /* write the reference's -D TIMER CSV (chrono.cu) into `dir` (NULL or "" = off; env

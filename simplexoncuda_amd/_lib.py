@@ -82,6 +82,7 @@ SIGNATURES = {
     "simplex_set_verbose": (None, [ctypes.c_int]),
     "simplex_set_update_rows": (None, [ctypes.c_int]),
     "simplex_set_snake": (None, [ctypes.c_int]),
+    "simplex_set_store_sc1": (None, [ctypes.c_int]),
     "simplex_set_batch": (None, [ctypes.c_int]),
     "simplex_set_device": (None, [ctypes.c_int]),
     "simplex_set_timer_dir": (None, [ctypes.c_char_p]),

@@ -260,5 +260,9 @@ def set_snake(mode):
     _lib.load().simplex_set_snake(int(mode))
 
 
+def set_store_sc1(mode):
+    _lib.load().simplex_set_store_sc1(int(mode))
+
+
 def set_batch(p):
     _lib.load().simplex_set_batch(int(p))

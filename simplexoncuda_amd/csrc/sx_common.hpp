@@ -70,6 +70,7 @@ struct Cols {
 struct UpdateCfg {
     int rows_per_block;  // 1, 2, 4 or 8
     int snake;           // alternate the sweep direction every pivot
+    int sc1;             // write-through (sc1) tableau stores
 };
 
 int sx_enter_blocks(int L);

@@ -51,6 +51,7 @@ struct Config {
     int verbose = 0;
     int update_rows = 0;  // 0: auto (by tableau size)
     int snake = -1;       // -1: auto, 0: off, 1: on
+    int sc1 = -1;         // write-through tableau stores: -1 auto, 0, 1
     int batch = 16;
     int device = -1;
     int virtual_ranks = 1;
@@ -412,14 +413,19 @@ class Engine {
 
     // ---------------------------------------------------------------- one pivot
     UpdateCfg update_cfg() const {
-        // measured on MI355X (tools/bench_update.hip): 2 rows per block is best up to ~1 GB
-        // per shard, 1 row above; reversing the sweep every other pivot pays once the shard's
-        // tableau outgrows the 256 MB Infinity Cache.
+        // measured on MI355X (tools/bench_update.hip, stored shapes 1024x3073 .. 32768x40961):
+        // a tableau inside the 256 MB Infinity Cache streams best with 2 rows per block, plain
+        // stores, fixed order; above it, reversing the sweep every other pivot lets a sweep
+        // start on the lines the previous one left in the cache, and write-through (sc1)
+        // stores help; 1 row per block up to ~1 GB and beyond ~4 GB, 2 in between.
         double bytes = 0.0;
         for (auto &x : sh) bytes = std::max(bytes, 8.0 * (double)x.rows * (double)cols(N).Ns);
+        const bool big = bytes > 256.0 * 1024 * 1024;
         UpdateCfg c;
-        c.rows_per_block = g_cfg.update_rows > 0 ? g_cfg.update_rows : (bytes > 2.0e9 ? 1 : 2);
-        c.snake = g_cfg.snake >= 0 ? g_cfg.snake : (bytes > 256.0 * 1024 * 1024 ? 1 : 0);
+        c.rows_per_block = g_cfg.update_rows > 0 ? g_cfg.update_rows
+                                                 : (!big ? 2 : ((bytes <= 1.1e9 || bytes > 4.0e9) ? 1 : 2));
+        c.snake = g_cfg.snake >= 0 ? g_cfg.snake : (big ? 1 : 0);
+        c.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : (big ? 1 : 0);
         return c;
     }
 
@@ -692,6 +698,7 @@ int simplex_version(void) { return 1; }
 void simplex_set_verbose(int on) { g_cfg.verbose = on; }
 void simplex_set_update_rows(int rb) { g_cfg.update_rows = (rb == 1 || rb == 2 || rb == 4 || rb == 8) ? rb : 0; }
 void simplex_set_snake(int mode) { g_cfg.snake = mode < 0 ? -1 : (mode ? 1 : 0); }
+void simplex_set_store_sc1(int mode) { g_cfg.sc1 = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_batch(int pivots) { g_cfg.batch = pivots > 0 ? pivots : 16; }
 void simplex_set_device(int device) {
     g_cfg.device = device;

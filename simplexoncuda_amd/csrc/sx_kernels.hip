@@ -384,7 +384,20 @@ __global__ __launch_bounds__(512) void k_select_gathered(const double *__restric
 // load/store per row), a block covers 512 columns x RB rows.  With SNAKE the tile order
 // is reversed on every other pivot, so a sweep starts on the lines the previous one wrote
 // last -- still resident in the 256 MB Infinity Cache.
-template <int RB, bool SNAKE>
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte store of a tableau element pair: plain, or write-through (sc1) via a buffer
+// resource so the line leaves the XCD L2 at once (no dirty-L2 write-back at the end of the
+// launch, less L2 pollution on a once-touched stream)
+template <bool SC1>
+__device__ __forceinline__ void store_pair(double *p, double2 v, __amdgpu_buffer_rsrc_t rs, int byte_off) {
+    if (SC1)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, byte_off, 0, 16);
+    else
+        *reinterpret_cast<double2 *>(p) = v;
+}
+
+template <int RB, bool SNAKE, bool SC1>
 __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows, int row0, size_t ld, Cols c,
                                                 double *__restrict__ d, const double *__restrict__ prow_buf,
                                                 size_t prow_stride, const double *__restrict__ colE, DevState *st,
@@ -507,6 +520,8 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows
         const double2 pr = *reinterpret_cast<const double2 *>(prow + j);
         double *base = T + (size_t)i0 * ld + j;
         if (nrow == RB) {
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(T + (size_t)i0 * ld, 0, (int)(RB * ld * 8), 0x00020000);
             double2 x[RB];
 #pragma unroll
             for (int k = 0; k < RB; ++k)
@@ -523,7 +538,7 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows
                     const double f = s_f[k];
                     x[k].x = fma(f, pr.x, x[k].x);
                     x[k].y = fma(f, pr.y, x[k].y);
-                    *reinterpret_cast<double2 *>(base + (size_t)k * ld) = x[k];
+                    store_pair<SC1>(base + (size_t)k * ld, x[k], rs, (int)(((size_t)k * ld + j) * 8));
                 }
             }
         } else {
@@ -726,15 +741,24 @@ void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, Cols c
 }
 
 template <int RB>
-static void launch_update_rb(dim3 grid, bool snake, double *T, int rows, int row0, size_t ld, Cols N, double *d,
-                             const double *prow_buf, size_t prow_stride, const double *colE, DevState *st,
+static void launch_update_rb(dim3 grid, bool snake, bool sc1, double *T, int rows, int row0, size_t ld, Cols N,
+                             double *d, const double *prow_buf, size_t prow_stride, const double *colE, DevState *st,
                              double *rnew, size_t rnew_stride, TilePart *enter_parts, hipStream_t s) {
-    if (snake)
-        k_update<RB, true><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew,
-                                                rnew_stride, enter_parts);
-    else
-        k_update<RB, false><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew,
-                                                 rnew_stride, enter_parts);
+#define SX_UPD(SN, SC)                                                                                        \
+    k_update<RB, SN, SC><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, \
+                                              rnew_stride, enter_parts)
+    if (snake) {
+        if (sc1)
+            SX_UPD(true, true);
+        else
+            SX_UPD(true, false);
+    } else {
+        if (sc1)
+            SX_UPD(false, true);
+        else
+            SX_UPD(false, false);
+    }
+#undef SX_UPD
 }
 
 void sx_launch_update(double *T, int rows, int row0, size_t ld, Cols N, double *d, const double *prow_buf,
@@ -749,10 +773,10 @@ void sx_launch_update(double *T, int rows, int row0, size_t ld, Cols N, double *
     dim3 grid(cols_blocks, rg + 1);
     const bool sn = cfg.snake != 0;
     switch (rb) {
-    case 1: launch_update_rb<1>(grid, sn, T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, rnew_stride, enter_parts, s); break;
-    case 2: launch_update_rb<2>(grid, sn, T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, rnew_stride, enter_parts, s); break;
-    case 4: launch_update_rb<4>(grid, sn, T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, rnew_stride, enter_parts, s); break;
-    default: launch_update_rb<8>(grid, sn, T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, rnew_stride, enter_parts, s); break;
+    case 1: launch_update_rb<1>(grid, sn, cfg.sc1 != 0, T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, rnew_stride, enter_parts, s); break;
+    case 2: launch_update_rb<2>(grid, sn, cfg.sc1 != 0, T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, rnew_stride, enter_parts, s); break;
+    case 4: launch_update_rb<4>(grid, sn, cfg.sc1 != 0, T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, rnew_stride, enter_parts, s); break;
+    default: launch_update_rb<8>(grid, sn, cfg.sc1 != 0, T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, rnew_stride, enter_parts, s); break;
     }
 }
 

@@ -195,17 +195,21 @@ def test_session_pivots(gpu):
 
 @pytest.mark.parametrize("rb", [1, 2, 4, 8])
 @pytest.mark.parametrize("snake", [0, 1])
-def test_update_configs_bit_exact(gpu, rb, snake):
-    """every (rows per block, sweep order) variant of the update kernel gives the same bits"""
+@pytest.mark.parametrize("sc1", [0, 1])
+def test_update_configs_bit_exact(gpu, rb, snake, sc1):
+    """every (rows per block, sweep order, store flavour) variant of the update kernel gives
+    the same bits"""
     T, d, base = _phase1_state(333, 1025, 7)
     Tg, dg, bg = T.copy(), d.copy(), base.copy()
     try:
         sx.set_update_rows(rb)
         sx.set_snake(snake)
+        sx.set_store_sc1(sc1)
         sx.dev_pivots(Tg, dg, bg, 21)
     finally:
         sx.set_update_rows(0)
         sx.set_snake(-1)
+        sx.set_store_sc1(-1)
     oracle.solve(T, d, base, max_pivots=21)
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 

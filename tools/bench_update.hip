@@ -229,18 +229,19 @@ int main(int argc, char **argv) {
     Args a{T, m, ld, N, prow, f, m / 3, 37.5, 0};
     Variant vs[] = {
         {"rb2_c1", launch_var<2, 1, false, false>},
+        {"rb1_c1", launch_var<1, 1, false, false>},
+        {"rb4_c1", launch_var<4, 1, false, false>},
+        {"rb1_c1_snake", launch_var<1, 1, false, true>},
         {"rb2_c1_snake", launch_var<2, 1, false, true>},
         {"rb4_c1_snake", launch_var<4, 1, false, true>},
-        {"buf_rb2_snake_plain", launch_sc1<2, true, 0>},
+        {"rb8_c1_snake", launch_var<8, 1, false, true>},
+        {"rb2_c1_t128_snake", launch_var<2, 1, false, true, false, 128>},
+        {"rb2_c1_nts_snake", launch_var<2, 1, false, true, true>},
+        {"buf_rb1_snake_sc1", launch_sc1<1, true, 16>},
         {"buf_rb2_snake_sc1", launch_sc1<2, true, 16>},
         {"buf_rb4_snake_sc1", launch_sc1<4, true, 16>},
-        {"buf_rb2_sc1", launch_sc1<2, false, 16>},
         {"buf_rb1_sc1", launch_sc1<1, false, 16>},
-        {"buf_rb2_snake_nt", launch_sc1<2, true, 2>},
-        {"pair+rb2_snake", launch_pair<launch_var<2, 1, false, true>>},
-        {"pair+buf_rb2_snake_sc1", launch_pair<launch_sc1<2, true, 16>>},
-        {"pair+rb1", launch_pair<launch_var<1, 1, false, false>>},
-        {"pair+buf_rb1_sc1", launch_pair<launch_sc1<1, false, 16>>},
+        {"buf_rb2_sc1", launch_sc1<2, false, 16>},
     };
     const int nv = sizeof(vs) / sizeof(vs[0]);
     std::vector<double> ref((size_t)m * ld), out((size_t)m * ld);
