@@ -413,17 +413,17 @@ class Engine {
 
     // ---------------------------------------------------------------- one pivot
     UpdateCfg update_cfg() const {
-        // measured on MI355X (tools/bench_update.hip, stored shapes 1024x3073 .. 32768x40961):
-        // a tableau inside the 256 MB Infinity Cache streams best with 2 rows per block, plain
-        // stores, fixed order; above it, reversing the sweep every other pivot lets a sweep
+        // A/B in the real pivot loop (tools/sweep_update.py, interleaved rounds on MI355X):
+        // a shard inside the 256 MB Infinity Cache streams best with 2 rows per block, plain
+        // stores, fixed order.  Above it, reversing the sweep every other pivot lets a sweep
         // start on the lines the previous one left in the cache, and write-through (sc1)
-        // stores help; 1 row per block up to ~1 GB and beyond ~4 GB, 2 in between.
+        // stores help: config 3 (0.8 GB stored) 117 us vs 142 us with neither; beyond ~4 GB
+        // 1 row per block is best (config 5 on one GPU, 21 GB: 3.82 ms vs 4.05 ms).
         double bytes = 0.0;
         for (auto &x : sh) bytes = std::max(bytes, 8.0 * (double)x.rows * (double)cols(N).Ns);
         const bool big = bytes > 256.0 * 1024 * 1024;
         UpdateCfg c;
-        c.rows_per_block = g_cfg.update_rows > 0 ? g_cfg.update_rows
-                                                 : (!big ? 2 : ((bytes <= 1.1e9 || bytes > 4.0e9) ? 1 : 2));
+        c.rows_per_block = g_cfg.update_rows > 0 ? g_cfg.update_rows : (bytes > 4.0e9 ? 1 : 2);
         c.snake = g_cfg.snake >= 0 ? g_cfg.snake : (big ? 1 : 0);
         c.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : (big ? 1 : 0);
         return c;
