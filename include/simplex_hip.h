@@ -63,6 +63,9 @@ problem_t *simplex_problem_from_arrays(int n, int m, const double *A_colmajor, c
  * published pivot counts), 1 = glibc rand() */
 problem_t *simplex_generate_problem_ex(int n, int m, unsigned int seed, int lo, int hi, int rand_kind);
 void simplex_free_problem_struct(problem_t *problem);
+/* generateRandomProblem computed on the GPU (jump-ahead XORWOW, one thread per row chunk, as
+ * the reference's generator.cu does on its GPU); bit-identical to the host generator */
+problem_t *simplex_generate_problem_device(int n, int m, unsigned int seed, int lo, int hi, int rand_kind);
 
 /* ---- benchmark session: a resident phase-1 tableau and timed pivots ---- */
 typedef struct {
@@ -79,6 +82,9 @@ typedef struct {
 
 typedef struct simplex_session simplex_session;
 simplex_session *simplex_session_open(problem_t *problem); /* builds phase 1 + canonicalises d */
+/* same tableau as simplex_session_open(generateRandomProblem(n, m, seed, lo, hi)), synthesised
+ * directly in HBM (each shard generates only its rows; no host copy of A) */
+simplex_session *simplex_session_open_generated(int n, int m, unsigned int seed, int lo, int hi, int rand_kind);
 /* k pivots; time_updates = s > 0 brackets every s-th update launch with HIP events */
 int simplex_session_pivots(simplex_session *s, long long k, int time_updates, simplex_timing_t *out);
 double simplex_session_objective(simplex_session *s);   /* d[0] */
@@ -97,6 +103,9 @@ int simplex_dev_update_objective(const double *T, long long m, long long N, long
                                  double *d);
 /* phase-1 tableau as built on the device (row-major m x ld, ld >= 1+n+2m), d and base */
 int simplex_dev_build_phase1(problem_t *problem, double *T, long long ld, double *d, int *base);
+/* the same from the device generator */
+int simplex_dev_build_phase1_generated(int n, int m, unsigned int seed, int lo, int hi, double *T, long long ld,
+                                       double *d, int *base);
 
 #ifdef __cplusplus
 }

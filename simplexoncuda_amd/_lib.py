@@ -99,6 +99,13 @@ SIGNATURES = {
     "simplex_generate_problem_ex": (P_PROBLEM, [ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_int,
                                                 ctypes.c_int, ctypes.c_int]),
     "simplex_free_problem_struct": (None, [P_PROBLEM]),
+    "simplex_generate_problem_device": (P_PROBLEM, [ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_int,
+                                                    ctypes.c_int, ctypes.c_int]),
+    "simplex_session_open_generated": (ctypes.c_void_p, [ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_int,
+                                                         ctypes.c_int, ctypes.c_int]),
+    "simplex_dev_build_phase1_generated": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_int,
+                                                          ctypes.c_int, c_double_p, ctypes.c_longlong, c_double_p,
+                                                          c_int_p]),
     "simplex_session_open": (ctypes.c_void_p, [P_PROBLEM]),
     "simplex_session_pivots": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int,
                                               ctypes.POINTER(TimingT)]),

@@ -101,6 +101,14 @@ def generateRandomProblem(nVars, nConstraints, seed, minGenerator=-100, maxGener
                                                    maxGenerator, rand_kind))
 
 
+def generateRandomProblemDevice(nVars, nConstraints, seed, minGenerator=-100, maxGenerator=100,
+                                rand_kind=RAND_MSVC):
+    """generateRandomProblem computed on the GPU (bit-identical to the host generator)."""
+    lib = _lib.load()
+    return Problem(lib.simplex_generate_problem_device(nVars, nConstraints, seed & 0xFFFFFFFF, minGenerator,
+                                                       maxGenerator, rand_kind))
+
+
 def _with_file(path, mode, fn):
     f = _libc.fopen(str(path).encode(), mode.encode())
     if not f:
@@ -165,9 +173,14 @@ def twoPhaseMethodEx(problem, max_pivots=-1):
 class Session:
     """A resident phase-1 tableau on this process's GPU shard, for timed pivots."""
 
-    def __init__(self, problem):
+    def __init__(self, problem=None, generated=None):
+        """problem: a Problem; or generated=(n, m, seed, lo, hi) to synthesise the tableau in HBM."""
         self._lib = _lib.load()
-        self._h = self._lib.simplex_session_open(problem.ptr)
+        if generated is not None:
+            n, m, seed, lo, hi = generated
+            self._h = self._lib.simplex_session_open_generated(n, m, seed & 0xFFFFFFFF, lo, hi, RAND_MSVC)
+        else:
+            self._h = self._lib.simplex_session_open(problem.ptr)
         if not self._h:
             raise RuntimeError("simplex_session_open failed")
 
@@ -229,6 +242,16 @@ def dev_build_phase1(problem):
     d = np.zeros(N1)
     base = np.zeros(max(m, 1), dtype=np.int32)
     lib.simplex_dev_build_phase1(problem.ptr, _dp(T), N1, _dp(d), _ip(base))
+    return T, d, base[:m]
+
+
+def dev_build_phase1_generated(n, m, seed, lo, hi):
+    lib = _lib.load()
+    N1 = 1 + n + 2 * m
+    T = np.zeros((m, N1))
+    d = np.zeros(N1)
+    base = np.zeros(max(m, 1), dtype=np.int32)
+    lib.simplex_dev_build_phase1_generated(n, m, seed & 0xFFFFFFFF, lo, hi, _dp(T), N1, _dp(d), _ip(base))
     return T, d, base[:m]
 
 

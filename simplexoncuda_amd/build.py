@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "simplexoncuda_amd")
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libsimplex_hip.so")
-SOURCES = ["sx_kernels.hip", "sx_engine.cpp", "sx_problem.cpp"]
+SOURCES = ["sx_kernels.hip", "sx_generator.hip", "sx_engine.cpp", "sx_problem.cpp"]
 HEADERS = ["sx_common.hpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SIMPLEX_OFFLOAD_ARCH", "gfx950")

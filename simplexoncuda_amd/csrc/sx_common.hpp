@@ -100,5 +100,12 @@ void sx_launch_build_rows(double *T, int rows, int row0, size_t ld, int n, int m
 void sx_launch_init_vectors(double *d, int N1, int n, int m, int *base, hipStream_t s);
 void sx_launch_phase2_costs(double *d, int n, int m, const double *c, hipStream_t s);
 void sx_launch_gather_rhs(const double *T, int rows, size_t ld, double *out, hipStream_t s);
+// device generator (sx_generator.hip) and the CRT seeding (sx_problem.cpp)
+void sx_crt_seeds(unsigned seed, int kind, uint32_t out[3]);
+void sx_launch_gen_rows(uint32_t seedA, int n, int m, int row0, int rows, double lo, double hi, double *T, size_t ld,
+                        double *A_cm, hipStream_t s);
+void sx_launch_gen_vector(uint32_t seed, long long first, int count, double lo, double hi, double *out,
+                          hipStream_t s);
+
 void sx_launch_argmin_vector(const double *v, long long L, TilePart *parts, int *out_idx, double *out_v,
                              hipStream_t s);

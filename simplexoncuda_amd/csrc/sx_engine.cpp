@@ -332,6 +332,24 @@ class Engine {
         }
     }
 
+    // the same tableau as build_phase1(generateRandomProblem(n, m, seed, lo, hi)), synthesised
+    // on the device: every shard generates only its own rows (jump-ahead XORWOW)
+    void build_phase1_generated(unsigned seed, int lo, int hi, int rand_kind) {
+        uint32_t sd[3];
+        sx_crt_seeds(seed, rand_kind, sd);
+        double *b_dev = dalloc<double>(m);
+        sx_launch_gen_vector(sd[0], 0, m, lo, hi, b_dev, s);
+        if (!c_dev) c_dev = dalloc<double>(n);
+        sx_launch_gen_vector(sd[1], 0, n, lo, hi, c_dev, s);
+        for (auto &x : sh) {
+            sx_launch_gen_rows(sd[2], n, m, x.row0, x.rows, lo, hi, x.T, ld, nullptr, s);
+            sx_launch_build_rows(x.T, x.rows, x.row0, ld, n, m, Ns1, nullptr, b_dev, s);
+            sx_launch_init_vectors(x.d, N1, n, m, x.base, s);
+        }
+        SX_HIP(hipStreamSynchronize(s));
+        (void)hipFree(b_dev);
+    }
+
     // ---------------------------------------------------------------- collectives
     void allgather_tiles() {
         if (rccl) {
@@ -822,10 +840,23 @@ struct simplex_session {
     bool started = false;
 };
 
+static simplex_session *session_finish(simplex_session *S);
+
 simplex_session *simplex_session_open(problem_t *problem) {
     simplex_session *S = new simplex_session;
     S->E = new Engine(problem->vars, problem->constraints);
     S->E->build_phase1(problem);
+    return session_finish(S);
+}
+
+simplex_session *simplex_session_open_generated(int n, int m, unsigned int seed, int lo, int hi, int rand_kind) {
+    simplex_session *S = new simplex_session;
+    S->E = new Engine(n, m);
+    S->E->build_phase1_generated(seed, lo, hi, rand_kind);
+    return session_finish(S);
+}
+
+static simplex_session *session_finish(simplex_session *S) {
     S->E->update_objective(S->E->N1);
     S->E->N = S->E->N1;
     S->E->reset_state(-1);
@@ -939,6 +970,39 @@ int simplex_dev_update_objective(const double *T, long long m, long long N, long
     E.update_objective((int)N);
     SX_HIP(hipStreamSynchronize(E.s));
     SX_HIP(hipMemcpy(d, E.sh[0].d, sizeof(double) * N, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+problem_t *sx_malloc_problem(int n, int m);
+
+problem_t *simplex_generate_problem_device(int n, int m, unsigned int seed, int lo, int hi, int rand_kind) {
+    problem_t *p = sx_malloc_problem(n, m);
+    uint32_t sd[3];
+    sx_crt_seeds(seed, rand_kind, sd);
+    hipStream_t s;
+    SX_HIP(hipStreamCreate(&s));
+    double *A = dalloc<double>((size_t)n * m), *b = dalloc<double>(m), *c = dalloc<double>(n);
+    sx_launch_gen_vector(sd[0], 0, m, lo, hi, b, s);
+    sx_launch_gen_vector(sd[1], 0, n, lo, hi, c, s);
+    sx_launch_gen_rows(sd[2], n, m, 0, m, lo, hi, nullptr, 0, A, s);
+    if (n > 0 && m > 0)
+        SX_HIP(hipMemcpyAsync(p->constraintsMatrix, A, sizeof(double) * (size_t)n * m, hipMemcpyDeviceToHost, s));
+    if (m > 0) SX_HIP(hipMemcpyAsync(p->knownTermsVector, b, sizeof(double) * m, hipMemcpyDeviceToHost, s));
+    if (n > 0) SX_HIP(hipMemcpyAsync(p->objectiveFunction, c, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+    SX_HIP(hipStreamSynchronize(s));
+    (void)hipFree(A);
+    (void)hipFree(b);
+    (void)hipFree(c);
+    (void)hipStreamDestroy(s);
+    return p;
+}
+
+int simplex_dev_build_phase1_generated(int n, int m, unsigned int seed, int lo, int hi, double *T, long long ld,
+                                       double *d, int *base) {
+    Engine E(n, m);
+    E.build_phase1_generated(seed, lo, hi, 0);
+    E.download(T, (size_t)ld, E.N1, d);
+    E.read_base(base);
     return 0;
 }
 

@@ -53,7 +53,10 @@ inline double draw_value(Xorwow &g, double lo, double span) {
     return std::fma((double)u, span, lo);
 }
 
-void crt_seeds(unsigned seed, int kind, uint32_t out[3]) {
+}  // namespace
+
+// problem.cu:63-67: srand(seed); three rand() calls (MSVC LCG or glibc TYPE_3)
+void sx_crt_seeds(unsigned seed, int kind, uint32_t out[3]) {
     if (kind == 0) {  // MSVC: holdrand = holdrand * 214013 + 2531011; (holdrand >> 16) & 0x7fff
         uint32_t h = seed;
         for (int k = 0; k < 3; ++k) {
@@ -76,6 +79,8 @@ void crt_seeds(unsigned seed, int kind, uint32_t out[3]) {
     for (int k = 0; k < 3; ++k) out[k] = ((uint32_t)r[344 + k]) >> 1;
 }
 
+namespace {
+
 problem_t *malloc_problem(int n, int m) {  // problem.cu:7-18
     problem_t *p = (problem_t *)malloc(sizeof(problem_t));
     p->constraints = m;
@@ -93,7 +98,7 @@ extern "C" {
 problem_t *simplex_generate_problem_ex(int n, int m, unsigned int seed, int lo, int hi, int rand_kind) {
     problem_t *p = malloc_problem(n, m);
     uint32_t sd[3];
-    crt_seeds(seed, rand_kind, sd);
+    sx_crt_seeds(seed, rand_kind, sd);
     const double dlo = (double)lo, span = (double)hi - (double)lo;
     {
         Xorwow g(sd[0]);
@@ -161,6 +166,8 @@ void freeProblem(problem_t *problem) {  // problem.cu:183-188 (the struct itself
     free(problem->knownTermsVector);
     free(problem->objectiveFunction);
 }
+
+problem_t *sx_malloc_problem(int n, int m) { return malloc_problem(n, m); }
 
 problem_t *simplex_problem_from_arrays(int n, int m, const double *A_colmajor, const double *b, const double *c) {
     problem_t *p = malloc_problem(n, m);
