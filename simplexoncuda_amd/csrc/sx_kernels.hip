@@ -816,7 +816,8 @@ void sx_launch_build_rows(double *T, int rows, int row0, size_t ld, int n, int m
     if (rows <= 0) return;
     dim3 tb(32, 8);
     dim3 tg((rows + 31) / 32, (n + 31) / 32);
-    if (n > 0) k_fill_structural<<<tg, tb, 0, s>>>(T, rows, ld, n, A_local);
+    // A_local == nullptr: the structural columns are already in T (device generator)
+    if (n > 0 && A_local != nullptr) k_fill_structural<<<tg, tb, 0, s>>>(T, rows, ld, n, A_local);
     int gx = (Ns + 255) / 256;
     if (gx > 64) gx = 64;
     dim3 rg(gx, rows);
