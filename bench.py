@@ -136,9 +136,11 @@ def main():
     def measure(config, steps, warmup, events):
         """W untimed + K timed phase-1 pivots of `config`; returns timing + roofline."""
         n, m, seed = CONFIGS[config]
-        problem = sx.generateRandomProblem(n, m, seed, 1, 100)
-        sess = sx.Session(problem)
-        del problem
+        t_setup = time.perf_counter()
+        # generateRandomProblem(n, m, seed, 1, 100) synthesised directly in HBM, each rank its rows
+        sess = sx.Session(generated=(n, m, seed, 1, 100))
+        torch.cuda.synchronize()
+        t_setup = time.perf_counter() - t_setup
         if warmup > 0:
             sess.pivots(warmup)
         barrier()
@@ -156,7 +158,7 @@ def main():
         avg_update_s = tim.update_ms / 1e3 / max(tim.update_launches, 1)
         achieved = tim.update_bytes / avg_update_s / 1e9 if tim.update_launches else None
         return {"n": n, "m": m, "seed": seed, "tim": tim, "elapsed": elapsed, "pivots": tim.pivots,
-                "avg_update_s": avg_update_s, "achieved": achieved}
+                "avg_update_s": avg_update_s, "achieved": achieved, "setup_s": t_setup}
 
     r = measure(args.config, args.steps, args.warmup, args.update_events)
     n, m, seed, tim, elapsed, pivots = r["n"], r["m"], r["seed"], r["tim"], r["elapsed"], r["pivots"]
@@ -178,12 +180,13 @@ def main():
         "scaling": "strong",
         "vs_baseline": (pivots / elapsed) / REF_PIVOTS_PER_S[args.config] if args.config in REF_PIVOTS_PER_S else None,
         "dtype": "f64",
-        "data": f"synthetic: generateRandomProblem(n={n}, m={m}, seed={seed}, [1,100]) (generator.cu/cuRAND-XORWOW restatement)",
+        "data": f"synthetic: generateRandomProblem(n={n}, m={m}, seed={seed}, [1,100]) -- the reference's -t "
+                "instance (cuRAND-XORWOW + MSVC rand semantics), synthesised on the GPU",
         "config": {
             "workload": f"{args.config}: phase-1 pivots, {m}x{N1} fp64 tableau (m={m}, n={n})",
             "m": m, "n": n, "seed": seed, "tableau_width": tim.width, "stored_width": tim.stored_width,
             "rows_per_gpu_rank0": tim.local_rows, "parallelism": f"row-block x{world}",
-            "pivots_timed": pivots, "status_after": tim.status,
+            "pivots_timed": pivots, "status_after": tim.status, "setup_s": r["setup_s"],
         },
         "roofline": {
             "bound": "hbm",
@@ -208,7 +211,7 @@ def main():
             "value": r2["pivots"] / r2["elapsed"], "unit": "pivots/s",
             "ms_per_step": r2["elapsed"] * 1e3 / max(r2["pivots"], 1),
             "steps": args.secondary_steps, "warmup": args.secondary_warmup, "pivots_timed": r2["pivots"],
-            "rows_per_gpu_rank0": t2.local_rows,
+            "rows_per_gpu_rank0": t2.local_rows, "setup_s": r2["setup_s"],
             "update_GBps_rank0": r2["achieved"], "update_frac_of_peak": r2["achieved"] / HBM_PEAK_GBS
             if r2["achieved"] else None, "avg_update_us": r2["avg_update_s"] * 1e6,
         }
