@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstring>
 #include <ctime>
+#include <functional>
 #include <map>
 #include <string>
 #include <mutex>
@@ -59,6 +60,7 @@ struct Config {
     std::string timer_dir;   // non-empty: write the reference's TIMER CSV there
     int exchange_mode = 0;   // 0 auto, 1 tile allgather + row allreduce, 2 row-gather
     int alias = 1;           // store phase-1 artificial columns as their slack columns
+    int debug = -1;          // -1: from SIMPLEX_DEBUG; 1: print the tableau after every step
     bool benchmark = false;
     // distributed
     bool dist = false;
@@ -192,6 +194,7 @@ class Engine {
     hipEvent_t poll_ev[2] = {nullptr, nullptr};
     double *c_dev = nullptr;            // objective coefficients c (phase 2)
     long long phase_pivots[2] = {0, 0};
+    std::function<void(int)> on_pivot;  // DEBUG trace: called after every pivot (solver.cu:112-116)
 
     Engine(int n_, int m_, bool alias_ = true) : n(n_), m(m_) {
         N1 = 1 + n + 2 * m;
@@ -513,8 +516,16 @@ class Engine {
         const int batch = g_cfg.batch > 0 ? g_cfg.batch : 16;
         const bool timed = ch && ch->on();
         std::vector<hipEvent_t> it_ev;  // TIMER CSV: one event pair per loop iteration
+        if (on_pivot) {  // DEBUG: one pivot at a time, tableau printed after each
+            for (;;) {
+                enqueue_pivot(nullptr, nullptr);
+                if (read_state().status != SX_NOT_ENDED) break;
+                flush();  // the pending pivot row back into T for printing (idempotent)
+                on_pivot(width);
+            }
+        }
         long long k = 0;
-        for (;; ++k) {
+        for (; !on_pivot; ++k) {
             for (int b = 0; b < batch; ++b) {
                 if (timed) {
                     hipEvent_t e0, e1;
@@ -634,6 +645,31 @@ static bool artificial_equals_slack(const double *T, long long m, long long N, l
 // tabular_t <-> engine
 std::map<const tabular_t *, Engine *> g_tabs;
 
+// tabular.cu:41-98 print(): one line per tableau column (the reference stores the transpose):
+// the m constraint entries, then the objective entry; the base vector last
+void print_tableau(FILE *out, Engine &E, int width) {
+    if (E.rccl) return;  // the rows of other ranks are not here
+    const int m = E.m;
+    std::vector<double> T((size_t)m * width), d(width);
+    std::vector<int> base(m);
+    E.download(T.data(), width, width, d.data());
+    E.read_base(base.data());
+    fprintf(out, "\n--------------- Tabular --------------\n");
+    for (int j = 0; j < width; ++j) {
+        for (int i = 0; i < m; ++i) fprintf(out, "%.2lf\t", T[(size_t)i * width + j]);
+        fprintf(out, "\t|\t %.11lf\n", d[j]);
+        if (j == 0) fprintf(out, "\n");
+    }
+    fprintf(out, "Base\n");
+    for (int i = 0; i < m; ++i) fprintf(out, "%d\t", base[i]);
+    fflush(out);
+}
+
+bool debug_on() {
+    if (g_cfg.debug < 0) g_cfg.debug = getenv("SIMPLEX_DEBUG") ? 1 : 0;
+    return g_cfg.debug > 0;
+}
+
 // ------------------------------------------------------------------ the two-phase driver
 int two_phase(problem_t *P, double *solution, double *opt, int *base_out, long long *pivots_out,
               long long max_pivots) {
@@ -649,11 +685,24 @@ int two_phase(problem_t *P, double *solution, double *opt, int *base_out, long l
     E.build_phase1(P);
     ch.stop(E.s);
     say("Phase 1: Resetting out-of-base variables");
+    if (debug_on()) {
+        fprintf(stdout, "\nTableu nella situazione iniziale\n");
+        print_tableau(stdout, E, E.N1);
+        E.on_pivot = [&E](int w) { print_tableau(stdout, E, w); };
+    }
     ch.start(E.s, E.N1, m, "gauss1");
     E.update_objective(E.N1);
     ch.stop(E.s);
+    if (debug_on()) {
+        fprintf(stdout, "\nTableu dopo l'eliminazione di gauss\n");
+        print_tableau(stdout, E, E.N1);
+    }
     say("Phase 1: Solving auxiliary problem");
     const int st1 = E.run_phase(E.N1, max_pivots, &p1, &ch);  // return value ignored by the reference (:258)
+    if (debug_on()) {
+        fprintf(stdout, "\nTableu dopo il lancio del primo solver\n");
+        print_tableau(stdout, E, E.N1);
+    }
     const double d0 = E.read_d0();
     std::vector<int> base(m);
     if (st1 == SX_PIVOT_CAP) {
@@ -683,6 +732,10 @@ int two_phase(problem_t *P, double *solution, double *opt, int *base_out, long l
         ch.stop(E.s);
         say("Phase 2: Solving original problem");
         status = E.run_phase(E.N2, max_pivots, &p2, &ch);
+        if (debug_on()) {
+            fprintf(stdout, "\nTableu dopo seconda esecuzione del solver\n");
+            print_tableau(stdout, E, E.N2);
+        }
         E.read_base(base.data());
         if (status == FEASIBLE) {
             // getSolutionHost (:370-383)

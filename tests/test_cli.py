@@ -70,3 +70,16 @@ def test_cli_benchmark_sweep_writes_reference_csv(gpu, tmp_path):
                       + ["solve"] * p2 + ["solution"])
             assert ops == expect
             assert all(int(x[1]) == m and float(x[3]) >= 0 for x in rows[1:])
+
+
+@pytest.mark.gpu
+def test_debug_trace(gpu, tmp_path):
+    """SIMPLEX_DEBUG=1: the reference's DEBUG build output (tableau after fill, canonicalisation,
+    every pivot and each phase), in its transposed print format"""
+    r = run(["-f", os.path.join(GOLDEN, "examples", "smallProblem.txt")], tmp_path, SIMPLEX_DEBUG="1")
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = r.stdout
+    assert out.count("--------------- Tabular --------------") == 2 + 2 + 1 + 2 + 1  # fill, gauss, 2+2 pivots, 2 ends
+    assert "Tableu nella situazione iniziale" in out and "Tableu dopo seconda esecuzione del solver" in out
+    last = out[out.rindex("Tableu dopo seconda esecuzione del solver"):]
+    assert "|\t 64.00000000000" in last and "Base\n3\t0\t" in last
