@@ -48,6 +48,15 @@ void simplex_set_force_exchange(int on);
 void simplex_set_exchange_mode(int mode);
 /* store each phase-1 artificial column as its (bit-identical) slack column: 1 on (default), 0 off */
 void simplex_set_alias(int on);
+/* rows whose entering-column entry is exactly 0 are left untouched by the update (default on).
+ * Engaged only when it is bit-exact: the tableau holds no -0.0 (true unless a b_i < 0 row was
+ * negated by the build quirk, or the caller uploads one) and the pivot-row values are finite. */
+void simplex_set_skip_zero(int on);
+/* the update's row sweep runs waves x (blocks resident on the device) blocks (default 2; <= 0 resets) */
+void simplex_set_update_waves(double waves);
+/* update kernel: -1 auto, 0 resident blocks sweeping the list of rows to update, 1 one block
+ * per (512 columns, rows-per-block rows) over the whole tableau */
+void simplex_set_update_mode(int mode);
 
 /* ---- extended drop-in entry ---- */
 /* twoPhaseMethod + final basis (base_out[m]) and per-phase pivot counts (pivots_out[2]);
@@ -77,7 +86,10 @@ typedef struct {
     int width;                 /* tableau width N of the phase (reference counting) */
     int stored_width;          /* columns actually stored and swept (artificials alias slacks in phase 1) */
     long long local_rows;      /* constraint rows owned by this process */
-    double update_bytes;       /* algorithmic bytes per update launch: 16 * local_rows * stored_width + 16 * N */
+    double update_bytes;       /* dense bytes per update launch: 16 * local_rows * stored_width + 16 * N */
+    long long touched_rows;    /* timed launches: sum of the rows they swept (nonzero factor, or pending) */
+    double touched_bytes;      /* timed launches: sum of the bytes they move: 32 * rows * (column pairs with a
+                                  nonzero pivot-row entry) + 16 * N; the dense figure when skipping is off */
 } simplex_timing_t;
 
 typedef struct simplex_session simplex_session;
@@ -89,6 +101,10 @@ simplex_session *simplex_session_open_generated(int n, int m, unsigned int seed,
 int simplex_session_pivots(simplex_session *s, long long k, int time_updates, simplex_timing_t *out);
 double simplex_session_objective(simplex_session *s);   /* d[0] */
 long long simplex_session_total_pivots(simplex_session *s);
+/* per timed launch of the last simplex_session_pivots call: rows the update swept (this
+ * process's shards) and its duration in microseconds; returns the number of launches logged
+ * (at most cap are copied) */
+long long simplex_session_launch_log(simplex_session *s, long long *rows, double *update_us, long long cap);
 void simplex_session_close(simplex_session *s);
 
 /* ---- kernel-level parity hooks (host arrays in/out, device compute) ---- */

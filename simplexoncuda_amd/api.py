@@ -190,6 +190,15 @@ class Session:
         self._lib.simplex_session_pivots(self._h, k, int(time_updates), ctypes.byref(t))
         return t
 
+    def launch_log(self):
+        """(rows swept, update microseconds) per timed launch of the last pivots() call."""
+        n = self._lib.simplex_session_launch_log(self._h, None, None, 0)
+        rows = np.zeros(max(n, 1), dtype=np.int64)
+        us = np.zeros(max(n, 1), dtype=np.float64)
+        self._lib.simplex_session_launch_log(self._h, rows.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)),
+                                             _dp(us), n)
+        return rows[:n], us[:n]
+
     def objective(self):
         return self._lib.simplex_session_objective(self._h)
 
@@ -269,6 +278,22 @@ def set_exchange_mode(mode):
 
 def set_alias(on):
     _lib.load().simplex_set_alias(1 if on else 0)
+
+
+def set_skip_zero(on):
+    """Leave rows with an exactly-zero entering-column entry untouched (default on; engaged
+    only where bit-exact, see include/simplex_hip.h)."""
+    _lib.load().simplex_set_skip_zero(1 if on else 0)
+
+
+def set_update_waves(w):
+    """Blocks of the update's row sweep as a multiple of the device's resident capacity."""
+    _lib.load().simplex_set_update_waves(float(w))
+
+
+def set_update_mode(mode):
+    """-1 auto, 0 resident row-list sweep, 1 one-shot grid."""
+    _lib.load().simplex_set_update_mode(int(mode))
 
 
 def set_verbose(on):

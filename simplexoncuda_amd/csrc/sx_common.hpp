@@ -44,8 +44,20 @@ struct __attribute__((aligned(16))) DevState {
     unsigned ticket;       // arrival counter of the ratio/select hand-off (zero between launches)
     double dmin_next;      // its value
     unsigned ticket_d;     // arrival counter of the objective-row blocks of the update
-    int pad0;
+    int touched;           // this shard's rows the current update sweeps (rows with a nonzero factor)
+    int touched_pairs;     // column pairs of the current pivot row holding a nonzero (swept columns)
+    int pad1;
 };
+
+// tile_cnt[t] of a ratio tile: the number of listed rows, plus SX_TILE_WIDE when a listed
+// row's entry is too large for the factor -a/p to be finite with p >= eps
+#define SX_TILE_WIDE 0x40000000
+#define SX_TILE_COUNT(x) ((x) & (SX_TILE_WIDE - 1))
+
+// TilePart.elig packs "any entry >= eps" (bit 0) and the tile's count of nonzero
+// entering-column entries (bits 1..)
+#define SX_ELIG(x) ((x) & 1)
+#define SX_NNZ(x) ((x) >> 1)
 
 // Error convention of the reference (error.cu:5-12): print "<msg> in <file> at line <n>"
 // and exit(EXIT_FAILURE).
@@ -71,21 +83,25 @@ struct UpdateCfg {
     int rows_per_block;  // 1, 2, 4 or 8
     int snake;           // alternate the sweep direction every pivot
     int sc1;             // write-through (sc1) tableau stores
+    int skip_zero;       // skip rows whose factor is exactly zero (only when bit-exact: no -0.0 in T)
+    int one_shot;        // 1: one block per (512 columns, RB rows); 0: resident blocks sweep the row list
 };
 
 int sx_enter_blocks(int L);
 void sx_launch_enter(const double *d, int L, TilePart *parts, DevState *st, hipStream_t s);
 void sx_launch_ratio_select(const double *T, int rows, int row0, size_t ld, TilePart *tiles_local, double *colE,
                             DevState *st, int *base, const double *rnew, size_t rnew_stride, bool select,
-                            double *slots, size_t slot_stride, Cols c, hipStream_t s);
+                            double *slots, size_t slot_stride, Cols c, int *rowlist, int *tile_cnt, int skip_zero,
+                            hipStream_t s);
 void sx_launch_select_gathered(const double *slots, size_t slot_stride, int B2, int *base, DevState *st,
-                               hipStream_t s);
+                               int tile0, int nslots, hipStream_t s);
 void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, Cols c, const TilePart *tiles_all, int B2,
                           double *prow_out, int *base, DevState *st, const double *rnew, size_t rnew_stride,
-                          hipStream_t s);
+                          int tile0, int slots, hipStream_t s);
 void sx_launch_update(double *T, int rows, int row0, size_t ld, Cols c, double *d, const double *prow_buf,
                       size_t prow_stride, const double *colE, DevState *st, double *rnew, size_t rnew_stride,
-                      TilePart *enter_parts, UpdateCfg cfg, hipStream_t s);
+                      TilePart *enter_parts, const int *rowlist, const int *tile_cnt, UpdateCfg cfg, hipStream_t s);
+void sx_set_update_waves(float w);  // resident-grid multiple of the update's row sweep (default 2)
 void sx_launch_flush_row(double *T, int rows, int row0, size_t ld, int Ns, const double *rnew, size_t rnew_stride,
                          const DevState *st, hipStream_t s);
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s);

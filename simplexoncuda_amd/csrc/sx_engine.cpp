@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <ctime>
 #include <functional>
@@ -60,6 +61,8 @@ struct Config {
     std::string timer_dir;   // non-empty: write the reference's TIMER CSV there
     int exchange_mode = 0;   // 0 auto, 1 tile allgather + row allreduce, 2 row-gather
     int alias = 1;           // store phase-1 artificial columns as their slack columns
+    int skip_zero = 1;       // leave zero-factor rows untouched where that is bit-exact
+    int update_mode = -1;    // -1 auto, 0 resident row-list sweep, 1 one-shot grid
     int debug = -1;          // -1: from SIMPLEX_DEBUG; 1: print the tableau after every step
     bool benchmark = false;
     // distributed
@@ -80,6 +83,22 @@ void say(const char *s) {
 }
 
 inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+inline bool is_neg_zero(double v) { return v == 0.0 && std::signbit(v); }
+
+bool any_neg_zero(const double *v, size_t count) {
+    for (size_t i = 0; i < count; ++i)
+        if (is_neg_zero(v[i])) return true;
+    return false;
+}
+
+// the build quirk (twoPhaseMethod.cu:160-175) negates a whole row when compare(b_i) < 0:
+// its zero entries become -0.0
+bool any_negated_row(const double *b, int m) {
+    for (int i = 0; i < m; ++i)
+        if (compare(b[i], 0.0, SIMPLEX_EPSILON) < 0) return true;
+    return false;
+}
 
 template <typename T>
 T *dalloc(size_t count) {
@@ -167,6 +186,8 @@ struct Shard {
     double *rhs_all = nullptr;
     int *base = nullptr;
     TilePart *enter_parts = nullptr;
+    int *rowlist = nullptr;   // per 512-row tile: the rows the update sweeps (k_ratio_select)
+    int *tile_cnt = nullptr;
     TilePart *tiles_local = nullptr;
     TilePart *tiles_all = nullptr;
     DevState *st = nullptr;
@@ -194,6 +215,9 @@ class Engine {
     hipEvent_t poll_ev[2] = {nullptr, nullptr};
     double *c_dev = nullptr;            // objective coefficients c (phase 2)
     long long phase_pivots[2] = {0, 0};
+    // no -0.0 anywhere in T: skipping rows whose factor is +-0 is then bit-exact (fma(+-0, p, x)
+    // == x for finite p and x != -0.0, and the update itself never creates a -0.0)
+    bool no_neg_zero = false;
     std::function<void(int)> on_pivot;  // DEBUG trace: called after every pivot (solver.cu:112-116)
 
     Engine(int n_, int m_, bool alias_ = true) : n(n_), m(m_) {
@@ -284,6 +308,8 @@ class Engine {
         if (xchg) x.rhs_all = dalloc<double>((size_t)W * rpr);
         x.base = dalloc<int>(m);
         x.enter_parts = dalloc<TilePart>(SX_TILE);
+        x.rowlist = dalloc<int>((size_t)slots * SX_TILE);
+        x.tile_cnt = dalloc<int>(slots);
         x.tiles_local = dalloc<TilePart>(slots);
         if (xchg) x.tiles_all = dalloc<TilePart>((size_t)W * slots);
         x.st = dalloc<DevState>(1);
@@ -305,7 +331,7 @@ class Engine {
     void free_shard(Shard &x) {
         for (void *p : {(void *)x.T, (void *)x.d, (void *)x.colE, (void *)x.prow, (void *)x.prow_send,
                         (void *)x.slot_send, (void *)x.slot_all, (void *)x.rnew, (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
-                        (void *)x.rhs_all, (void *)x.base, (void *)x.enter_parts, (void *)x.tiles_local,
+                        (void *)x.rhs_all, (void *)x.base, (void *)x.enter_parts, (void *)x.rowlist, (void *)x.tile_cnt, (void *)x.tiles_local,
                         (void *)x.tiles_all, (void *)x.st})
             if (p) (void)hipFree(p);
     }
@@ -328,6 +354,9 @@ class Engine {
             if (A_local) (void)hipFree(A_local);
         }
         (void)hipFree(b_dev);
+        no_neg_zero = !any_negated_row(P->knownTermsVector, m) &&
+                      !any_neg_zero(P->knownTermsVector, (size_t)m) &&
+                      !any_neg_zero(P->constraintsMatrix, (size_t)n * m);
         if (!c_dev) {
             c_dev = dalloc<double>(n);
             if (n > 0)
@@ -349,8 +378,12 @@ class Engine {
             sx_launch_build_rows(x.T, x.rows, x.row0, ld, n, m, Ns1, nullptr, b_dev, s);
             sx_launch_init_vectors(x.d, N1, n, m, x.base, s);
         }
+        // generated values fma(u, span, lo) are never -0.0; only the b < 0 quirk makes them
+        std::vector<double> b_host(m);
+        if (m > 0) SX_HIP(hipMemcpyAsync(b_host.data(), b_dev, sizeof(double) * m, hipMemcpyDeviceToHost, s));
         SX_HIP(hipStreamSynchronize(s));
         (void)hipFree(b_dev);
+        no_neg_zero = !any_negated_row(b_host.data(), m);
     }
 
     // ---------------------------------------------------------------- collectives
@@ -434,19 +467,22 @@ class Engine {
 
     // ---------------------------------------------------------------- one pivot
     UpdateCfg update_cfg() const {
-        // A/B in the real pivot loop (tools/sweep_update.py, interleaved rounds on MI355X):
-        // a shard inside the 256 MB Infinity Cache streams best with 2 rows per block, plain
-        // stores, fixed order.  Above it, reversing the sweep every other pivot lets a sweep
-        // start on the lines the previous one left in the cache, and write-through (sc1)
-        // stores help: config 3 (0.8 GB stored) 117 us vs 142 us with neither; beyond ~4 GB
-        // 1 row per block is best (config 5 on one GPU, 21 GB: 3.82 ms vs 4.05 ms).
+        // Measured in the real pivot loop (tools/pivot_profile.py, tools/sweep_update.py on
+        // MI355X).  The resident row-list sweep (mode 0) makes a pivot whose entering column is
+        // almost all zeros (about half of phase 1's: a slack column entering) cost ~10 us
+        // instead of a full sweep, and sweeps dense pivots within ~5 % of the one-shot grid:
+        // 4 rows per iteration, 2x the resident grid.  Above the 256 MB Infinity Cache,
+        // reversing the sweep every other pivot lets it start on the lines the previous one
+        // left in the cache, and write-through (sc1) stores help.
         double bytes = 0.0;
         for (auto &x : sh) bytes = std::max(bytes, 8.0 * (double)x.rows * (double)cols(N).Ns);
         const bool big = bytes > 256.0 * 1024 * 1024;
         UpdateCfg c;
-        c.rows_per_block = g_cfg.update_rows > 0 ? g_cfg.update_rows : (bytes > 4.0e9 ? 1 : 2);
+        c.one_shot = g_cfg.update_mode == 1 ? 1 : 0;
+        c.rows_per_block = g_cfg.update_rows > 0 ? g_cfg.update_rows : (c.one_shot ? (bytes > 4.0e9 ? 1 : 2) : 4);
         c.snake = g_cfg.snake >= 0 ? g_cfg.snake : (big ? 1 : 0);
         c.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : (big ? 1 : 0);
+        c.skip_zero = (g_cfg.skip_zero && no_neg_zero) ? 1 : 0;
         return c;
     }
 
@@ -461,22 +497,24 @@ class Engine {
         const Cols c = cols(N);
         for (auto &x : sh)
             sx_launch_ratio_select(x.T, x.rows, x.row0, ld, x.tiles_local, x.colE, x.st, x.base, x.rnew, ld, !xchg,
-                                   rowgather ? x.slot_send : nullptr, slot_stride, c, s);
+                                   rowgather ? x.slot_send : nullptr, slot_stride, c, x.rowlist, x.tile_cnt,
+                                   cfg.skip_zero, s);
         if (rowgather) {
             allgather_slots();
-            for (auto &x : sh) sx_launch_select_gathered(x.slot_all, slot_stride, W * slots, x.base, x.st, s);
+            for (auto &x : sh)
+                sx_launch_select_gathered(x.slot_all, slot_stride, W * slots, x.base, x.st, x.rank * slots, slots, s);
         } else if (xchg) {
             allgather_tiles();
             for (auto &x : sh)
                 sx_launch_select_row(x.T, x.rows, x.row0, ld, c, x.tiles_all, W * slots, x.prow_send, x.base, x.st,
-                                     x.rnew, ld, s);
+                                     x.rnew, ld, x.rank * slots, slots, s);
             allreduce_prow();
         }
         if (ev0) SX_HIP(hipEventRecord(ev0, s));
         for (auto &x : sh) {
             const double *pb = rowgather ? x.slot_all : (xchg ? x.prow : nullptr);
             sx_launch_update(x.T, x.rows, x.row0, ld, c, x.d, pb, rowgather ? slot_stride : 0, x.colE, x.st, x.rnew,
-                             ld, x.enter_parts, cfg, s);
+                             ld, x.enter_parts, x.rowlist, x.tile_cnt, cfg, s);
         }
         if (ev1) SX_HIP(hipEventRecord(ev1, s));
     }
@@ -618,6 +656,9 @@ class Engine {
     // artificial columns must equal the slack columns, checked by the callers below)
     void upload(const double *T_host, size_t ld_host, int width, const double *d_host, const int *base_host) {
         const Cols c = cols(width);
+        no_neg_zero = true;
+        for (int i = 0; i < m && no_neg_zero; ++i)
+            if (any_neg_zero(T_host + (size_t)i * ld_host, (size_t)width)) no_neg_zero = false;
         for (auto &x : sh) {
             if (x.rows > 0)
                 SX_HIP(hipMemcpy2DAsync(x.T, ld * sizeof(double), T_host + (size_t)x.row0 * ld_host,
@@ -778,6 +819,9 @@ void simplex_set_device(int device) {
 void simplex_set_virtual_ranks(int world) { g_cfg.virtual_ranks = world > 1 ? world : 1; }
 void simplex_set_force_exchange(int on) { g_cfg.force_exchange = on ? 1 : 0; }
 void simplex_set_alias(int on) { g_cfg.alias = on ? 1 : 0; }
+void simplex_set_skip_zero(int on) { g_cfg.skip_zero = on ? 1 : 0; }
+void simplex_set_update_waves(double waves) { sx_set_update_waves((float)waves); }
+void simplex_set_update_mode(int mode) { g_cfg.update_mode = (mode >= 0 && mode <= 1) ? mode : -1; }
 void simplex_set_exchange_mode(int mode) { g_cfg.exchange_mode = (mode >= 0 && mode <= 2) ? mode : 0; }
 void simplex_set_timer_dir(const char *dir) { g_cfg.timer_dir = dir ? dir : ""; }
 
@@ -891,6 +935,8 @@ struct simplex_session {
     Engine *E;
     long long total = 0;
     bool started = false;
+    std::vector<long long> log_rows;  // per timed launch of the last pivots call
+    std::vector<double> log_us;
 };
 
 static simplex_session *session_finish(simplex_session *S);
@@ -926,6 +972,10 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
     const long long nt = every ? (k + every - 1) / every : 0;
     std::vector<hipEvent_t> evs(2 * (size_t)nt);
     for (auto &e : evs) SX_HIP(hipEventCreate(&e));
+    // rows each timed update actually touched (DevState.touched, summed over local shards)
+    const size_t nsh = E.sh.size();
+    // (DevState.touched, DevState.touched_pairs) after each timed update
+    int *touched_dev = dalloc<int>((size_t)(nt > 0 ? nt : 1) * nsh * 2);
     hipEvent_t w0, w1;
     SX_HIP(hipEventCreate(&w0));
     SX_HIP(hipEventCreate(&w1));
@@ -934,6 +984,10 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
     for (long long i = 0; i < k; ++i) {
         const bool timed = every && (i % every == 0);
         E.enqueue_pivot(timed ? evs[2 * (i / every)] : nullptr, timed ? evs[2 * (i / every) + 1] : nullptr);
+        if (timed)
+            for (size_t q = 0; q < nsh; ++q)
+                SX_HIP(hipMemcpyAsync(touched_dev + 2 * ((size_t)(i / every) * nsh + q), &E.sh[q].st->touched,
+                                      2 * sizeof(int), hipMemcpyDeviceToDevice, E.s));
     }
     SX_HIP(hipEventRecord(w1, E.s));
     SX_HIP(hipEventSynchronize(w1));
@@ -952,13 +1006,35 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
     t.stored_width = E.cols(E.N).Ns;
     t.update_bytes = 16.0 * (double)rows * (double)t.stored_width + 16.0 * (double)E.N;
     double sum = 0.0;
+    std::vector<float> per((size_t)(nt > 0 ? nt : 1), 0.f);
     for (long long i = 0; i < nt; ++i) {
-        float u = 0.f;
-        SX_HIP(hipEventElapsedTime(&u, evs[2 * i], evs[2 * i + 1]));
-        sum += u;
+        SX_HIP(hipEventElapsedTime(&per[(size_t)i], evs[2 * i], evs[2 * i + 1]));
+        sum += per[(size_t)i];
     }
     t.update_ms = sum;
     t.update_launches = nt;
+    std::vector<int> touched((size_t)(nt > 0 ? nt : 1) * nsh * 2, 0);
+    SX_HIP(hipMemcpy(touched.data(), touched_dev, sizeof(int) * touched.size(), hipMemcpyDeviceToHost));
+    (void)hipFree(touched_dev);
+    const UpdateCfg ucfg = E.update_cfg();
+    const bool skipping = ucfg.skip_zero != 0;
+    const long long all_pairs = (t.stored_width + 1) / 2;
+    S->log_rows.assign((size_t)nt, 0);
+    S->log_us.assign((size_t)nt, 0.0);
+    for (long long i = 0; i < nt; ++i) {
+        for (size_t q = 0; q < nsh; ++q) {
+            const int *tq = touched.data() + 2 * ((size_t)i * nsh + q);
+            // rows the update swept (read + written), the deferred pivot row included, over the
+            // column pairs it swept (the list sweep leaves the pivot row's zero pairs alone)
+            const long long rows_i = skipping ? (long long)tq[0] : E.sh[q].rows;
+            const long long pairs_i = (skipping && !ucfg.one_shot) ? (long long)tq[1] : all_pairs;
+            t.touched_rows += rows_i;
+            t.touched_bytes += 32.0 * (double)rows_i * (double)pairs_i;
+            S->log_rows[(size_t)i] += rows_i;
+            S->log_us[(size_t)i] = 1e3 * (double)per[(size_t)i];
+        }
+        t.touched_bytes += 16.0 * (double)E.N * (double)nsh;
+    }
     for (auto &e : evs) (void)hipEventDestroy(e);
     (void)hipEventDestroy(w0);
     (void)hipEventDestroy(w1);
@@ -969,6 +1045,15 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
 
 double simplex_session_objective(simplex_session *S) { return S->E->read_d0(); }
 long long simplex_session_total_pivots(simplex_session *S) { return S->E->read_state().pivots; }
+
+long long simplex_session_launch_log(simplex_session *S, long long *rows, double *update_us, long long cap) {
+    const long long n = (long long)S->log_rows.size();
+    for (long long i = 0; i < n && i < cap; ++i) {
+        if (rows) rows[i] = S->log_rows[(size_t)i];
+        if (update_us) update_us[i] = S->log_us[(size_t)i];
+    }
+    return n;
+}
 
 void simplex_session_close(simplex_session *S) {
     if (!S) return;

@@ -171,7 +171,8 @@ __device__ __forceinline__ const double *row_src(const double *T, size_t ld, int
 __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__ T, int rows, int row0, size_t ld,
                                                       TilePart *tiles_local, double *colE, DevState *st, int *base,
                                                       const double *__restrict__ rnew, size_t rnew_stride,
-                                                      int select, double *slots, size_t slot_stride, Cols c) {
+                                                      int select, double *slots, size_t slot_stride, Cols c,
+                                                      int *rowlist, int *tile_cnt, int skip_zero) {
     if (st->status != SX_NOT_ENDED) return;
     const bool leader = blockIdx.x == 0 && threadIdx.x == 0;
     const long long piv = st->pivots;
@@ -197,19 +198,39 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
     double rv = DBL_MAX;
     int ri = -1;
     int elig = 0;
+    bool listed = false, wide = false;
     if (li < rows) {
         const double *row = row_src(T, ld, li, pend, rcur);
         const double a = row[c.map(1 + e)];
         const double b = row[0];
         colE[li] = a;
         elig = a >= SX_EPS;
+        // rows the update must sweep: a nonzero factor, or the pending row (its values live in
+        // rnew until the update writes them back); every row when skipping is off
+        listed = !skip_zero || a != 0.0 || li == pend;
+        wide = listed && !(fabs(a) <= 1e299);  // |a / p| could overflow (p >= 1e-9), or a is not finite
         const double ratio = cmp_eps(a, 0.0) > 0 ? b / a : DBL_MAX;
         if (cmp_eps(ratio, rv) < 0) {
             rv = ratio;
             ri = row0 + li;
         }
     }
-    const int any = __syncthreads_or(elig);
+    // compact this tile's listed rows, in row order, to rowlist[tile*512 ...]
+    __shared__ int s_wc[SX_TILE / 64];
+    const unsigned long long bal = __ballot(listed);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0) s_wc[wv] = __popcll(bal);
+    int any = __syncthreads_or(elig);
+    const int any_wide = __syncthreads_or(wide);
+    int pos = 0, cnt = 0;
+    for (int w = 0; w < SX_TILE / 64; ++w) {
+        pos += w < wv ? s_wc[w] : 0;
+        cnt += s_wc[w];
+    }
+    if (listed) rowlist[blockIdx.x * SX_TILE + pos + __popcll(bal & ((1ull << lane) - 1))] = li;
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = cnt | (any_wide ? SX_TILE_WIDE : 0);
+    if (leader) st->touched_pairs = 0;  // counted by the update
+    any |= cnt << 1;  // packed: SX_ELIG / SX_NNZ
     block_argmin512(rv, ri, s_v, s_i);
     if (!select) {
         if (slots == nullptr) {
@@ -251,6 +272,9 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
     const int B2 = gridDim.x;
     double tv = DBL_MAX;
     int ti = -1, te = 0;
+    __shared__ int s_nnz;
+    if (threadIdx.x == 0) s_nnz = 0;
+    __syncthreads();
     if ((int)threadIdx.x < B2) {
         double cv;
         int ci;
@@ -259,8 +283,9 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
             tv = cv;
             ti = ci;
         }
+        atomicAdd(&s_nnz, SX_NNZ(te));
     }
-    const int anyall = __syncthreads_or(te);
+    const int anyall = __syncthreads_or(SX_ELIG(te));
     if (!anyall) {
         if (threadIdx.x == 0) {
             st->ticket = 0;
@@ -278,6 +303,7 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
             st->r_prev = st->r;
             st->r = ti;
             st->pivots = piv + 1;
+            st->touched = s_nnz;
         }
     }
 }
@@ -291,17 +317,22 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
 __global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T, int rows, int row0, size_t ld,
                                                     int Ns, const TilePart *__restrict__ tiles_all, int B2,
                                                     double *prow_out, int *base, DevState *st,
-                                                    const double *__restrict__ rnew, size_t rnew_stride) {
+                                                    const double *__restrict__ rnew, size_t rnew_stride, int tile0,
+                                                    int nslots) {
     if (st->status != SX_NOT_ENDED) return;
     const bool leader = blockIdx.x == 0 && threadIdx.x == 0;
     __shared__ double s_v[16];
     __shared__ int s_i[16];
     __shared__ int s_r;
-    const int elig = ((int)threadIdx.x < B2) ? tiles_all[threadIdx.x].elig : 0;
-    if (!__syncthreads_or(elig)) {
+    const int pk = ((int)threadIdx.x < B2) ? tiles_all[threadIdx.x].elig : 0;
+    if (!__syncthreads_or(SX_ELIG(pk))) {
         if (leader) st->status = SX_UNBOUNDED;  // solver.cu:96-102
         return;
     }
+    __shared__ int s_nnz;
+    if (threadIdx.x == 0) s_nnz = 0;
+    __syncthreads();
+    if ((int)threadIdx.x >= tile0 && (int)threadIdx.x < tile0 + nslots) atomicAdd(&s_nnz, SX_NNZ(pk));
     double v;
     int r;
     stage2_512(tiles_all, B2, v, r, s_v, s_i);
@@ -329,6 +360,7 @@ __global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T
             st->r_prev = st->r;
             st->r = r;
             st->pivots = piv + 1;
+            st->touched = s_nnz;
         }
     }
 }
@@ -337,22 +369,26 @@ __global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T
 // winners (the reference's pass-2 tree), checks the unbounded condition and records the
 // pivot; the update then reads the pivot row from the winning slot.
 __global__ __launch_bounds__(512) void k_select_gathered(const double *__restrict__ slots, size_t slot_stride, int B2,
-                                                         int *base, DevState *st) {
+                                                         int *base, DevState *st, int tile0, int nslots) {
     if (st->status != SX_NOT_ENDED) return;
     __shared__ double s_v[16];
     __shared__ int s_i[16];
     double v = DBL_MAX;
-    int r = -1, elig = 0;
+    int r = -1, pk = 0;
+    __shared__ int s_nnz;
+    if (threadIdx.x == 0) s_nnz = 0;
+    __syncthreads();
     if ((int)threadIdx.x < B2) {
         const TilePart *h = reinterpret_cast<const TilePart *>(slots + (size_t)threadIdx.x * slot_stride);
-        elig = h->elig;
+        pk = h->elig;
         const double c = h->v;
         if (cmp_eps(c, v) < 0) {
             v = c;
             r = h->idx;
         }
+        if ((int)threadIdx.x >= tile0 && (int)threadIdx.x < tile0 + nslots) atomicAdd(&s_nnz, SX_NNZ(pk));
     }
-    if (!__syncthreads_or(elig)) {
+    if (!__syncthreads_or(SX_ELIG(pk))) {
         if (threadIdx.x == 0) st->status = SX_UNBOUNDED;  // solver.cu:96-102
         return;
     }
@@ -365,6 +401,7 @@ __global__ __launch_bounds__(512) void k_select_gathered(const double *__restric
             st->r_prev = st->r;
             st->r = r;
             st->pivots += 1;
+            st->touched = s_nnz;
         }
     }
 }
@@ -397,12 +434,139 @@ __device__ __forceinline__ void store_pair(double *p, double2 v, __amdgpu_buffer
         *reinterpret_cast<double2 *>(p) = v;
 }
 
+// Objective row of the update (grid row 0 of either update kernel, dispatched first): d[j] =
+// fma(-(d_e / p), prow[j], d[j]) and pass 1 of the NEXT entering argmin per 512-tile
+// (reduction.cu:51-80); the last block to arrive runs pass 2 and stores (e_next, dmin_next).
+// 512 reference threads on 256.
+__device__ void objective_row(const double *__restrict__ prow, double p, double *__restrict__ d, DevState *st,
+                              TilePart *enter_parts, Cols c) {
+    // ---- objective row + next entering argmin (512 reference threads on 256)
+    __shared__ double s_v[16];
+    __shared__ int s_i[16];
+    __shared__ int s_last;
+    const int L = c.N - 1;
+    const int B1 = (L + SX_TILE - 1) / SX_TILE;
+    if ((int)blockIdx.x >= B1) return;
+    const double fd = -st->dmin / p;
+    if (blockIdx.x == 0 && threadIdx.x == 0) d[0] = fma(fd, prow[0], d[0]);
+    double v0 = DBL_MAX, v1 = DBL_MAX;
+    int i0 = -1, i1 = -1;
+    const int ia = blockIdx.x * SX_TILE + threadIdx.x, ib = ia + 256;
+    if (ia < L) {
+        const double x = fma(fd, prow[c.map(1 + ia)], d[1 + ia]);
+        d[1 + ia] = x;
+        if (cmp_eps(x, v0) < 0) {
+            v0 = x;
+            i0 = ia;
+        }
+    }
+    if (ib < L) {
+        const double x = fma(fd, prow[c.map(1 + ib)], d[1 + ib]);
+        d[1 + ib] = x;
+        if (cmp_eps(x, v1) < 0) {
+            v1 = x;
+            i1 = ib;
+        }
+    }
+    half_argmin(v0, i0);  // reference warps 0..7
+    half_argmin(v1, i1);  // reference warps 8..15
+    const int lane = threadIdx.x & 31, h = threadIdx.x >> 5;
+    if (lane == 0) {
+        s_v[h] = v0;
+        s_i[h] = i0;
+        s_v[h + 8] = v1;
+        s_i[h + 8] = i1;
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        double v = (threadIdx.x < 16) ? s_v[threadIdx.x] : DBL_MAX;
+        int i = (threadIdx.x < 16) ? s_i[threadIdx.x] : -1;
+        half_argmin(v, i);
+        if (threadIdx.x == 0) {
+            store_tile_sc1(enter_parts + blockIdx.x, v, i, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned t = __hip_atomic_fetch_add(&st->ticket_d, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            s_last = (t == (unsigned)B1 - 1);
+        }
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // last objective block: pass 2 (reference pass-2 tree; B1 <= 256 here)
+    double v = DBL_MAX;
+    int i = -1;
+    if ((int)threadIdx.x < B1) {
+        double cv;
+        int ci, ce;
+        load_tile_sc1(enter_parts + threadIdx.x, cv, ci, ce);
+        if (cmp_eps(cv, v) < 0) {
+            v = cv;
+            i = ci;
+        }
+    }
+    half_argmin(v, i);
+    __syncthreads();
+    if (lane == 0) {
+        s_v[h] = v;
+        s_i[h] = i;
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        v = (threadIdx.x < 8) ? s_v[threadIdx.x] : DBL_MAX;
+        i = (threadIdx.x < 8) ? s_i[threadIdx.x] : -1;
+        half_argmin(v, i);
+        if (threadIdx.x == 0) {
+            st->e_next = i;
+            st->dmin_next = v;
+            st->ticket_d = 0;
+        }
+    }
+    return;
+}
+
+// Exclusive prefix of the per-tile list lengths (n <= 512 tiles, 256 threads): s_pre[t] =
+// first list position of tile t, s_pre[n] = total; wide = some tile flagged SX_TILE_WIDE.
+// All threads of the block must call it.
+__device__ int scan_tile_counts(const int *__restrict__ cnt, int n, int *s_pre, bool &wide) {
+    __shared__ int s_w[4];
+    const int t = threadIdx.x, lane = t & 63;
+    const int ra = 2 * t < n ? cnt[2 * t] : 0;
+    const int rb = 2 * t + 1 < n ? cnt[2 * t + 1] : 0;
+    wide = __syncthreads_or((ra | rb) & SX_TILE_WIDE) != 0;
+    const int a = SX_TILE_COUNT(ra), b = SX_TILE_COUNT(rb);
+    int v = a + b;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(v, o, 64);
+        if (lane >= o) v += y;
+    }
+    if (lane == 63) s_w[t >> 6] = v;
+    __syncthreads();
+    int off = 0;
+    for (int w = 0; w < (t >> 6); ++w) off += s_w[w];
+    const int excl = v + off - a - b;
+    if (2 * t < n) s_pre[2 * t] = excl;
+    if (2 * t + 1 < n) s_pre[2 * t + 1] = excl + a;
+    if (t == 0) s_pre[n] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    __syncthreads();
+    return s_pre[n];
+}
+
+// row of list position k (0 <= k < total): tile t holds positions [s_pre[t], s_pre[t+1]) at
+// rowlist[t*512 ...]; the cursor t moves from the previous lookup, either direction
+__device__ __forceinline__ int list_row(int k, int &t, const int *s_pre, const int *__restrict__ rowlist) {
+    while (s_pre[t + 1] <= k) ++t;
+    while (s_pre[t] > k) --t;
+    return rowlist[t * SX_TILE + (k - s_pre[t])];
+}
+
 template <int RB, bool SNAKE, bool SC1>
 __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows, int row0, size_t ld, Cols c,
                                                 double *__restrict__ d, const double *__restrict__ prow_buf,
                                                 size_t prow_stride, const double *__restrict__ colE, DevState *st,
                                                 double *__restrict__ rnew, size_t rnew_stride,
-                                                TilePart *enter_parts) {
+                                                TilePart *enter_parts, const int *__restrict__ rowlist,
+                                                const int *__restrict__ tile_cnt, int ntiles, int skip_zero) {
     if (st->status != SX_NOT_ENDED) return;
     const long long q = st->pivots;
     const int e = st->e;
@@ -414,91 +578,134 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows
                                   : ((q >= 2 && st->r_prev == st->r) ? rprev : T + (size_t)rl * ld);
     const double p = prow[c.map(1 + e)];
     if (blockIdx.y == 0) {
-        // ---- objective row + next entering argmin (512 reference threads on 256)
-        __shared__ double s_v[16];
-        __shared__ int s_i[16];
-        __shared__ int s_last;
-        const int L = c.N - 1;
-        const int B1 = (L + SX_TILE - 1) / SX_TILE;
-        if ((int)blockIdx.x >= B1) return;
-        const double fd = -st->dmin / p;
-        if (blockIdx.x == 0 && threadIdx.x == 0) d[0] = fma(fd, prow[0], d[0]);
-        double v0 = DBL_MAX, v1 = DBL_MAX;
-        int i0 = -1, i1 = -1;
-        const int ia = blockIdx.x * SX_TILE + threadIdx.x, ib = ia + 256;
-        if (ia < L) {
-            const double x = fma(fd, prow[c.map(1 + ia)], d[1 + ia]);
-            d[1 + ia] = x;
-            if (cmp_eps(x, v0) < 0) {
-                v0 = x;
-                i0 = ia;
-            }
-        }
-        if (ib < L) {
-            const double x = fma(fd, prow[c.map(1 + ib)], d[1 + ib]);
-            d[1 + ib] = x;
-            if (cmp_eps(x, v1) < 0) {
-                v1 = x;
-                i1 = ib;
-            }
-        }
-        half_argmin(v0, i0);  // reference warps 0..7
-        half_argmin(v1, i1);  // reference warps 8..15
-        const int lane = threadIdx.x & 31, h = threadIdx.x >> 5;
-        if (lane == 0) {
-            s_v[h] = v0;
-            s_i[h] = i0;
-            s_v[h + 8] = v1;
-            s_i[h + 8] = i1;
-        }
-        __syncthreads();
-        if (threadIdx.x < 32) {
-            double v = (threadIdx.x < 16) ? s_v[threadIdx.x] : DBL_MAX;
-            int i = (threadIdx.x < 16) ? s_i[threadIdx.x] : -1;
-            half_argmin(v, i);
-            if (threadIdx.x == 0) {
-                store_tile_sc1(enter_parts + blockIdx.x, v, i, 0);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                const unsigned t = __hip_atomic_fetch_add(&st->ticket_d, 1u, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT);
-                s_last = (t == (unsigned)B1 - 1);
-            }
-        }
-        __syncthreads();
-        if (!s_last) return;
-        // last objective block: pass 2 (reference pass-2 tree; B1 <= 256 here)
-        double v = DBL_MAX;
-        int i = -1;
-        if ((int)threadIdx.x < B1) {
-            double cv;
-            int ci, ce;
-            load_tile_sc1(enter_parts + threadIdx.x, cv, ci, ce);
-            if (cmp_eps(cv, v) < 0) {
-                v = cv;
-                i = ci;
-            }
-        }
-        half_argmin(v, i);
-        __syncthreads();
-        if (lane == 0) {
-            s_v[h] = v;
-            s_i[h] = i;
-        }
-        __syncthreads();
-        if (threadIdx.x < 32) {
-            v = (threadIdx.x < 8) ? s_v[threadIdx.x] : DBL_MAX;
-            i = (threadIdx.x < 8) ? s_i[threadIdx.x] : -1;
-            half_argmin(v, i);
-            if (threadIdx.x == 0) {
-                st->e_next = i;
-                st->dmin_next = v;
-                st->ticket_d = 0;
-            }
-        }
+        objective_row(prow, p, d, st, enter_parts, c);
         return;
     }
-    const int rg = gridDim.y - 1;  // row groups of T
-    const int N = c.Ns;            // stored columns
+    // ---- tableau rows: a fixed set of G blocks per 512-column tile sweeps the rows; each
+    // thread holds its two pivot-row values for the whole sweep
+    const int G = gridDim.y - 1;
+    const int N = c.Ns;  // stored columns
+    const int cb = (N + 511) / 512;
+    if ((int)blockIdx.x >= cb) return;
+    const bool rev = SNAKE && (q & 1);
+    const int bx = rev ? cb - 1 - (int)blockIdx.x : (int)blockIdx.x;
+    const int by = blockIdx.y - 1;
+    const int j = (bx * 256 + threadIdx.x) * 2;
+    const bool active = j < N, pair = j + 1 < N;
+    double2 pr = make_double2(0.0, 0.0);
+    if (active) {
+        if (pair)
+            pr = *reinterpret_cast<const double2 *>(prow + j);
+        else
+            pr.x = prow[j];
+    }
+    // Rows left out of the sweep (factor exactly +-0) keep their bits only when every
+    // fma(+-0, p, x) == x: p finite (checked here, per column tile) and x != -0.0 (the engine
+    // passes skip_zero only for tableaux without -0.0).  Otherwise the tile sweeps all rows.
+    __shared__ int s_pre[SX_TILE + 1];
+    const bool listed = skip_zero && __syncthreads_and(isfinite(pr.x) && isfinite(pr.y));
+    bool wide = true;
+    const int total = listed ? scan_tile_counts(tile_cnt, ntiles, s_pre, wide) : rows;
+    // Columns whose pivot-row pair is (+-0, +-0) are left as they are, in every row but the
+    // pending one (its values come from rprev): fma(f, +-0, x) == x for finite f and x != -0.0.
+    // Those lanes' loads and stores carry an out-of-range buffer offset, which the hardware
+    // drops -- no memory access, and no branch in the loop.
+    const bool zc = active && listed && !wide && pr.x == 0.0 && pr.y == 0.0;
+    {
+        const int nzp = __syncthreads_count(active && !zc);
+        if (by == 0 && threadIdx.x == 0) atomicAdd(&st->touched_pairs, nzp);
+    }
+    if (!active) return;
+    const int ng = (total + RB - 1) / RB;
+    if (by >= ng) return;
+    int tc = rev ? ntiles - 1 : 0;  // tile cursor of the list lookups
+    const double2 rp = make_double2(pr.x / p, pr.y / p);  // the new pivot row
+    // The loop body is straight-line memory code (no loads or stores under branches), so
+    // the compiler's wait counters can keep the next group's loads in flight across the
+    // current group's stores.  Past the end of the list a group repeats its first row (same
+    // thread, same value), and a fetch past the last group reads rprev.  The thread of an odd
+    // last column moves the pair (j, j+1): j+1 < ld is row padding (or, in phase 2 without
+    // aliasing, a dead artificial column).
+    const int off_j = j * 8;
+    const int oob = (int)(ld * 8);  // past the descriptor's range: the access is dropped
+    auto fetch = [&](int g, int *row, double2 *x, double *f) {
+        const bool live = g < ng;
+        const int gg = rev ? ng - 1 - g : g;
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+            const int idx = gg * RB + k;
+            int r = (live && idx < total) ? (listed ? list_row(idx, tc, s_pre, rowlist) : idx) : -1;
+            r = __builtin_amdgcn_readfirstlane(r);
+            row[k] = (k > 0 && r < 0) ? row[0] : r;
+        }
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+            const bool from_prev = row[k] == pl;
+            const double *src = (row[k] < 0 || from_prev) ? rprev : T + (size_t)row[k] * ld;
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(src), 0, oob,
+                                                                               0x00020000);
+            const bool skip = row[k] < 0 || row[k] == rl || (zc && !from_prev);
+            x[k] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, skip ? oob : off_j, 0, 0));
+            f[k] = row[k] >= 0 ? -colE[row[k]] / p : 0.0;
+        }
+    };
+    auto update = [&](const int *row, const double2 *x, const double *f) {
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+            const bool is_r = row[k] == rl;
+            double *dst = is_r ? rout : T + (size_t)row[k] * ld;
+            double2 y;
+            y.x = is_r ? rp.x : fma(f[k], pr.x, x[k].x);
+            y.y = is_r ? rp.y : fma(f[k], pr.y, x[k].y);
+            // a lane of a zero column keeps x only if f is finite (checked per row: uniform)
+            const bool skip = zc && !is_r && row[k] != pl && isfinite(f[k]);
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, oob, 0x00020000);
+            if (SC1)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, skip ? oob : off_j, 0, 16);
+            else
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, skip ? oob : off_j, 0, 0);
+        }
+    };
+    // software pipeline, ping-pong between two register sets: the loads of group g+G are in
+    // flight while group g is updated
+    int ra[RB], rb_[RB];
+    double2 xa[RB], xb[RB];
+    double fa[RB], fb[RB];
+    fetch(by, ra, xa, fa);
+    for (int g = by; g < ng; g += 2 * G) {
+        fetch(g + G, rb_, xb, fb);
+        update(ra, xa, fa);
+        if (g + G >= ng) break;
+        fetch(g + 2 * G, ra, xa, fa);
+        update(rb_, xb, fb);
+    }
+}
+
+// One-shot variant of the update: one block per (512 columns, RB rows), the whole tableau in
+// one grid -- the hardware's in-order dispatch keeps the active window of rows tight, which
+// streams best when every row is swept.  Zero-factor rows are skipped per thread (same
+// exactness conditions as the list sweep) but their blocks still run.
+template <int RB, bool SNAKE, bool SC1>
+__global__ __launch_bounds__(256) void k_update_grid(double *__restrict__ T, int rows, int row0, size_t ld, Cols c,
+                                                     double *__restrict__ d, const double *__restrict__ prow_buf,
+                                                     size_t prow_stride, const double *__restrict__ colE,
+                                                     DevState *st, double *__restrict__ rnew, size_t rnew_stride,
+                                                     TilePart *enter_parts, int skip_zero) {
+    if (st->status != SX_NOT_ENDED) return;
+    const long long q = st->pivots;
+    const int rl = st->r - row0;
+    const int pl = (q >= 2 && st->r_prev != st->r) ? st->r_prev - row0 : -1;
+    const double *rprev = rnew + (size_t)((q - 1) & 1) * rnew_stride;
+    double *rout = rnew + (size_t)(q & 1) * rnew_stride;
+    const double *prow = prow_buf ? (prow_stride ? prow_buf + (size_t)(st->r / SX_TILE) * prow_stride + 2 : prow_buf)
+                                  : ((q >= 2 && st->r_prev == st->r) ? rprev : T + (size_t)rl * ld);
+    const double p = prow[c.map(1 + st->e)];
+    if (blockIdx.y == 0) {
+        objective_row(prow, p, d, st, enter_parts, c);
+        return;
+    }
+    const int rg = gridDim.y - 1;
+    const int N = c.Ns;
     const int cb = (N + 511) / 512;
     if ((int)blockIdx.x >= cb) return;
     int bx = blockIdx.x, by = blockIdx.y - 1;
@@ -516,59 +723,27 @@ __global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows
     const int j = (bx * 256 + threadIdx.x) * 2;
     if (j >= N) return;
     const int nrow = rows - i0 < RB ? rows - i0 : RB;
-    if (j + 1 < N) {
-        const double2 pr = *reinterpret_cast<const double2 *>(prow + j);
-        double *base = T + (size_t)i0 * ld + j;
-        if (nrow == RB) {
-            const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(T + (size_t)i0 * ld, 0, (int)(RB * ld * 8), 0x00020000);
-            double2 x[RB];
+    // pair (j, j+1) always: j+1 < ld (see k_update)
+    const double2 pr = *reinterpret_cast<const double2 *>(prow + j);
+    const bool fin = skip_zero && isfinite(pr.x) && isfinite(pr.y);
+    double *base = T + (size_t)i0 * ld + j;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(T + (size_t)i0 * ld, 0, (int)(RB * ld * 8), 0x00020000);
+    bool skip[RB];
+    double2 x[RB];
 #pragma unroll
-            for (int k = 0; k < RB; ++k)
-                if (i0 + k != rl)
-                    x[k] = *reinterpret_cast<const double2 *>(i0 + k == pl ? rprev + j : base + (size_t)k * ld);
+    for (int k = 0; k < RB; ++k) {
+        skip[k] = k >= nrow || i0 + k == rl || (fin && s_f[k] == 0.0 && i0 + k != pl);
+        if (!skip[k]) x[k] = *reinterpret_cast<const double2 *>(i0 + k == pl ? rprev + j : base + (size_t)k * ld);
+    }
 #pragma unroll
-            for (int k = 0; k < RB; ++k) {
-                if (i0 + k == rl) {
-                    double2 y;
-                    y.x = pr.x / p;
-                    y.y = pr.y / p;
-                    *reinterpret_cast<double2 *>(rout + j) = y;
-                } else {
-                    const double f = s_f[k];
-                    x[k].x = fma(f, pr.x, x[k].x);
-                    x[k].y = fma(f, pr.y, x[k].y);
-                    store_pair<SC1>(base + (size_t)k * ld, x[k], rs, (int)(((size_t)k * ld + j) * 8));
-                }
-            }
-        } else {
-            for (int k = 0; k < nrow; ++k) {
-                if (i0 + k == rl) {
-                    double2 y;
-                    y.x = pr.x / p;
-                    y.y = pr.y / p;
-                    *reinterpret_cast<double2 *>(rout + j) = y;
-                } else {
-                    double2 x = *reinterpret_cast<const double2 *>(i0 + k == pl ? rprev + j : base + (size_t)k * ld);
-                    const double f = s_f[k];
-                    x.x = fma(f, pr.x, x.x);
-                    x.y = fma(f, pr.y, x.y);
-                    *reinterpret_cast<double2 *>(base + (size_t)k * ld) = x;
-                }
-            }
-        }
-    } else {
-        // last (odd) column of the phase width: scalar path
-        const double pr = prow[j];
-        for (int k = 0; k < nrow; ++k) {
-            if (i0 + k == rl) {
-                rout[j] = pr / p;
-            } else {
-                double *x = T + (size_t)(i0 + k) * ld + j;
-                const double old = (i0 + k == pl) ? rprev[j] : *x;
-                *x = fma(s_f[k], pr, old);
-            }
-        }
+    for (int k = 0; k < RB; ++k) {
+        if (k < nrow && i0 + k == rl)
+            *reinterpret_cast<double2 *>(rout + j) = make_double2(pr.x / p, pr.y / p);
+        if (skip[k]) continue;
+        x[k].x = fma(s_f[k], pr.x, x[k].x);
+        x[k].y = fma(s_f[k], pr.y, x[k].y);
+        store_pair<SC1>(base + (size_t)k * ld, x[k], rs, (int)(((size_t)k * ld + j) * 8));
     }
 }
 
@@ -715,38 +890,79 @@ void sx_launch_enter(const double *d, int L, TilePart *parts, DevState *st, hipS
 
 void sx_launch_ratio_select(const double *T, int rows, int row0, size_t ld, TilePart *tiles_local, double *colE,
                             DevState *st, int *base, const double *rnew, size_t rnew_stride, bool select,
-                            double *slots, size_t slot_stride, Cols c, hipStream_t s) {
+                            double *slots, size_t slot_stride, Cols c, int *rowlist, int *tile_cnt, int skip_zero,
+                            hipStream_t s) {
     int g = (rows + SX_TILE - 1) / SX_TILE;
     if (g < 1) g = 1;  // a shard without rows still decides optimality for its own state
     if (select && g > SX_TILE) SX_FATAL("too many ratio tiles for the 512-thread pass 2");
     k_ratio_select<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, tiles_local, colE, st, base, rnew, rnew_stride,
-                                         select ? 1 : 0, slots, slot_stride, c);
+                                         select ? 1 : 0, slots, slot_stride, c, rowlist, tile_cnt, skip_zero);
 }
 
 void sx_launch_select_gathered(const double *slots, size_t slot_stride, int B2, int *base, DevState *st,
-                               hipStream_t s) {
+                               int tile0, int nslots, hipStream_t s) {
     if (B2 > SX_TILE) SX_FATAL("too many ratio tiles for the 512-thread pass 2");
-    k_select_gathered<<<1, SX_TILE, 0, s>>>(slots, slot_stride, B2, base, st);
+    k_select_gathered<<<1, SX_TILE, 0, s>>>(slots, slot_stride, B2, base, st, tile0, nslots);
 }
 
 void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, Cols c, const TilePart *tiles_all, int B2,
                           double *prow_out, int *base, DevState *st, const double *rnew, size_t rnew_stride,
-                          hipStream_t s) {
+                          int tile0, int nslots, hipStream_t s) {
     if (B2 > SX_TILE) SX_FATAL("too many ratio tiles for the 512-thread pass 2");
     const int N = c.Ns;
     int g = (N + 4 * SX_TILE - 1) / (4 * SX_TILE);
     if (g < 1) g = 1;
     if (g > 64) g = 64;
-    k_select_row<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, N, tiles_all, B2, prow_out, base, st, rnew, rnew_stride);
+    k_select_row<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, N, tiles_all, B2, prow_out, base, st, rnew, rnew_stride,
+                                       tile0, nslots);
+}
+
+// blocks of a kernel resident on the whole device at once
+template <typename K>
+static int update_capacity(K kernel) {
+    static int cap = 0;  // per kernel instantiation
+    if (cap == 0) {
+        int per_cu = 0, dev = 0, cus = 0;
+        SX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0));
+        SX_HIP(hipGetDevice(&dev));
+        SX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        cap = (per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 1);
+    }
+    return cap;
+}
+
+// row-sweeping blocks per column tile: the whole grid (objective row + G rows of tiles)
+// resident in one wave, each block looping over its share of the row groups
+static float g_update_waves = 2.0f;
+void sx_set_update_waves(float w) { g_update_waves = w > 0.f ? w : 2.0f; }
+
+static int row_slots(int capacity, int col_blocks, int rows, int rb) {
+    long long g = (long long)(g_update_waves * (float)capacity) / col_blocks - 1;
+    const long long groups = rows > 0 ? (rows + rb - 1) / rb : 1;
+    if (g > groups) g = groups;
+    if (g < 1) g = 1;
+    if (g > 65535 - 1) g = 65535 - 1;
+    return (int)g;
 }
 
 template <int RB>
 static void launch_update_rb(dim3 grid, bool snake, bool sc1, double *T, int rows, int row0, size_t ld, Cols N,
                              double *d, const double *prow_buf, size_t prow_stride, const double *colE, DevState *st,
-                             double *rnew, size_t rnew_stride, TilePart *enter_parts, hipStream_t s) {
-#define SX_UPD(SN, SC)                                                                                        \
-    k_update<RB, SN, SC><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, \
-                                              rnew_stride, enter_parts)
+                             double *rnew, size_t rnew_stride, TilePart *enter_parts, const int *rowlist,
+                             const int *tile_cnt, int ntiles, int skip_zero, bool one_shot, hipStream_t s) {
+#define SX_UPD(SN, SC)                                                                                           \
+    do {                                                                                                         \
+        if (one_shot) {                                                                                          \
+            grid.y = 1 + (rows > 0 ? (rows + RB - 1) / RB : 0);                                                  \
+            k_update_grid<RB, SN, SC><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow_buf, prow_stride, colE,  \
+                                                           st, rnew, rnew_stride, enter_parts, skip_zero);      \
+        } else {                                                                                                 \
+            grid.y = 1 + row_slots(update_capacity(k_update<RB, SN, SC>), grid.x, rows, RB);                    \
+            k_update<RB, SN, SC><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st,   \
+                                                      rnew, rnew_stride, enter_parts, rowlist, tile_cnt, ntiles,  \
+                                                      skip_zero);                                                \
+        }                                                                                                        \
+    } while (0)
     if (snake) {
         if (sc1)
             SX_UPD(true, true);
@@ -763,21 +979,25 @@ static void launch_update_rb(dim3 grid, bool snake, bool sc1, double *T, int row
 
 void sx_launch_update(double *T, int rows, int row0, size_t ld, Cols N, double *d, const double *prow_buf,
                       size_t prow_stride, const double *colE, DevState *st, double *rnew, size_t rnew_stride,
-                      TilePart *enter_parts, UpdateCfg cfg, hipStream_t s) {
+                      TilePart *enter_parts, const int *rowlist, const int *tile_cnt, UpdateCfg cfg, hipStream_t s) {
     const int B1 = (N.N - 1 + SX_TILE - 1) / SX_TILE;
     if (B1 > 256) SX_FATAL("entering vector too long for the update's pass 2");
     int cols_blocks = (N.Ns + 511) / 512;
     if (cols_blocks < B1) cols_blocks = B1;
-    const int rb = cfg.rows_per_block;
-    const int rg = rows > 0 ? (rows + rb - 1) / rb : 0;
-    dim3 grid(cols_blocks, rg + 1);
-    const bool sn = cfg.snake != 0;
-    switch (rb) {
-    case 1: launch_update_rb<1>(grid, sn, cfg.sc1 != 0, T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, rnew_stride, enter_parts, s); break;
-    case 2: launch_update_rb<2>(grid, sn, cfg.sc1 != 0, T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, rnew_stride, enter_parts, s); break;
-    case 4: launch_update_rb<4>(grid, sn, cfg.sc1 != 0, T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, rnew_stride, enter_parts, s); break;
-    default: launch_update_rb<8>(grid, sn, cfg.sc1 != 0, T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, rnew_stride, enter_parts, s); break;
+    const int ntiles = rows > 0 ? (rows + SX_TILE - 1) / SX_TILE : 1;  // k_ratio_select's grid
+    if (ntiles > SX_TILE) SX_FATAL("too many row tiles for the update's list scan");
+    dim3 grid(cols_blocks, 2);
+    const bool sn = cfg.snake != 0, sc = cfg.sc1 != 0;
+#define SX_RB(R)                                                                                             \
+    launch_update_rb<R>(grid, sn, sc, T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, rnew_stride, \
+                        enter_parts, rowlist, tile_cnt, ntiles, cfg.skip_zero, cfg.one_shot != 0, s)
+    switch (cfg.rows_per_block) {
+    case 1: SX_RB(1); break;
+    case 2: SX_RB(2); break;
+    case 4: SX_RB(4); break;
+    default: SX_RB(8); break;
     }
+#undef SX_RB
 }
 
 void sx_launch_flush_row(double *T, int rows, int row0, size_t ld, int Ns, const double *rnew, size_t rnew_stride,

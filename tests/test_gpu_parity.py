@@ -193,24 +193,49 @@ def test_session_pivots(gpu):
     s.close()
 
 
+@pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("rb", [1, 2, 4, 8])
 @pytest.mark.parametrize("snake", [0, 1])
 @pytest.mark.parametrize("sc1", [0, 1])
-def test_update_configs_bit_exact(gpu, rb, snake, sc1):
-    """every (rows per block, sweep order, store flavour) variant of the update kernel gives
-    the same bits"""
+def test_update_configs_bit_exact(gpu, mode, rb, snake, sc1):
+    """every (kernel form, rows per block/iteration, sweep order, store flavour) variant of the
+    update kernel gives the same bits"""
     T, d, base = _phase1_state(333, 1025, 7)
     Tg, dg, bg = T.copy(), d.copy(), base.copy()
     try:
+        sx.set_update_mode(mode)
         sx.set_update_rows(rb)
         sx.set_snake(snake)
         sx.set_store_sc1(sc1)
         sx.dev_pivots(Tg, dg, bg, 21)
     finally:
+        sx.set_update_mode(-1)
         sx.set_update_rows(0)
         sx.set_snake(-1)
         sx.set_store_sc1(-1)
     oracle.solve(T, d, base, max_pivots=21)
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+@pytest.mark.parametrize("waves", [1e-4, 0.3, 2, 64])
+@pytest.mark.parametrize("skip", [0, 1])
+def test_update_row_sweep_slots_bit_exact(gpu, waves, skip):
+    """the resident row sweep with 1 block per column tile (every block walks all row groups,
+    both directions) up to more blocks than row groups"""
+    T, d, base = _phase1_state(210, 1700, 3)
+    Tg, dg, bg = T.copy(), d.copy(), base.copy()
+    try:
+        sx.set_update_mode(0)
+        sx.set_update_waves(waves)
+        sx.set_skip_zero(skip)
+        sx.set_snake(1)
+        sx.dev_pivots(Tg, dg, bg, 90)
+    finally:
+        sx.set_update_mode(-1)
+        sx.set_update_waves(0)
+        sx.set_skip_zero(1)
+        sx.set_snake(-1)
+    oracle.solve(T, d, base, max_pivots=90)
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 
@@ -270,3 +295,71 @@ def test_pivots_without_alias_invariant(gpu):
     sx.dev_pivots(Tg, dg, bg, 30)
     oracle.solve(T, d, base, max_pivots=30)
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+# ------------------------------------------------------------------ zero-factor row skipping
+@pytest.mark.parametrize("skip", [0, 1])
+@pytest.mark.parametrize("rb,W", [(1, 1), (2, 1), (8, 1), (2, 3)])
+def test_skip_zero_bit_exact(gpu, skip, rb, W):
+    """rows whose entering-column entry is exactly 0 are left untouched: same bits as the
+    oracle's full sweep (about half of the phase-1 pivots bring in a slack column whose entries
+    are almost all 0)"""
+    T, d, base = _phase1_state(300, 1100, 11)
+    Tg, dg, bg = T.copy(), d.copy(), base.copy()
+    try:
+        sx.set_skip_zero(skip)
+        sx.set_update_rows(rb)
+        sx.set_virtual_ranks(W)
+        sx.dev_pivots(Tg, dg, bg, 120)
+    finally:
+        sx.set_skip_zero(1)
+        sx.set_update_rows(0)
+        sx.set_virtual_ranks(1)
+    oracle.solve(T, d, base, max_pivots=120)
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+@pytest.mark.parametrize("lo", [-100, 1])
+def test_skip_zero_disengaged_with_negative_zeros(gpu, lo):
+    """a tableau holding -0.0 (the b<0 row negation of the build, or a caller's upload) must be
+    swept in full: fma(0, p, -0.0) is +0.0, so skipping would change bits"""
+    T, d, base = _phase1_state(200, 700, 5, lo, 100)
+    if lo > 0:
+        T[T == 0.0] = -0.0
+    assert np.signbit(T[T == 0.0]).any()
+    Tg, dg, bg = T.copy(), d.copy(), base.copy()
+    sx.dev_pivots(Tg, dg, bg, 60)
+    oracle.solve(T, d, base, max_pivots=60)
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+def test_skip_zero_two_phase_negated_rows(gpu):
+    """generated instances with b_i < 0 (values in [-100, 100]): host and device builds"""
+    p = sx.generateRandomProblem(150, 700, 1234, -100, 100)
+    _check_two_phase(p)
+    s = sx.Session(generated=(150, 700, 1234, -100, 100))
+    t = s.pivots(40, time_updates=1)
+    assert t.touched_rows == 40 * 700  # full sweeps: the tableau holds -0.0
+    s.close()
+
+
+def test_session_touched_rows(gpu):
+    """touched-row accounting of the timed updates: full sweeps with skipping off, fewer rows
+    with it on, and the same pivots either way"""
+    n, m = 2048, 1024
+    res = {}
+    for skip in (0, 1):
+        try:
+            sx.set_skip_zero(skip)
+            s = sx.Session(generated=(n, m, n * 100 + m, 1, 100))
+            t = s.pivots(400, time_updates=1)
+            res[skip] = (t, s.objective())
+            s.close()
+        finally:
+            sx.set_skip_zero(1)
+    t0, t1 = res[0][0], res[1][0]
+    assert t0.touched_rows == 400 * m
+    assert t0.touched_bytes == pytest.approx(400 * t0.update_bytes, rel=1e-3)  # pairs: ceil(width / 2)
+    assert 400 <= t1.touched_rows < t0.touched_rows
+    assert t1.touched_bytes < t0.touched_bytes
+    assert same(res[0][1], res[1][1])
