@@ -3,8 +3,10 @@
 Workload (BASELINE.json configs[2], the config the roofline target is quoted on):
 generateRandomProblem(n=8192, m=4096, seed=823296, [1,100]) -- the reference's own -t
 instance (main.cu:56-64) -- phase-1 tableau 4096 x 16385 fp64 (537 MB) resident in HBM.
-A "step" is one simplex pivot (entering argmin, ratio test, pivot-row fetch, rank-1
-update of the whole tableau).  W untimed pivots, then K timed pivots.
+A "step" is one simplex pivot (entering argmin, ratio test, pivot row, objective row, and
+the rank-1 update of the whole tableau -- applied in sweeps of 16 pivots).
+W untimed pivots, then K timed pivots: by default pivots 50..8950 of the instance's 8981
+phase-1 pivots, i.e. the whole phase at its real mix of sparse and dense pivots.
 
 N GPUs (torchrun, one process per GPU): the constraint rows are split into N contiguous
 512-aligned blocks; every pivot does one tile-winner allgather and one pivot-row
@@ -93,16 +95,16 @@ def cpu_baseline(n, m, seed, pivots, sx):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000, help="timed pivots")
+    ap.add_argument("--steps", type=int, default=8900, help="timed pivots")
     ap.add_argument("--warmup", type=int, default=50, help="untimed pivots before timing")
     ap.add_argument("--config", default="config3", choices=sorted(CONFIGS))
-    ap.add_argument("--update-rows", type=int, default=0, help="rows per update workgroup (0 = auto)")
-    ap.add_argument("--snake", type=int, default=-1, help="alternate update sweep: -1 auto, 0 off, 1 on")
+    ap.add_argument("--update-rows", type=int, default=0, help="rows per sweep step (0 = auto)")
+    ap.add_argument("--batch", type=int, default=0, help="pivots per tableau sweep (0 = library default, 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--update-events", type=int, default=8,
-                    help="bracket every k-th update launch with HIP events (0 = none)")
-    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_update_config3.json"),
-                    help="per-launch HBM bytes of the update kernel from rocprofv3 --pmc (JSON)")
+    ap.add_argument("--update-events", type=int, default=1,
+                    help="bracket every k-th sweep launch with HIP events (0 = none)")
+    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_sweep_config3.json"),
+                    help="per-launch HBM bytes of the sweep kernel from rocprofv3 --pmc (JSON)")
     ap.add_argument("--secondary", default="config5",
                     help="second workload timed in the same run ('' to skip): the m=32768 scaling problem")
     ap.add_argument("--secondary-steps", type=int, default=40)
@@ -127,7 +129,7 @@ def main():
     else:
         sx.load().simplex_set_device(local_rank)
     sx.set_update_rows(args.update_rows)
-    sx.set_snake(args.snake)
+    sx.set_batch(args.batch)
 
     def barrier():
         if world > 1:
@@ -156,9 +158,8 @@ def main():
             elapsed = float(tt.item())
         sess.close()
         avg_update_s = tim.update_ms / 1e3 / max(tim.update_launches, 1)
-        # algorithmic bytes of the launches actually timed: rows with an exactly-zero factor are
-        # left untouched (bit-exact), so only the touched rows count
-        achieved = tim.touched_bytes / (tim.update_ms / 1e3) / 1e9 if tim.update_launches else None
+        # algorithmic bytes of a sweep: every stored tableau element read and written once
+        achieved = tim.swept_bytes / (tim.update_ms / 1e3) / 1e9 if tim.update_launches else None
         return {"n": n, "m": m, "seed": seed, "tim": tim, "elapsed": elapsed, "pivots": tim.pivots,
                 "avg_update_s": avg_update_s, "achieved": achieved, "setup_s": t_setup}
 
@@ -197,12 +198,12 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS if achieved else None,
             "traffic": traffic,
-            "kernel": "k_update (rank-1 pivot update, rank 0)",
-            "algorithmic_bytes_per_launch": tim.touched_bytes / max(tim.update_launches, 1),
-            "dense_bytes_per_launch": tim.update_bytes,
-            "touched_row_fraction": tim.touched_rows / max(tim.update_launches * tim.local_rows, 1),
+            "kernel": "k_sweep (rank-1 pivot updates of a batch applied to the tableau, rank 0)",
+            "algorithmic_bytes_per_launch": tim.update_bytes,
+            "pivots_per_launch": tim.swept_pivots / max(tim.update_launches, 1),
             "avg_launch_us": avg_update_s * 1e6,
             "timed_launches": tim.update_launches,
+            "sweep_share_of_time": tim.update_ms / max(tim.wall_ms, 1e-9),
         },
         "cpu_baseline": None,
     }

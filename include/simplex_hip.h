@@ -22,10 +22,13 @@ extern "C" {
 /* ---- configuration ---- */
 int simplex_version(void);
 void simplex_set_verbose(int on);            /* reference progress lines on stdout */
-void simplex_set_update_rows(int rb);        /* rows per update workgroup: 1, 2, 4, 8; 0 = auto */
-void simplex_set_snake(int mode);            /* alternate update sweep direction: -1 auto, 0, 1 */
+void simplex_set_update_rows(int rb);        /* rows per sweep step: 1, 2, 4; 0 = auto */
+void simplex_set_snake(int mode);            /* kept for ABI compatibility: sweeps always alternate direction */
 void simplex_set_store_sc1(int mode);        /* write-through tableau stores: -1 auto, 0, 1 */
-void simplex_set_batch(int pivots);          /* pivots enqueued between status polls */
+/* pivots per tableau sweep (1..32, default 16): the pivots of a batch are selected on the
+ * current values (pending pivots applied on the fly) and then applied to the tableau in one
+ * sweep -- the same IEEE operations in the same order as one sweep per pivot */
+void simplex_set_batch(int pivots);
 void simplex_set_device(int device);
 /* write the reference's -D TIMER CSV (chrono.cu) into `dir` (NULL or "" = off; env
  * SIMPLEX_TIMER_DIR also enables it); benchmark mode names it benchmark_<n>_<m>.txt */
@@ -48,15 +51,8 @@ void simplex_set_force_exchange(int on);
 void simplex_set_exchange_mode(int mode);
 /* store each phase-1 artificial column as its (bit-identical) slack column: 1 on (default), 0 off */
 void simplex_set_alias(int on);
-/* rows whose entering-column entry is exactly 0 are left untouched by the update (default on).
- * Engaged only when it is bit-exact: the tableau holds no -0.0 (true unless a b_i < 0 row was
- * negated by the build quirk, or the caller uploads one) and the pivot-row values are finite. */
-void simplex_set_skip_zero(int on);
-/* the update's row sweep runs waves x (blocks resident on the device) blocks (default 2; <= 0 resets) */
+/* the sweep's grid: waves x (blocks resident on the device) blocks (default 1; <= 0 resets) */
 void simplex_set_update_waves(double waves);
-/* update kernel: -1 auto, 0 resident blocks sweeping the list of rows to update, 1 one block
- * per (512 columns, rows-per-block rows) over the whole tableau */
-void simplex_set_update_mode(int mode);
 
 /* ---- extended drop-in entry ---- */
 /* twoPhaseMethod + final basis (base_out[m]) and per-phase pivot counts (pivots_out[2]);
@@ -79,17 +75,16 @@ problem_t *simplex_generate_problem_device(int n, int m, unsigned int seed, int 
 /* ---- benchmark session: a resident phase-1 tableau and timed pivots ---- */
 typedef struct {
     double wall_ms;            /* device time of the whole call (events on the engine stream) */
-    double update_ms;          /* sum of the timed rank-1 update kernel durations (HIP events) */
+    double update_ms;          /* sum of the timed sweep kernel durations (HIP events) */
     long long pivots;          /* pivots applied during the call */
-    long long update_launches; /* update kernel launches timed */
+    long long update_launches; /* sweeps timed (those that applied at least one pivot) */
     int status;                /* phase status after the call (SIMPLEX_NOT_ENDED while running) */
     int width;                 /* tableau width N of the phase (reference counting) */
     int stored_width;          /* columns actually stored and swept (artificials alias slacks in phase 1) */
     long long local_rows;      /* constraint rows owned by this process */
-    double update_bytes;       /* dense bytes per update launch: 16 * local_rows * stored_width + 16 * N */
-    long long touched_rows;    /* timed launches: sum of the rows they swept (nonzero factor, or pending) */
-    double touched_bytes;      /* timed launches: sum of the bytes they move: 32 * rows * (column pairs with a
-                                  nonzero pivot-row entry) + 16 * N; the dense figure when skipping is off */
+    double update_bytes;       /* bytes per sweep: 16 * local_rows * stored_width (read + write of T) */
+    long long swept_pivots;    /* timed sweeps: pivots they applied */
+    double swept_bytes;        /* timed sweeps: bytes they moved */
 } simplex_timing_t;
 
 typedef struct simplex_session simplex_session;
@@ -97,13 +92,13 @@ simplex_session *simplex_session_open(problem_t *problem); /* builds phase 1 + c
 /* same tableau as simplex_session_open(generateRandomProblem(n, m, seed, lo, hi)), synthesised
  * directly in HBM (each shard generates only its rows; no host copy of A) */
 simplex_session *simplex_session_open_generated(int n, int m, unsigned int seed, int lo, int hi, int rand_kind);
-/* k pivots; time_updates = s > 0 brackets every s-th update launch with HIP events */
+/* k pivots (the call ends with a sweep, so the tableau is materialised on return);
+ * time_updates = s > 0 brackets every s-th sweep with HIP events */
 int simplex_session_pivots(simplex_session *s, long long k, int time_updates, simplex_timing_t *out);
 double simplex_session_objective(simplex_session *s);   /* d[0] */
 long long simplex_session_total_pivots(simplex_session *s);
-/* per timed launch of the last simplex_session_pivots call: rows the update swept (this
- * process's shards) and its duration in microseconds; returns the number of launches logged
- * (at most cap are copied) */
+/* per timed sweep of the last simplex_session_pivots call: pivots it applied and its
+ * duration in microseconds; returns the number of sweeps logged (at most cap are copied) */
 long long simplex_session_launch_log(simplex_session *s, long long *rows, double *update_us, long long cap);
 void simplex_session_close(simplex_session *s);
 

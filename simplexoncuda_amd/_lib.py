@@ -53,8 +53,8 @@ class TimingT(ctypes.Structure):
         ("stored_width", ctypes.c_int),
         ("local_rows", ctypes.c_longlong),
         ("update_bytes", ctypes.c_double),
-        ("touched_rows", ctypes.c_longlong),
-        ("touched_bytes", ctypes.c_double),
+        ("swept_pivots", ctypes.c_longlong),
+        ("swept_bytes", ctypes.c_double),
     ]
 
 
@@ -96,9 +96,7 @@ SIGNATURES = {
     "simplex_set_force_exchange": (None, [ctypes.c_int]),
     "simplex_set_exchange_mode": (None, [ctypes.c_int]),
     "simplex_set_alias": (None, [ctypes.c_int]),
-    "simplex_set_skip_zero": (None, [ctypes.c_int]),
     "simplex_set_update_waves": (None, [ctypes.c_double]),
-    "simplex_set_update_mode": (None, [ctypes.c_int]),
     "twoPhaseMethodEx": (ctypes.c_int, [P_PROBLEM, c_double_p, c_double_p, c_int_p, c_ll_p, ctypes.c_longlong]),
     "simplex_problem_from_arrays": (P_PROBLEM, [ctypes.c_int, ctypes.c_int, c_double_p, c_double_p, c_double_p]),
     "simplex_generate_problem_ex": (P_PROBLEM, [ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_int,

@@ -185,13 +185,14 @@ class Session:
             raise RuntimeError("simplex_session_open failed")
 
     def pivots(self, k, time_updates=0):
-        """k pivots; time_updates = s > 0 times every s-th update launch with HIP events."""
+        """k pivots (ending with a sweep, so the tableau is materialised); time_updates = s > 0
+        times every s-th tableau sweep with HIP events."""
         t = _lib.TimingT()
         self._lib.simplex_session_pivots(self._h, k, int(time_updates), ctypes.byref(t))
         return t
 
     def launch_log(self):
-        """(rows swept, update microseconds) per timed launch of the last pivots() call."""
+        """(pivots applied, sweep microseconds) per timed sweep of the last pivots() call."""
         n = self._lib.simplex_session_launch_log(self._h, None, None, 0)
         rows = np.zeros(max(n, 1), dtype=np.int64)
         us = np.zeros(max(n, 1), dtype=np.float64)
@@ -280,20 +281,9 @@ def set_alias(on):
     _lib.load().simplex_set_alias(1 if on else 0)
 
 
-def set_skip_zero(on):
-    """Leave rows with an exactly-zero entering-column entry untouched (default on; engaged
-    only where bit-exact, see include/simplex_hip.h)."""
-    _lib.load().simplex_set_skip_zero(1 if on else 0)
-
-
 def set_update_waves(w):
-    """Blocks of the update's row sweep as a multiple of the device's resident capacity."""
+    """Blocks of the tableau sweep as a multiple of the device's resident capacity (<= 0: default)."""
     _lib.load().simplex_set_update_waves(float(w))
-
-
-def set_update_mode(mode):
-    """-1 auto, 0 resident row-list sweep, 1 one-shot grid."""
-    _lib.load().simplex_set_update_mode(int(mode))
 
 
 def set_verbose(on):
@@ -313,4 +303,5 @@ def set_store_sc1(mode):
 
 
 def set_batch(p):
+    """Pivots per tableau sweep (1..32; <= 0: default 16)."""
     _lib.load().simplex_set_batch(int(p))

@@ -33,31 +33,43 @@ struct __attribute__((aligned(16))) TilePart {
 struct __attribute__((aligned(16))) DevState {
     int status;            // SX_NOT_ENDED while the phase runs
     int e;                 // entering variable of the current pivot (column e+1)
-    int r;                 // leaving row (global) of the current pivot; after the update its
-                           // new values sit in rnew[pivots & 1] until the next update writes
-                           // them back (the row is read in place as the pivot row meanwhile)
-    int r_prev;            // leaving row of the previous pivot
-    double dmin;           // reduced cost of the entering variable (d[e+1] before update)
-    long long pivots;      // pivots applied in this phase
+    int r;                 // leaving row (global) of the current pivot
+    int pad0;
+    double dmin;           // reduced cost of the entering variable (d[e+1] before the pivot)
+    long long pivots;      // pivots selected in this phase
     long long max_pivots;  // < 0: no cap (reference behaviour)
     int e_next;            // entering argmin of the updated objective row (next pivot)
     unsigned ticket;       // arrival counter of the ratio/select hand-off (zero between launches)
     double dmin_next;      // its value
-    unsigned ticket_d;     // arrival counter of the objective-row blocks of the update
-    int touched;           // this shard's rows the current update sweeps (rows with a nonzero factor)
-    int touched_pairs;     // column pairs of the current pivot row holding a nonzero (swept columns)
+    unsigned ticket_d;     // arrival counter of the objective-row blocks of k_pivot_row
+    unsigned batch_tag;    // batch id of the last selected pivot ...
+    int batch_count;       // ... and the number of pivots selected in that batch
     int pad1;
 };
 
-// tile_cnt[t] of a ratio tile: the number of listed rows, plus SX_TILE_WIDE when a listed
-// row's entry is too large for the factor -a/p to be finite with p >= eps
-#define SX_TILE_WIDE 0x40000000
-#define SX_TILE_COUNT(x) ((x) & (SX_TILE_WIDE - 1))
-
-// TilePart.elig packs "any entry >= eps" (bit 0) and the tile's count of nonzero
-// entering-column entries (bits 1..)
+// TilePart.elig: bit 0 = "some entry >= eps" of the tile (the unbounded test)
 #define SX_ELIG(x) ((x) & 1)
-#define SX_NNZ(x) ((x) >> 1)
+
+// Deferred pivots: at most SX_KMAX pivots between two sweeps of the tableau.
+#define SX_KMAX 32
+
+// Record of one pending pivot (slot s of the current batch).
+struct __attribute__((aligned(16))) PivRec {
+    int r;     // leaving row (global)
+    int e;     // entering variable
+    double p;  // pivot element
+};
+
+// Device buffers of the pending pivots of a shard, plus the batch id and slot of the pivot
+// being enqueued (kernel arguments).
+struct Pending {
+    double *U;               // [SX_KMAX][ld] pivot rows (current leaving-row values, before /p)
+    double *F;               // [rows][SX_KMAX] row factors -(a_ie / p)
+    PivRec *recs;            // [SX_KMAX]
+    unsigned long long *PM;  // [rows] (batch id << 32) | slots where the row left the basis
+    unsigned batch;          // id of the current batch (never 0)
+    int q;                   // slot of the pivot being enqueued (pivots pending before it)
+};
 
 // Error convention of the reference (error.cu:5-12): print "<msg> in <file> at line <n>"
 // and exit(EXIT_FAILURE).
@@ -79,31 +91,27 @@ struct Cols {
 };
 
 // ---- kernel launchers (sx_kernels.hip) ----
-struct UpdateCfg {
-    int rows_per_block;  // 1, 2, 4 or 8
-    int snake;           // alternate the sweep direction every pivot
+struct SweepCfg {
+    int batch;           // pivots per sweep (1..SX_KMAX): register slots of the sweep
+    int rows_per_block;  // 1, 2 or 4 rows per step
     int sc1;             // write-through (sc1) tableau stores
-    int skip_zero;       // skip rows whose factor is exactly zero (only when bit-exact: no -0.0 in T)
-    int one_shot;        // 1: one block per (512 columns, RB rows); 0: resident blocks sweep the row list
 };
 
 int sx_enter_blocks(int L);
 void sx_launch_enter(const double *d, int L, TilePart *parts, DevState *st, hipStream_t s);
 void sx_launch_ratio_select(const double *T, int rows, int row0, size_t ld, TilePart *tiles_local, double *colE,
-                            DevState *st, int *base, const double *rnew, size_t rnew_stride, bool select,
-                            double *slots, size_t slot_stride, Cols c, int *rowlist, int *tile_cnt, int skip_zero,
-                            hipStream_t s);
+                            DevState *st, int *base, bool select, double *slots, size_t slot_stride, Cols c,
+                            const Pending &pd, hipStream_t s);
 void sx_launch_select_gathered(const double *slots, size_t slot_stride, int B2, int *base, DevState *st,
-                               int tile0, int nslots, hipStream_t s);
+                               const Pending &pd, hipStream_t s);
 void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, Cols c, const TilePart *tiles_all, int B2,
-                          double *prow_out, int *base, DevState *st, const double *rnew, size_t rnew_stride,
-                          int tile0, int slots, hipStream_t s);
-void sx_launch_update(double *T, int rows, int row0, size_t ld, Cols c, double *d, const double *prow_buf,
-                      size_t prow_stride, const double *colE, DevState *st, double *rnew, size_t rnew_stride,
-                      TilePart *enter_parts, const int *rowlist, const int *tile_cnt, UpdateCfg cfg, hipStream_t s);
-void sx_set_update_waves(float w);  // resident-grid multiple of the update's row sweep (default 2)
-void sx_launch_flush_row(double *T, int rows, int row0, size_t ld, int Ns, const double *rnew, size_t rnew_stride,
-                         const DevState *st, hipStream_t s);
+                          double *prow_out, int *base, DevState *st, const Pending &pd, hipStream_t s);
+void sx_launch_pivot_row(const double *T, int rows, int row0, size_t ld, Cols c, double *d, const double *prow_buf,
+                         size_t prow_stride, const double *colE, DevState *st, const Pending &pd,
+                         TilePart *enter_parts, hipStream_t s);
+void sx_launch_sweep(double *T, int rows, size_t ld, int Ns, const Pending &pd, const DevState *st, int rev,
+                     SweepCfg cfg, hipStream_t s);
+void sx_set_update_waves(float w);  // resident-grid multiple of the sweep (default 1)
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s);
 
 void sx_launch_coef(const double *d, const int *base, int row0, int rows, double *coef, hipStream_t s);

@@ -4,8 +4,9 @@
 // Reference call structure replaced: twoPhaseMethod (twoPhaseMethod.cu:385)
 // -> phase1/phase2 (:225, :285) -> solve (solver.cu:128) -> per-iteration solve (:78).
 // The reference crosses PCIe ~10 times per pivot (blocking copies, mallocs, syncs).  Here a
-// pivot is four kernels (plus, on several GPUs, two RCCL collectives) enqueued on one
-// stream; the host only polls a pinned status word once per batch of pivots.
+// pivot is two kernels (plus, on several GPUs, one or two RCCL collectives) enqueued on one
+// stream, and the tableau itself is swept once per batch of pivots (deferred rank-1 updates,
+// DESIGN.md §3); the host only polls a pinned status word once per batch.
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -54,15 +55,13 @@ struct Config {
     int update_rows = 0;  // 0: auto (by tableau size)
     int snake = -1;       // -1: auto, 0: off, 1: on
     int sc1 = -1;         // write-through tableau stores: -1 auto, 0, 1
-    int batch = 16;
+    int batch = 16;          // pivots per tableau sweep (deferred updates), 1..SX_KMAX
     int device = -1;
     int virtual_ranks = 1;
     int force_exchange = 0;  // run the multi-shard exchange path even with one shard
     std::string timer_dir;   // non-empty: write the reference's TIMER CSV there
     int exchange_mode = 0;   // 0 auto, 1 tile allgather + row allreduce, 2 row-gather
     int alias = 1;           // store phase-1 artificial columns as their slack columns
-    int skip_zero = 1;       // leave zero-factor rows untouched where that is bit-exact
-    int update_mode = -1;    // -1 auto, 0 resident row-list sweep, 1 one-shot grid
     int debug = -1;          // -1: from SIMPLEX_DEBUG; 1: print the tableau after every step
     bool benchmark = false;
     // distributed
@@ -83,22 +82,6 @@ void say(const char *s) {
 }
 
 inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
-
-inline bool is_neg_zero(double v) { return v == 0.0 && std::signbit(v); }
-
-bool any_neg_zero(const double *v, size_t count) {
-    for (size_t i = 0; i < count; ++i)
-        if (is_neg_zero(v[i])) return true;
-    return false;
-}
-
-// the build quirk (twoPhaseMethod.cu:160-175) negates a whole row when compare(b_i) < 0:
-// its zero entries become -0.0
-bool any_negated_row(const double *b, int m) {
-    for (int i = 0; i < m; ++i)
-        if (compare(b[i], 0.0, SIMPLEX_EPSILON) < 0) return true;
-    return false;
-}
 
 template <typename T>
 T *dalloc(size_t count) {
@@ -178,7 +161,10 @@ struct Shard {
     double *prow_send = nullptr;
     double *slot_send = nullptr;  // row-gather: per tile [TilePart header | winner row]
     double *slot_all = nullptr;
-    double *rnew = nullptr;
+    double *U = nullptr;              // pending pivot rows [SX_KMAX][ld]
+    double *F = nullptr;              // pending row factors [rows][SX_KMAX]
+    PivRec *recs = nullptr;           // pending pivot records [SX_KMAX]
+    unsigned long long *PM = nullptr; // [rows] pending leaving-row slots (batch-tagged)
     double *coef = nullptr;
     double *gemv_local = nullptr;
     double *gemv_all = nullptr;
@@ -186,8 +172,6 @@ struct Shard {
     double *rhs_all = nullptr;
     int *base = nullptr;
     TilePart *enter_parts = nullptr;
-    int *rowlist = nullptr;   // per 512-row tile: the rows the update sweeps (k_ratio_select)
-    int *tile_cnt = nullptr;
     TilePart *tiles_local = nullptr;
     TilePart *tiles_all = nullptr;
     DevState *st = nullptr;
@@ -215,9 +199,11 @@ class Engine {
     hipEvent_t poll_ev[2] = {nullptr, nullptr};
     double *c_dev = nullptr;            // objective coefficients c (phase 2)
     long long phase_pivots[2] = {0, 0};
-    // no -0.0 anywhere in T: skipping rows whose factor is +-0 is then bit-exact (fma(+-0, p, x)
-    // == x for finite p and x != -0.0, and the update itself never creates a -0.0)
-    bool no_neg_zero = false;
+    // deferred pivots: the host numbers batches (ids never repeat, 0 is never used) and the
+    // slots inside the current one; every batch ends with a sweep of the tableau
+    unsigned batch_id = 1;
+    int q_host = 0;
+    long long sweeps = 0;
     std::function<void(int)> on_pivot;  // DEBUG trace: called after every pivot (solver.cu:112-116)
 
     Engine(int n_, int m_, bool alias_ = true) : n(n_), m(m_) {
@@ -302,14 +288,19 @@ class Engine {
             }
             SX_HIP(hipMemcpy(x.slot_send, init.data(), sizeof(double) * init.size(), hipMemcpyHostToDevice));
         }
-        x.rnew = dalloc<double>(2 * ld);
+        x.U = dalloc<double>((size_t)SX_KMAX * ld);
+        x.F = dalloc<double>(rows_alloc * SX_KMAX);
+        x.recs = dalloc<PivRec>(SX_KMAX);
+        x.PM = dalloc<unsigned long long>(rows_alloc);
+        SX_HIP(hipMemsetAsync(x.U, 0, (size_t)SX_KMAX * ld * sizeof(double), s));
+        SX_HIP(hipMemsetAsync(x.F, 0, rows_alloc * SX_KMAX * sizeof(double), s));
+        SX_HIP(hipMemsetAsync(x.recs, 0, SX_KMAX * sizeof(PivRec), s));
+        SX_HIP(hipMemsetAsync(x.PM, 0, rows_alloc * sizeof(unsigned long long), s));
         x.coef = dalloc<double>(rows_alloc);
         x.rhs_local = dalloc<double>(rpr);
         if (xchg) x.rhs_all = dalloc<double>((size_t)W * rpr);
         x.base = dalloc<int>(m);
         x.enter_parts = dalloc<TilePart>(SX_TILE);
-        x.rowlist = dalloc<int>((size_t)slots * SX_TILE);
-        x.tile_cnt = dalloc<int>(slots);
         x.tiles_local = dalloc<TilePart>(slots);
         if (xchg) x.tiles_all = dalloc<TilePart>((size_t)W * slots);
         x.st = dalloc<DevState>(1);
@@ -330,8 +321,9 @@ class Engine {
 
     void free_shard(Shard &x) {
         for (void *p : {(void *)x.T, (void *)x.d, (void *)x.colE, (void *)x.prow, (void *)x.prow_send,
-                        (void *)x.slot_send, (void *)x.slot_all, (void *)x.rnew, (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
-                        (void *)x.rhs_all, (void *)x.base, (void *)x.enter_parts, (void *)x.rowlist, (void *)x.tile_cnt, (void *)x.tiles_local,
+                        (void *)x.slot_send, (void *)x.slot_all, (void *)x.U, (void *)x.F, (void *)x.recs, (void *)x.PM,
+                        (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
+                        (void *)x.rhs_all, (void *)x.base, (void *)x.enter_parts, (void *)x.tiles_local,
                         (void *)x.tiles_all, (void *)x.st})
             if (p) (void)hipFree(p);
     }
@@ -354,9 +346,6 @@ class Engine {
             if (A_local) (void)hipFree(A_local);
         }
         (void)hipFree(b_dev);
-        no_neg_zero = !any_negated_row(P->knownTermsVector, m) &&
-                      !any_neg_zero(P->knownTermsVector, (size_t)m) &&
-                      !any_neg_zero(P->constraintsMatrix, (size_t)n * m);
         if (!c_dev) {
             c_dev = dalloc<double>(n);
             if (n > 0)
@@ -378,12 +367,8 @@ class Engine {
             sx_launch_build_rows(x.T, x.rows, x.row0, ld, n, m, Ns1, nullptr, b_dev, s);
             sx_launch_init_vectors(x.d, N1, n, m, x.base, s);
         }
-        // generated values fma(u, span, lo) are never -0.0; only the b < 0 quirk makes them
-        std::vector<double> b_host(m);
-        if (m > 0) SX_HIP(hipMemcpyAsync(b_host.data(), b_dev, sizeof(double) * m, hipMemcpyDeviceToHost, s));
         SX_HIP(hipStreamSynchronize(s));
         (void)hipFree(b_dev);
-        no_neg_zero = !any_negated_row(b_host.data(), m);
     }
 
     // ---------------------------------------------------------------- collectives
@@ -466,71 +451,89 @@ class Engine {
     }
 
     // ---------------------------------------------------------------- one pivot
-    UpdateCfg update_cfg() const {
-        // Measured in the real pivot loop (tools/pivot_profile.py, tools/sweep_update.py on
-        // MI355X).  The resident row-list sweep (mode 0) makes a pivot whose entering column is
-        // almost all zeros (about half of phase 1's: a slack column entering) cost ~10 us
-        // instead of a full sweep, and sweeps dense pivots within ~5 % of the one-shot grid:
-        // 4 rows per iteration, 2x the resident grid.  Above the 256 MB Infinity Cache,
-        // reversing the sweep every other pivot lets it start on the lines the previous one
-        // left in the cache, and write-through (sc1) stores help.
+    SweepCfg sweep_cfg(int batch) const {
+        // Measured in the real pivot loop (tools/sweep_update.py on MI355X): write-through
+        // (sc1) stores pay once the shard exceeds the 256 MB Infinity Cache.
         double bytes = 0.0;
         for (auto &x : sh) bytes = std::max(bytes, 8.0 * (double)x.rows * (double)cols(N).Ns);
         const bool big = bytes > 256.0 * 1024 * 1024;
-        UpdateCfg c;
-        c.one_shot = g_cfg.update_mode == 1 ? 1 : 0;
-        c.rows_per_block = g_cfg.update_rows > 0 ? g_cfg.update_rows : (c.one_shot ? (bytes > 4.0e9 ? 1 : 2) : 4);
-        c.snake = g_cfg.snake >= 0 ? g_cfg.snake : (big ? 1 : 0);
+        SweepCfg c;
+        c.batch = batch;
+        c.rows_per_block = g_cfg.update_rows > 0 ? std::min(g_cfg.update_rows, 4) : 2;
         c.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : (big ? 1 : 0);
-        c.skip_zero = (g_cfg.skip_zero && no_neg_zero) ? 1 : 0;
         return c;
     }
 
+    // pivots per sweep: the configured batch (1 while tracing every pivot)
+    int batch_size() const {
+        if (on_pivot) return 1;
+        return std::max(1, std::min(g_cfg.batch, SX_KMAX));
+    }
+
+    Pending pending(const Shard &x) const {
+        Pending p;
+        p.U = x.U;
+        p.F = x.F;
+        p.recs = x.recs;
+        p.PM = x.PM;
+        p.batch = batch_id;
+        p.q = q_host;
+        return p;
+    }
+
     // pass 1 of the entering argmin for the first pivot of a phase (later pivots get it
-    // from the update kernel)
+    // from k_pivot_row)
     void enqueue_enter_partials() {
         for (auto &x : sh) sx_launch_enter(x.d, N - 1, x.enter_parts, x.st, s);
     }
 
-    void enqueue_pivot(hipEvent_t ev0, hipEvent_t ev1) {
-        const UpdateCfg cfg = update_cfg();
+    // one pivot into slot q_host of the current batch: ratio test + selection, the pivot
+    // row, the objective row and the next entering variable.  The tableau is not touched.
+    void enqueue_pivot() {
         const Cols c = cols(N);
         for (auto &x : sh)
-            sx_launch_ratio_select(x.T, x.rows, x.row0, ld, x.tiles_local, x.colE, x.st, x.base, x.rnew, ld, !xchg,
-                                   rowgather ? x.slot_send : nullptr, slot_stride, c, x.rowlist, x.tile_cnt,
-                                   cfg.skip_zero, s);
+            sx_launch_ratio_select(x.T, x.rows, x.row0, ld, x.tiles_local, x.colE, x.st, x.base, !xchg,
+                                   rowgather ? x.slot_send : nullptr, slot_stride, c, pending(x), s);
         if (rowgather) {
             allgather_slots();
-            for (auto &x : sh)
-                sx_launch_select_gathered(x.slot_all, slot_stride, W * slots, x.base, x.st, x.rank * slots, slots, s);
+            for (auto &x : sh) sx_launch_select_gathered(x.slot_all, slot_stride, W * slots, x.base, x.st, pending(x), s);
         } else if (xchg) {
             allgather_tiles();
             for (auto &x : sh)
                 sx_launch_select_row(x.T, x.rows, x.row0, ld, c, x.tiles_all, W * slots, x.prow_send, x.base, x.st,
-                                     x.rnew, ld, x.rank * slots, slots, s);
+                                     pending(x), s);
             allreduce_prow();
         }
-        if (ev0) SX_HIP(hipEventRecord(ev0, s));
         for (auto &x : sh) {
             const double *pb = rowgather ? x.slot_all : (xchg ? x.prow : nullptr);
-            sx_launch_update(x.T, x.rows, x.row0, ld, c, x.d, pb, rowgather ? slot_stride : 0, x.colE, x.st, x.rnew,
-                             ld, x.enter_parts, x.rowlist, x.tile_cnt, cfg, s);
+            sx_launch_pivot_row(x.T, x.rows, x.row0, ld, c, x.d, pb, rowgather ? slot_stride : 0, x.colE, x.st,
+                                pending(x), x.enter_parts, s);
         }
-        if (ev1) SX_HIP(hipEventRecord(ev1, s));
+        ++q_host;
     }
 
-    // write the last pivot row back into T (it is deferred to the next pivot's update)
-    void flush() {
-        for (auto &x : sh) sx_launch_flush_row(x.T, x.rows, x.row0, ld, cols(N).Ns, x.rnew, ld, x.st, s);
+    // apply the batch's pivots to the tableau (a no-op kernel when none was selected) and
+    // start a new batch
+    void enqueue_sweep(hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
+        if (q_host == 0) return;
+        const SweepCfg cfg = sweep_cfg(q_host);
+        const int rev = (int)(sweeps & 1);  // alternate the sweep direction (Infinity-Cache reuse)
+        if (ev0) SX_HIP(hipEventRecord(ev0, s));
+        for (auto &x : sh) sx_launch_sweep(x.T, x.rows, ld, cols(N).Ns, pending(x), x.st, rev, cfg, s);
+        if (ev1) SX_HIP(hipEventRecord(ev1, s));
+        ++sweeps;
+        ++batch_id;
+        if (batch_id == 0) batch_id = 1;
+        q_host = 0;
     }
 
     void reset_state(long long max_pivots) {
+        enqueue_sweep();  // never leave pivots of an earlier call unapplied
         DevState init;
         std::memset(&init, 0, sizeof(init));
         init.status = SX_NOT_ENDED;
         init.e = -1;
         init.r = -1;
-        init.r_prev = -1;
         init.e_next = -1;
         init.max_pivots = max_pivots;
         for (auto &x : sh) SX_HIP(hipMemcpyAsync(x.st, &init, sizeof(init), hipMemcpyHostToDevice, s));
@@ -551,33 +554,37 @@ class Engine {
         N = width;
         reset_state(max_pivots);
         enqueue_enter_partials();
-        const int batch = g_cfg.batch > 0 ? g_cfg.batch : 16;
+        const int K = batch_size();
         const bool timed = ch && ch->on();
         std::vector<hipEvent_t> it_ev;  // TIMER CSV: one event pair per loop iteration
         if (on_pivot) {  // DEBUG: one pivot at a time, tableau printed after each
             for (;;) {
-                enqueue_pivot(nullptr, nullptr);
+                enqueue_pivot();
+                enqueue_sweep();
                 if (read_state().status != SX_NOT_ENDED) break;
-                flush();  // the pending pivot row back into T for printing (idempotent)
                 on_pivot(width);
             }
         }
+        // batches of K pivots + one sweep; the host polls the status of the batch before the
+        // last one, so the device never waits on the host
         long long k = 0;
         for (; !on_pivot; ++k) {
-            for (int b = 0; b < batch; ++b) {
+            for (int b = 0; b < K; ++b) {
                 if (timed) {
                     hipEvent_t e0, e1;
                     SX_HIP(hipEventCreate(&e0));
                     SX_HIP(hipEventCreate(&e1));
                     SX_HIP(hipEventRecord(e0, s));
-                    enqueue_pivot(nullptr, nullptr);
+                    enqueue_pivot();
+                    if (b == K - 1) enqueue_sweep();  // the batch's sweep counts to its last pivot
                     SX_HIP(hipEventRecord(e1, s));
                     it_ev.push_back(e0);
                     it_ev.push_back(e1);
                 } else {
-                    enqueue_pivot(nullptr, nullptr);
+                    enqueue_pivot();
                 }
             }
+            enqueue_sweep();
             const int slot = (int)(k & 1);
             SX_HIP(hipMemcpyAsync(st_host + slot, sh[0].st, sizeof(DevState), hipMemcpyDeviceToHost, s));
             SX_HIP(hipEventRecord(poll_ev[slot], s));
@@ -586,7 +593,6 @@ class Engine {
                 if (st_host[slot ^ 1].status != SX_NOT_ENDED) break;
             }
         }
-        flush();
         DevState f = read_state();
         if (timed) {
             const size_t iters = std::min(it_ev.size() / 2, (size_t)f.pivots + 1);
@@ -656,9 +662,6 @@ class Engine {
     // artificial columns must equal the slack columns, checked by the callers below)
     void upload(const double *T_host, size_t ld_host, int width, const double *d_host, const int *base_host) {
         const Cols c = cols(width);
-        no_neg_zero = true;
-        for (int i = 0; i < m && no_neg_zero; ++i)
-            if (any_neg_zero(T_host + (size_t)i * ld_host, (size_t)width)) no_neg_zero = false;
         for (auto &x : sh) {
             if (x.rows > 0)
                 SX_HIP(hipMemcpy2DAsync(x.T, ld * sizeof(double), T_host + (size_t)x.row0 * ld_host,
@@ -811,7 +814,7 @@ void simplex_set_verbose(int on) { g_cfg.verbose = on; }
 void simplex_set_update_rows(int rb) { g_cfg.update_rows = (rb == 1 || rb == 2 || rb == 4 || rb == 8) ? rb : 0; }
 void simplex_set_snake(int mode) { g_cfg.snake = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_store_sc1(int mode) { g_cfg.sc1 = mode < 0 ? -1 : (mode ? 1 : 0); }
-void simplex_set_batch(int pivots) { g_cfg.batch = pivots > 0 ? pivots : 16; }
+void simplex_set_batch(int pivots) { g_cfg.batch = pivots > 0 ? std::min(pivots, SX_KMAX) : 16; }
 void simplex_set_device(int device) {
     g_cfg.device = device;
     if (device >= 0) SX_HIP(hipSetDevice(device));
@@ -819,9 +822,7 @@ void simplex_set_device(int device) {
 void simplex_set_virtual_ranks(int world) { g_cfg.virtual_ranks = world > 1 ? world : 1; }
 void simplex_set_force_exchange(int on) { g_cfg.force_exchange = on ? 1 : 0; }
 void simplex_set_alias(int on) { g_cfg.alias = on ? 1 : 0; }
-void simplex_set_skip_zero(int on) { g_cfg.skip_zero = on ? 1 : 0; }
 void simplex_set_update_waves(double waves) { sx_set_update_waves((float)waves); }
-void simplex_set_update_mode(int mode) { g_cfg.update_mode = (mode >= 0 && mode <= 1) ? mode : -1; }
 void simplex_set_exchange_mode(int mode) { g_cfg.exchange_mode = (mode >= 0 && mode <= 2) ? mode : 0; }
 void simplex_set_timer_dir(const char *dir) { g_cfg.timer_dir = dir ? dir : ""; }
 
@@ -965,30 +966,42 @@ static simplex_session *session_finish(simplex_session *S) {
 }
 
 int simplex_session_pivots(simplex_session *S, long long k, int time_updates, simplex_timing_t *out) {
-    // time_updates = s > 0: bracket every s-th update launch with HIP events (events on
-    // every launch cost ~8 us per pivot, so a sample keeps the pivot rate undisturbed)
+    // k pivots in batches of the configured size, each batch ending with a sweep of the
+    // tableau (a call ends with one too, so T is materialised on return).  time_updates =
+    // s > 0: bracket every s-th sweep with HIP events and log how many pivots it applied.
     Engine &E = *S->E;
+    const int K = E.batch_size();
     const long long every = time_updates > 0 ? time_updates : 0;
-    const long long nt = every ? (k + every - 1) / every : 0;
+    const long long max_sweeps = (k + K - 1) / K + 1;
+    const long long nt = every ? (max_sweeps + every - 1) / every : 0;
     std::vector<hipEvent_t> evs(2 * (size_t)nt);
     for (auto &e : evs) SX_HIP(hipEventCreate(&e));
-    // rows each timed update actually touched (DevState.touched, summed over local shards)
-    const size_t nsh = E.sh.size();
-    // (DevState.touched, DevState.touched_pairs) after each timed update
-    int *touched_dev = dalloc<int>((size_t)(nt > 0 ? nt : 1) * nsh * 2);
+    std::vector<unsigned> ids((size_t)(nt > 0 ? nt : 1), 0u);
+    // (batch_tag, batch_count) after each timed sweep: the pivots it applied
+    int *tag_dev = dalloc<int>((size_t)(nt > 0 ? nt : 1) * 2);
     hipEvent_t w0, w1;
     SX_HIP(hipEventCreate(&w0));
     SX_HIP(hipEventCreate(&w1));
     const long long before = E.read_state().pivots;
+    long long nsw = 0, ntimed = 0;
+    auto sweep = [&]() {
+        const bool timed = every && (nsw % every == 0) && ntimed < nt;
+        const unsigned id = E.batch_id;
+        E.enqueue_sweep(timed ? evs[2 * ntimed] : nullptr, timed ? evs[2 * ntimed + 1] : nullptr);
+        if (timed) {
+            ids[(size_t)ntimed] = id;
+            SX_HIP(hipMemcpyAsync(tag_dev + 2 * ntimed, &E.sh[0].st->batch_tag, 2 * sizeof(int),
+                                  hipMemcpyDeviceToDevice, E.s));
+            ++ntimed;
+        }
+        ++nsw;
+    };
     SX_HIP(hipEventRecord(w0, E.s));
     for (long long i = 0; i < k; ++i) {
-        const bool timed = every && (i % every == 0);
-        E.enqueue_pivot(timed ? evs[2 * (i / every)] : nullptr, timed ? evs[2 * (i / every) + 1] : nullptr);
-        if (timed)
-            for (size_t q = 0; q < nsh; ++q)
-                SX_HIP(hipMemcpyAsync(touched_dev + 2 * ((size_t)(i / every) * nsh + q), &E.sh[q].st->touched,
-                                      2 * sizeof(int), hipMemcpyDeviceToDevice, E.s));
+        E.enqueue_pivot();
+        if (E.q_host >= K) sweep();
     }
+    if (E.q_host > 0) sweep();
     SX_HIP(hipEventRecord(w1, E.s));
     SX_HIP(hipEventSynchronize(w1));
     DevState f = E.read_state();
@@ -1004,36 +1017,24 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
     for (auto &x : E.sh) rows += x.rows;
     t.local_rows = rows;
     t.stored_width = E.cols(E.N).Ns;
-    t.update_bytes = 16.0 * (double)rows * (double)t.stored_width + 16.0 * (double)E.N;
-    double sum = 0.0;
-    std::vector<float> per((size_t)(nt > 0 ? nt : 1), 0.f);
-    for (long long i = 0; i < nt; ++i) {
-        SX_HIP(hipEventElapsedTime(&per[(size_t)i], evs[2 * i], evs[2 * i + 1]));
-        sum += per[(size_t)i];
-    }
-    t.update_ms = sum;
-    t.update_launches = nt;
-    std::vector<int> touched((size_t)(nt > 0 ? nt : 1) * nsh * 2, 0);
-    SX_HIP(hipMemcpy(touched.data(), touched_dev, sizeof(int) * touched.size(), hipMemcpyDeviceToHost));
-    (void)hipFree(touched_dev);
-    const UpdateCfg ucfg = E.update_cfg();
-    const bool skipping = ucfg.skip_zero != 0;
-    const long long all_pairs = (t.stored_width + 1) / 2;
-    S->log_rows.assign((size_t)nt, 0);
-    S->log_us.assign((size_t)nt, 0.0);
-    for (long long i = 0; i < nt; ++i) {
-        for (size_t q = 0; q < nsh; ++q) {
-            const int *tq = touched.data() + 2 * ((size_t)i * nsh + q);
-            // rows the update swept (read + written), the deferred pivot row included, over the
-            // column pairs it swept (the list sweep leaves the pivot row's zero pairs alone)
-            const long long rows_i = skipping ? (long long)tq[0] : E.sh[q].rows;
-            const long long pairs_i = (skipping && !ucfg.one_shot) ? (long long)tq[1] : all_pairs;
-            t.touched_rows += rows_i;
-            t.touched_bytes += 32.0 * (double)rows_i * (double)pairs_i;
-            S->log_rows[(size_t)i] += rows_i;
-            S->log_us[(size_t)i] = 1e3 * (double)per[(size_t)i];
-        }
-        t.touched_bytes += 16.0 * (double)E.N * (double)nsh;
+    t.update_bytes = 16.0 * (double)rows * (double)t.stored_width;
+    std::vector<int> tags((size_t)(nt > 0 ? nt : 1) * 2, 0);
+    SX_HIP(hipMemcpy(tags.data(), tag_dev, sizeof(int) * tags.size(), hipMemcpyDeviceToHost));
+    (void)hipFree(tag_dev);
+    S->log_rows.clear();
+    S->log_us.clear();
+    for (long long i = 0; i < ntimed; ++i) {
+        // a sweep whose batch selected no pivot (the phase had ended) is a no-op launch
+        const int applied = (unsigned)tags[2 * i] == ids[(size_t)i] ? tags[2 * i + 1] : 0;
+        if (applied <= 0) continue;
+        float us = 0.f;
+        SX_HIP(hipEventElapsedTime(&us, evs[2 * i], evs[2 * i + 1]));
+        t.update_ms += us;
+        t.update_launches += 1;
+        t.swept_pivots += applied;
+        t.swept_bytes += t.update_bytes;
+        S->log_rows.push_back(applied);
+        S->log_us.push_back(1e3 * (double)us);
     }
     for (auto &e : evs) (void)hipEventDestroy(e);
     (void)hipEventDestroy(w0);

@@ -149,30 +149,60 @@ __global__ __launch_bounds__(512) void k_enter_finish(const TilePart *parts, int
     }
 }
 
-// The leaving row of the previous pivot is not yet written back to T: its current values
-// are rnew[pivots & 1].  Source row i of a shard for the pivot being selected:
-__device__ __forceinline__ const double *row_src(const double *T, size_t ld, int li, int pend,
-                                                 const double *rnew_cur) {
-    return li == pend ? rnew_cur : T + (size_t)li * ld;
+// ---------------------------------------------------------------------------------------
+// Deferred pivots.  T holds the tableau as of the last sweep; the q pivots
+// of the current batch since then are kept as
+//   U[s][j]   pivot row of slot s: the leaving row's values at that pivot (before /p),
+//   F[i][s]   factor of local row i at slot s: -(a_ie / p)  (solver.cu:41),
+//   recs[s]   (leaving row r, entering variable e, pivot p),
+//   PM[i]     the slots where local row i was the leaving row, tagged with the batch id
+//             (entries of older batches read as empty).
+// The current value of an element is T[i][j] with the q pivots applied in order -- exactly
+// the IEEE operations the reference applies one pivot at a time (solver.cu:34-46):
+//   row r_s:  x = x / p_s             other rows:  x = fma(F[i][s], U[s][j], x)
+// so every decision (entering argmin, ratio test) sees the reference's bits.  One sweep per
+// batch applies all q pivots to every element: one read and one write of T per q pivots.
+
+__device__ __forceinline__ unsigned slot_mask(int q) { return q >= 32 ? ~0u : ((1u << q) - 1u); }
+
+__device__ __forceinline__ unsigned pend_bits(const unsigned long long *__restrict__ PM, int li, unsigned B,
+                                              unsigned mask) {
+    const unsigned long long w = PM[li];
+    return ((unsigned)(w >> 32) == B) ? ((unsigned)w & mask) : 0u;
+}
+
+// value of stored column `col` of a local row after the q pending pivots
+__device__ __forceinline__ double cur_value(double x, int q, unsigned bits, const double *__restrict__ Frow,
+                                            const double *__restrict__ U, size_t ld, int col,
+                                            const PivRec *__restrict__ recs) {
+    for (int s = 0; s < q; ++s) {
+        if ((bits >> s) & 1u)
+            x = x / recs[s].p;
+        else
+            x = fma(Frow[s], U[(size_t)s * ld + col], x);
+    }
+    return x;
 }
 
 // ---------------------------------------------------------------------------------------
 // K2: ratio test (+ row selection on a single shard).  The entering variable and its
-// reduced cost were produced by the previous update (or k_enter_finish).  Every block:
+// reduced cost were produced by the previous pivot's k_pivot_row (or k_enter_finish).
+// Every block:
 //  - ends the phase if compare(dmin) >= 0 (solver.cu:88),
-//  - builds the ratio vector of its 512 rows (createIndicatorsVector, reduction.cu:106-114),
-//    saves the pre-update entering column (the reference's rowPivot copy, solver.cu:90-94)
-//    and reduces it to the tile winner + "any entry >= eps" (isLessOrEqualThanZero,
-//    reduction.cu:186-201).
+//  - builds the ratio vector of its 512 rows (createIndicatorsVector, reduction.cu:106-114)
+//    from the current entering column and RHS, saves the entering column (the reference's
+//    rowPivot copy, solver.cu:90-94) and reduces it to the tile winner + "any entry >= eps"
+//    (isLessOrEqualThanZero, reduction.cu:186-201).
 // With select != 0 the last block to arrive runs the pass-2 tree over the tile winners
 // (minElement(knownTerms, rowPivot), solver.cu:104), declares UNBOUNDED (:96-102) or records
 // the pivot: base[r] = e (:105).  With several shards the tile winners are allgathered
-// first and k_select_row does that step.
+// first and k_select_row / k_select_gathered do that step.
 __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__ T, int rows, int row0, size_t ld,
                                                       TilePart *tiles_local, double *colE, DevState *st, int *base,
-                                                      const double *__restrict__ rnew, size_t rnew_stride,
                                                       int select, double *slots, size_t slot_stride, Cols c,
-                                                      int *rowlist, int *tile_cnt, int skip_zero) {
+                                                      const double *__restrict__ F, const double *__restrict__ U,
+                                                      const PivRec *__restrict__ recs,
+                                                      const unsigned long long *__restrict__ PM, unsigned B, int q) {
     if (st->status != SX_NOT_ENDED) return;
     const bool leader = blockIdx.x == 0 && threadIdx.x == 0;
     const long long piv = st->pivots;
@@ -190,47 +220,41 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
         st->e = e;
         st->dmin = v;
     }
-    const int pend = piv > 0 ? st->r - row0 : -1;
-    const double *rcur = rnew + (size_t)(piv & 1) * rnew_stride;
+    const int ce = c.map(1 + e);
+    const unsigned mask = slot_mask(q);
     __shared__ double s_v[16];
     __shared__ int s_i[16];
     const int li = blockIdx.x * SX_TILE + threadIdx.x;
     double rv = DBL_MAX;
     int ri = -1;
     int elig = 0;
-    bool listed = false, wide = false;
     if (li < rows) {
-        const double *row = row_src(T, ld, li, pend, rcur);
-        const double a = row[c.map(1 + e)];
-        const double b = row[0];
+        const double *row = T + (size_t)li * ld;
+        double b = row[0], a = row[ce];
+        if (q > 0) {
+            const unsigned bits = pend_bits(PM, li, B, mask);
+            const double *Fr = F + (size_t)li * SX_KMAX;
+            for (int s = 0; s < q; ++s) {
+                if ((bits >> s) & 1u) {
+                    const double p = recs[s].p;
+                    b = b / p;
+                    a = a / p;
+                } else {
+                    const double f = Fr[s];
+                    b = fma(f, U[(size_t)s * ld], b);
+                    a = fma(f, U[(size_t)s * ld + ce], a);
+                }
+            }
+        }
         colE[li] = a;
         elig = a >= SX_EPS;
-        // rows the update must sweep: a nonzero factor, or the pending row (its values live in
-        // rnew until the update writes them back); every row when skipping is off
-        listed = !skip_zero || a != 0.0 || li == pend;
-        wide = listed && !(fabs(a) <= 1e299);  // |a / p| could overflow (p >= 1e-9), or a is not finite
         const double ratio = cmp_eps(a, 0.0) > 0 ? b / a : DBL_MAX;
         if (cmp_eps(ratio, rv) < 0) {
             rv = ratio;
             ri = row0 + li;
         }
     }
-    // compact this tile's listed rows, in row order, to rowlist[tile*512 ...]
-    __shared__ int s_wc[SX_TILE / 64];
-    const unsigned long long bal = __ballot(listed);
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (lane == 0) s_wc[wv] = __popcll(bal);
-    int any = __syncthreads_or(elig);
-    const int any_wide = __syncthreads_or(wide);
-    int pos = 0, cnt = 0;
-    for (int w = 0; w < SX_TILE / 64; ++w) {
-        pos += w < wv ? s_wc[w] : 0;
-        cnt += s_wc[w];
-    }
-    if (listed) rowlist[blockIdx.x * SX_TILE + pos + __popcll(bal & ((1ull << lane) - 1))] = li;
-    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = cnt | (any_wide ? SX_TILE_WIDE : 0);
-    if (leader) st->touched_pairs = 0;  // counted by the update
-    any |= cnt << 1;  // packed: SX_ELIG / SX_NNZ
+    const int any = __syncthreads_or(elig);
     block_argmin512(rv, ri, s_v, s_i);
     if (!select) {
         if (slots == nullptr) {
@@ -255,8 +279,10 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
         __syncthreads();
         const int wl = s_ri - row0;
         if (s_ri >= 0) {
-            const double *src = row_src(T, ld, wl, pend, rcur);
-            for (int j = threadIdx.x; j < c.Ns; j += SX_TILE) slot[2 + j] = src[j];
+            const double *src = T + (size_t)wl * ld;
+            const unsigned bits = pend_bits(PM, wl, B, mask);
+            const double *Fr = F + (size_t)wl * SX_KMAX;
+            for (int j = threadIdx.x; j < c.Ns; j += SX_TILE) slot[2 + j] = cur_value(src[j], q, bits, Fr, U, ld, j, recs);
         }
         return;
     }
@@ -272,9 +298,6 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
     const int B2 = gridDim.x;
     double tv = DBL_MAX;
     int ti = -1, te = 0;
-    __shared__ int s_nnz;
-    if (threadIdx.x == 0) s_nnz = 0;
-    __syncthreads();
     if ((int)threadIdx.x < B2) {
         double cv;
         int ci;
@@ -283,7 +306,6 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
             tv = cv;
             ti = ci;
         }
-        atomicAdd(&s_nnz, SX_NNZ(te));
     }
     const int anyall = __syncthreads_or(SX_ELIG(te));
     if (!anyall) {
@@ -300,25 +322,26 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
             st->status = SX_NUMERIC_FAIL;
         } else {
             base[ti] = e;
-            st->r_prev = st->r;
             st->r = ti;
             st->pivots = piv + 1;
-            st->touched = s_nnz;
+            st->batch_tag = B;
+            st->batch_count = q + 1;
         }
     }
 }
 
 // ---------------------------------------------------------------------------------------
 // K3 (several shards): every block re-derives the leaving row from the allgathered tile
-// winners, checks the unbounded condition, records the pivot, and copies its chunk of the
-// pre-update pivot row (the reference's copyColumn, solver.cu:24-32, is a contiguous row
+// winners, checks the unbounded condition, records the pivot, and writes its chunk of the
+// current pivot row (the reference's copyColumn, solver.cu:24-32, is a contiguous row
 // here).  Only the owner contributes the row; the others contribute -0.0, the exact
 // additive identity, so the sum-allreduce reproduces the owner's row bit for bit.
 __global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T, int rows, int row0, size_t ld,
                                                     int Ns, const TilePart *__restrict__ tiles_all, int B2,
                                                     double *prow_out, int *base, DevState *st,
-                                                    const double *__restrict__ rnew, size_t rnew_stride, int tile0,
-                                                    int nslots) {
+                                                    const double *__restrict__ F, const double *__restrict__ U,
+                                                    const PivRec *__restrict__ recs,
+                                                    const unsigned long long *__restrict__ PM, unsigned B, int q) {
     if (st->status != SX_NOT_ENDED) return;
     const bool leader = blockIdx.x == 0 && threadIdx.x == 0;
     __shared__ double s_v[16];
@@ -329,10 +352,6 @@ __global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T
         if (leader) st->status = SX_UNBOUNDED;  // solver.cu:96-102
         return;
     }
-    __shared__ int s_nnz;
-    if (threadIdx.x == 0) s_nnz = 0;
-    __syncthreads();
-    if ((int)threadIdx.x >= tile0 && (int)threadIdx.x < tile0 + nslots) atomicAdd(&s_nnz, SX_NNZ(pk));
     double v;
     int r;
     stage2_512(tiles_all, B2, v, r, s_v, s_i);
@@ -344,11 +363,17 @@ __global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T
         return;
     }
     const long long piv = st->pivots;
-    const int pend = piv > 0 ? st->r - row0 : -1;
-    const bool own = r >= row0 && r < row0 + rows;
-    const double *src = own ? row_src(T, ld, r - row0, pend, rnew + (size_t)(piv & 1) * rnew_stride) : T;
-    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < Ns; j += gridDim.x * blockDim.x)
-        prow_out[j] = own ? src[j] : -0.0;
+    const int rl = r - row0;
+    const bool own = rl >= 0 && rl < rows;
+    if (own) {
+        const double *src = T + (size_t)rl * ld;
+        const unsigned bits = pend_bits(PM, rl, B, slot_mask(q));
+        const double *Fr = F + (size_t)rl * SX_KMAX;
+        for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < Ns; j += gridDim.x * blockDim.x)
+            prow_out[j] = cur_value(src[j], q, bits, Fr, U, ld, j, recs);
+    } else {
+        for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < Ns; j += gridDim.x * blockDim.x) prow_out[j] = -0.0;
+    }
     // commit the pivot once every block has read the state above: the last block to
     // arrive does it (the next kernel sees it after the launch boundary)
     __syncthreads();
@@ -357,27 +382,24 @@ __global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T
         if (t == gridDim.x - 1) {
             st->ticket = 0;
             base[r] = st->e;  // solver.cu:105
-            st->r_prev = st->r;
             st->r = r;
             st->pivots = piv + 1;
-            st->touched = s_nnz;
+            st->batch_tag = B;
+            st->batch_count = q + 1;
         }
     }
 }
 
 // K3 (row-gather exchange): one block picks the leaving row among the gathered tile
 // winners (the reference's pass-2 tree), checks the unbounded condition and records the
-// pivot; the update then reads the pivot row from the winning slot.
+// pivot; k_pivot_row then reads the pivot row from the winning slot.
 __global__ __launch_bounds__(512) void k_select_gathered(const double *__restrict__ slots, size_t slot_stride, int B2,
-                                                         int *base, DevState *st, int tile0, int nslots) {
+                                                         int *base, DevState *st, unsigned B, int q) {
     if (st->status != SX_NOT_ENDED) return;
     __shared__ double s_v[16];
     __shared__ int s_i[16];
     double v = DBL_MAX;
     int r = -1, pk = 0;
-    __shared__ int s_nnz;
-    if (threadIdx.x == 0) s_nnz = 0;
-    __syncthreads();
     if ((int)threadIdx.x < B2) {
         const TilePart *h = reinterpret_cast<const TilePart *>(slots + (size_t)threadIdx.x * slot_stride);
         pk = h->elig;
@@ -386,7 +408,6 @@ __global__ __launch_bounds__(512) void k_select_gathered(const double *__restric
             v = c;
             r = h->idx;
         }
-        if ((int)threadIdx.x >= tile0 && (int)threadIdx.x < tile0 + nslots) atomicAdd(&s_nnz, SX_NNZ(pk));
     }
     if (!__syncthreads_or(SX_ELIG(pk))) {
         if (threadIdx.x == 0) st->status = SX_UNBOUNDED;  // solver.cu:96-102
@@ -398,71 +419,89 @@ __global__ __launch_bounds__(512) void k_select_gathered(const double *__restric
             st->status = SX_NUMERIC_FAIL;
         } else {
             base[r] = st->e;  // solver.cu:105
-            st->r_prev = st->r;
             st->r = r;
             st->pivots += 1;
-            st->touched = s_nnz;
+            st->batch_tag = B;
+            st->batch_count = q + 1;
         }
     }
 }
 
 // ---------------------------------------------------------------------------------------
-// K4: the rank-1 pivot update (updateContraintsMatrix + updateCostsVector, solver.cu:34-56)
-//   row r:       rnew[q&1][j] = prow[j] / p     (q = pivot number; written back to T by the
-//                                                next update, which reads it as row r_prev)
-//   other rows:  T[i][j] = fma(-(a_ie / p), prow[j], T[i][j])   (factor hoisted per row:
-//                the reference recomputes the same division per element, bit-identical)
-//   objective:   d[j]    = fma(-(d_e / p),  prow[j], d[j])
-// prow is the pre-update pivot row, read in place on one shard (nothing writes row r
-// during the launch) or the allreduced copy on several.  Grid row 0 (dispatched first)
-// updates d and finishes the NEXT pivot's entering argmin: pass 1 per 512-tile
-// (reduction.cu:51-80), then the last block to arrive runs pass 2 and stores
-// (e_next, dmin_next).  Grid rows >= 1: a thread owns 2 adjacent columns (one 16-byte
-// load/store per row), a block covers 512 columns x RB rows.  With SNAKE the tile order
-// is reversed on every other pivot, so a sweep starts on the lines the previous one wrote
-// last -- still resident in the 256 MB Infinity Cache.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-// 16-byte store of a tableau element pair: plain, or write-through (sc1) via a buffer
-// resource so the line leaves the XCD L2 at once (no dirty-L2 write-back at the end of the
-// launch, less L2 pollution on a once-touched stream)
-template <bool SC1>
-__device__ __forceinline__ void store_pair(double *p, double2 v, __amdgpu_buffer_rsrc_t rs, int byte_off) {
-    if (SC1)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, byte_off, 0, 16);
-    else
-        *reinterpret_cast<double2 *>(p) = v;
-}
-
-// Objective row of the update (grid row 0 of either update kernel, dispatched first): d[j] =
-// fma(-(d_e / p), prow[j], d[j]) and pass 1 of the NEXT entering argmin per 512-tile
-// (reduction.cu:51-80); the last block to arrive runs pass 2 and stores (e_next, dmin_next).
-// 512 reference threads on 256.
-__device__ void objective_row(const double *__restrict__ prow, double p, double *__restrict__ d, DevState *st,
-                              TilePart *enter_parts, Cols c) {
+// K4: the pivot row of slot q and everything that depends only on it.
+//   U[q][j]  = current row r (the reference's colPivot, solver.cu:24-32)  -- read in place
+//              with the pending pivots applied on one shard, or taken from the exchanged
+//              row (prow_buf) on several;
+//   p        = U[q][e]  (= the entering column's entry at r; solver.cu:66);
+//   d[j]     = fma(-(d_e / p), U[q][j], d[j])  (updateCostsVector, solver.cu:48-56), and pass
+//              1 of the NEXT entering argmin per 512-tile (reduction.cu:51-80); the last block
+//              to arrive runs pass 2 and stores (e_next, dmin_next);
+//   F[i][q]  = -(a_ie / p) for the shard's rows (the factor of solver.cu:41);
+//   recs[q], PM[r] |= slot q.
+// Blocks [0, B1) are the objective-row tiles (512 logical columns each, 2 per thread);
+// the rest compute the factor column.  Writes to recs[q] / PM[r] race with nothing: readers
+// in this launch only look at slots < q.
+__global__ __launch_bounds__(256) void k_pivot_row(const double *__restrict__ T, int rows, int row0, size_t ld, Cols c,
+                                                   double *__restrict__ d, const double *__restrict__ prow_buf,
+                                                   size_t prow_stride, const double *__restrict__ colE, DevState *st,
+                                                   double *U, double *F, PivRec *recs, unsigned long long *PM,
+                                                   TilePart *enter_parts, unsigned B, int q, int B1) {
+    if (st->status != SX_NOT_ENDED) return;
+    const int r = st->r, e = st->e;
+    const int rl = r - row0;
+    const double *prow =
+        prow_buf ? (prow_stride ? prow_buf + (size_t)(r / SX_TILE) * prow_stride + 2 : prow_buf) : nullptr;
+    const double *trow = T + (size_t)(prow ? 0 : rl) * ld;
+    const unsigned bits = prow ? 0u : pend_bits(PM, rl, B, slot_mask(q));
+    const double *Fr = F + (size_t)(prow ? 0 : rl) * SX_KMAX;
+    auto cur = [&](int col) -> double {
+        return prow ? prow[col] : cur_value(trow[col], q, bits, Fr, U, ld, col, recs);
+    };
+    const double p = cur(c.map(1 + e));
+    if ((int)blockIdx.x >= B1) {
+        const int i = ((int)blockIdx.x - B1) * 256 + (int)threadIdx.x;
+        if (i < rows) F[(size_t)i * SX_KMAX + q] = -colE[i] / p;
+        if (i == rl) {
+            const unsigned long long w = PM[rl];
+            PM[rl] = (((unsigned)(w >> 32) == B) ? w : ((unsigned long long)B << 32)) | (1ull << q);
+        }
+        return;
+    }
+    double *Uq = U + (size_t)q * ld;
+    const double fd = -st->dmin / p;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const double u0 = cur(0);
+        Uq[0] = u0;
+        d[0] = fma(fd, u0, d[0]);
+        recs[q].r = r;
+        recs[q].e = e;
+        recs[q].p = p;
+    }
     // ---- objective row + next entering argmin (512 reference threads on 256)
     __shared__ double s_v[16];
     __shared__ int s_i[16];
     __shared__ int s_last;
     const int L = c.N - 1;
-    const int B1 = (L + SX_TILE - 1) / SX_TILE;
-    if ((int)blockIdx.x >= B1) return;
-    const double fd = -st->dmin / p;
-    if (blockIdx.x == 0 && threadIdx.x == 0) d[0] = fma(fd, prow[0], d[0]);
     double v0 = DBL_MAX, v1 = DBL_MAX;
     int i0 = -1, i1 = -1;
     const int ia = blockIdx.x * SX_TILE + threadIdx.x, ib = ia + 256;
     if (ia < L) {
-        const double x = fma(fd, prow[c.map(1 + ia)], d[1 + ia]);
-        d[1 + ia] = x;
+        const int j = 1 + ia;
+        const double u = cur(c.map(j));
+        if (j < c.Ns) Uq[j] = u;
+        const double x = fma(fd, u, d[j]);
+        d[j] = x;
         if (cmp_eps(x, v0) < 0) {
             v0 = x;
             i0 = ia;
         }
     }
     if (ib < L) {
-        const double x = fma(fd, prow[c.map(1 + ib)], d[1 + ib]);
-        d[1 + ib] = x;
+        const int j = 1 + ib;
+        const double u = cur(c.map(j));
+        if (j < c.Ns) Uq[j] = u;
+        const double x = fma(fd, u, d[j]);
+        d[j] = x;
         if (cmp_eps(x, v1) < 0) {
             v1 = x;
             i1 = ib;
@@ -521,242 +560,90 @@ __device__ void objective_row(const double *__restrict__ prow, double p, double 
             st->ticket_d = 0;
         }
     }
-    return;
 }
 
-// Exclusive prefix of the per-tile list lengths (n <= 512 tiles, 256 threads): s_pre[t] =
-// first list position of tile t, s_pre[n] = total; wide = some tile flagged SX_TILE_WIDE.
-// All threads of the block must call it.
-__device__ int scan_tile_counts(const int *__restrict__ cnt, int n, int *s_pre, bool &wide) {
-    __shared__ int s_w[4];
-    const int t = threadIdx.x, lane = t & 63;
-    const int ra = 2 * t < n ? cnt[2 * t] : 0;
-    const int rb = 2 * t + 1 < n ? cnt[2 * t + 1] : 0;
-    wide = __syncthreads_or((ra | rb) & SX_TILE_WIDE) != 0;
-    const int a = SX_TILE_COUNT(ra), b = SX_TILE_COUNT(rb);
-    int v = a + b;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(v, o, 64);
-        if (lane >= o) v += y;
-    }
-    if (lane == 63) s_w[t >> 6] = v;
-    __syncthreads();
-    int off = 0;
-    for (int w = 0; w < (t >> 6); ++w) off += s_w[w];
-    const int excl = v + off - a - b;
-    if (2 * t < n) s_pre[2 * t] = excl;
-    if (2 * t + 1 < n) s_pre[2 * t + 1] = excl + a;
-    if (t == 0) s_pre[n] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-    __syncthreads();
-    return s_pre[n];
-}
+// ---------------------------------------------------------------------------------------
+// K5: the sweep -- the batch's pivots applied to every stored element of the shard
+// (updateContraintsMatrix, solver.cu:34-46, for q pivots at once), in pivot order:
+//   x = T[i][j];  for s < q:  x = (i == r_s) ? x / p_s : fma(F[i][s], U[s][j], x);  T[i][j] = x
+// A thread owns two adjacent columns (one 16-byte load and store per row) and keeps their
+// KT pivot-row values in registers for the whole sweep; the row's factors F[i][0..q) and its
+// pivot-slot bits are wave-uniform (scalar loads).  A fixed set of G blocks per 512-column
+// tile walks the row groups (RB rows per step).  On odd sweeps the tile and row order are
+// reversed, so a sweep starts on the lines the previous one wrote last (still in the 256 MB
+// Infinity Cache).  The sweep runs whatever the phase status: a batch cut short by the end
+// of the phase is still materialised.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-// row of list position k (0 <= k < total): tile t holds positions [s_pre[t], s_pre[t+1]) at
-// rowlist[t*512 ...]; the cursor t moves from the previous lookup, either direction
-__device__ __forceinline__ int list_row(int k, int &t, const int *s_pre, const int *__restrict__ rowlist) {
-    while (s_pre[t + 1] <= k) ++t;
-    while (s_pre[t] > k) --t;
-    return rowlist[t * SX_TILE + (k - s_pre[t])];
-}
-
-template <int RB, bool SNAKE, bool SC1>
-__global__ __launch_bounds__(256) void k_update(double *__restrict__ T, int rows, int row0, size_t ld, Cols c,
-                                                double *__restrict__ d, const double *__restrict__ prow_buf,
-                                                size_t prow_stride, const double *__restrict__ colE, DevState *st,
-                                                double *__restrict__ rnew, size_t rnew_stride,
-                                                TilePart *enter_parts, const int *__restrict__ rowlist,
-                                                const int *__restrict__ tile_cnt, int ntiles, int skip_zero) {
-    if (st->status != SX_NOT_ENDED) return;
-    const long long q = st->pivots;
-    const int e = st->e;
-    const int rl = st->r - row0;
-    const int pl = (q >= 2 && st->r_prev != st->r) ? st->r_prev - row0 : -1;  // pending row, local
-    const double *rprev = rnew + (size_t)((q - 1) & 1) * rnew_stride;
-    double *rout = rnew + (size_t)(q & 1) * rnew_stride;
-    const double *prow = prow_buf ? (prow_stride ? prow_buf + (size_t)(st->r / SX_TILE) * prow_stride + 2 : prow_buf)
-                                  : ((q >= 2 && st->r_prev == st->r) ? rprev : T + (size_t)rl * ld);
-    const double p = prow[c.map(1 + e)];
-    if (blockIdx.y == 0) {
-        objective_row(prow, p, d, st, enter_parts, c);
-        return;
-    }
-    // ---- tableau rows: a fixed set of G blocks per 512-column tile sweeps the rows; each
-    // thread holds its two pivot-row values for the whole sweep
-    const int G = gridDim.y - 1;
-    const int N = c.Ns;  // stored columns
-    const int cb = (N + 511) / 512;
+template <int KT, int RB, bool SC1>
+__global__ __launch_bounds__(256) void k_sweep(double *__restrict__ T, int rows, size_t ld, int Ns,
+                                               const double *__restrict__ F, const double *__restrict__ U,
+                                               const PivRec *__restrict__ recs,
+                                               const unsigned long long *__restrict__ PM,
+                                               const DevState *__restrict__ st, unsigned B, int rev) {
+    const int cnt = st->batch_tag == B ? st->batch_count : 0;
+    if (cnt <= 0) return;
+    const int cb = (Ns + 511) / 512;
     if ((int)blockIdx.x >= cb) return;
-    const bool rev = SNAKE && (q & 1);
     const int bx = rev ? cb - 1 - (int)blockIdx.x : (int)blockIdx.x;
-    const int by = blockIdx.y - 1;
-    const int j = (bx * 256 + threadIdx.x) * 2;
-    const bool active = j < N, pair = j + 1 < N;
-    double2 pr = make_double2(0.0, 0.0);
-    if (active) {
-        if (pair)
-            pr = *reinterpret_cast<const double2 *>(prow + j);
-        else
-            pr.x = prow[j];
-    }
-    // Rows left out of the sweep (factor exactly +-0) keep their bits only when every
-    // fma(+-0, p, x) == x: p finite (checked here, per column tile) and x != -0.0 (the engine
-    // passes skip_zero only for tableaux without -0.0).  Otherwise the tile sweeps all rows.
-    __shared__ int s_pre[SX_TILE + 1];
-    const bool listed = skip_zero && __syncthreads_and(isfinite(pr.x) && isfinite(pr.y));
-    bool wide = true;
-    const int total = listed ? scan_tile_counts(tile_cnt, ntiles, s_pre, wide) : rows;
-    // Columns whose pivot-row pair is (+-0, +-0) are left as they are, in every row but the
-    // pending one (its values come from rprev): fma(f, +-0, x) == x for finite f and x != -0.0.
-    // Those lanes' loads and stores carry an out-of-range buffer offset, which the hardware
-    // drops -- no memory access, and no branch in the loop.
-    const bool zc = active && listed && !wide && pr.x == 0.0 && pr.y == 0.0;
-    {
-        const int nzp = __syncthreads_count(active && !zc);
-        if (by == 0 && threadIdx.x == 0) atomicAdd(&st->touched_pairs, nzp);
-    }
-    if (!active) return;
-    const int ng = (total + RB - 1) / RB;
-    if (by >= ng) return;
-    int tc = rev ? ntiles - 1 : 0;  // tile cursor of the list lookups
-    const double2 rp = make_double2(pr.x / p, pr.y / p);  // the new pivot row
-    // The loop body is straight-line memory code (no loads or stores under branches), so
-    // the compiler's wait counters can keep the next group's loads in flight across the
-    // current group's stores.  Past the end of the list a group repeats its first row (same
-    // thread, same value), and a fetch past the last group reads rprev.  The thread of an odd
-    // last column moves the pair (j, j+1): j+1 < ld is row padding (or, in phase 2 without
-    // aliasing, a dead artificial column).
-    const int off_j = j * 8;
-    const int oob = (int)(ld * 8);  // past the descriptor's range: the access is dropped
-    auto fetch = [&](int g, int *row, double2 *x, double *f) {
-        const bool live = g < ng;
-        const int gg = rev ? ng - 1 - g : g;
+    const int j = (bx * 256 + (int)threadIdx.x) * 2;
+    if (j >= Ns) return;  // the thread of an odd last column moves (j, j+1): j+1 < ld is padding
+    const unsigned mask = slot_mask(cnt);
+    double2 u[KT];
+#pragma unroll
+    for (int s = 0; s < KT; ++s)
+        u[s] = s < cnt ? *reinterpret_cast<const double2 *>(U + (size_t)s * ld + j) : make_double2(0.0, 0.0);
+    const int G = gridDim.y;
+    const int ng = (rows + RB - 1) / RB;
+    const int oob = (int)(ld * 8);
+    for (int g = blockIdx.y; g < ng; g += G) {
+        const int i0 = (rev ? ng - 1 - g : g) * RB;
+        double2 x[RB];
 #pragma unroll
         for (int k = 0; k < RB; ++k) {
-            const int idx = gg * RB + k;
-            int r = (live && idx < total) ? (listed ? list_row(idx, tc, s_pre, rowlist) : idx) : -1;
-            r = __builtin_amdgcn_readfirstlane(r);
-            row[k] = (k > 0 && r < 0) ? row[0] : r;
+            const int i = i0 + k < rows ? i0 + k : i0;
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(T + (size_t)i * ld, 0, oob, 0x00020000);
+            x[k] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, i0 + k < rows ? j * 8 : oob,
+                                                                                      0, 0));
         }
 #pragma unroll
         for (int k = 0; k < RB; ++k) {
-            const bool from_prev = row[k] == pl;
-            const double *src = (row[k] < 0 || from_prev) ? rprev : T + (size_t)row[k] * ld;
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(src), 0, oob,
-                                                                               0x00020000);
-            const bool skip = row[k] < 0 || row[k] == rl || (zc && !from_prev);
-            x[k] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, skip ? oob : off_j, 0, 0));
-            f[k] = row[k] >= 0 ? -colE[row[k]] / p : 0.0;
+            const int i = i0 + k;
+            if (i >= rows) break;
+            const double *Fr = F + (size_t)i * SX_KMAX;
+            const unsigned bits = pend_bits(PM, i, B, mask);
+            double2 y = x[k];
+            if (bits == 0u) {
+#pragma unroll
+                for (int s = 0; s < KT; ++s) {
+                    if (s < cnt) {
+                        const double f = Fr[s];
+                        y.x = fma(f, u[s].x, y.x);
+                        y.y = fma(f, u[s].y, y.y);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int s = 0; s < KT; ++s) {
+                    if (s < cnt) {
+                        if ((bits >> s) & 1u) {
+                            const double p = recs[s].p;
+                            y.x = y.x / p;
+                            y.y = y.y / p;
+                        } else {
+                            const double f = Fr[s];
+                            y.x = fma(f, u[s].x, y.x);
+                            y.y = fma(f, u[s].y, y.y);
+                        }
+                    }
+                }
+            }
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(T + (size_t)i * ld, 0, oob, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, j * 8, 0, SC1 ? 16 : 0);
         }
-    };
-    auto update = [&](const int *row, const double2 *x, const double *f) {
-#pragma unroll
-        for (int k = 0; k < RB; ++k) {
-            const bool is_r = row[k] == rl;
-            double *dst = is_r ? rout : T + (size_t)row[k] * ld;
-            double2 y;
-            y.x = is_r ? rp.x : fma(f[k], pr.x, x[k].x);
-            y.y = is_r ? rp.y : fma(f[k], pr.y, x[k].y);
-            // a lane of a zero column keeps x only if f is finite (checked per row: uniform)
-            const bool skip = zc && !is_r && row[k] != pl && isfinite(f[k]);
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, oob, 0x00020000);
-            if (SC1)
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, skip ? oob : off_j, 0, 16);
-            else
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, skip ? oob : off_j, 0, 0);
-        }
-    };
-    // software pipeline, ping-pong between two register sets: the loads of group g+G are in
-    // flight while group g is updated
-    int ra[RB], rb_[RB];
-    double2 xa[RB], xb[RB];
-    double fa[RB], fb[RB];
-    fetch(by, ra, xa, fa);
-    for (int g = by; g < ng; g += 2 * G) {
-        fetch(g + G, rb_, xb, fb);
-        update(ra, xa, fa);
-        if (g + G >= ng) break;
-        fetch(g + 2 * G, ra, xa, fa);
-        update(rb_, xb, fb);
     }
-}
-
-// One-shot variant of the update: one block per (512 columns, RB rows), the whole tableau in
-// one grid -- the hardware's in-order dispatch keeps the active window of rows tight, which
-// streams best when every row is swept.  Zero-factor rows are skipped per thread (same
-// exactness conditions as the list sweep) but their blocks still run.
-template <int RB, bool SNAKE, bool SC1>
-__global__ __launch_bounds__(256) void k_update_grid(double *__restrict__ T, int rows, int row0, size_t ld, Cols c,
-                                                     double *__restrict__ d, const double *__restrict__ prow_buf,
-                                                     size_t prow_stride, const double *__restrict__ colE,
-                                                     DevState *st, double *__restrict__ rnew, size_t rnew_stride,
-                                                     TilePart *enter_parts, int skip_zero) {
-    if (st->status != SX_NOT_ENDED) return;
-    const long long q = st->pivots;
-    const int rl = st->r - row0;
-    const int pl = (q >= 2 && st->r_prev != st->r) ? st->r_prev - row0 : -1;
-    const double *rprev = rnew + (size_t)((q - 1) & 1) * rnew_stride;
-    double *rout = rnew + (size_t)(q & 1) * rnew_stride;
-    const double *prow = prow_buf ? (prow_stride ? prow_buf + (size_t)(st->r / SX_TILE) * prow_stride + 2 : prow_buf)
-                                  : ((q >= 2 && st->r_prev == st->r) ? rprev : T + (size_t)rl * ld);
-    const double p = prow[c.map(1 + st->e)];
-    if (blockIdx.y == 0) {
-        objective_row(prow, p, d, st, enter_parts, c);
-        return;
-    }
-    const int rg = gridDim.y - 1;
-    const int N = c.Ns;
-    const int cb = (N + 511) / 512;
-    if ((int)blockIdx.x >= cb) return;
-    int bx = blockIdx.x, by = blockIdx.y - 1;
-    if (SNAKE && (q & 1)) {
-        bx = cb - 1 - bx;
-        by = rg - 1 - by;
-    }
-    __shared__ double s_f[RB];
-    const int i0 = by * RB;
-    if ((int)threadIdx.x < RB) {
-        const int i = i0 + threadIdx.x;
-        s_f[threadIdx.x] = (i < rows) ? -colE[i] / p : 0.0;
-    }
-    __syncthreads();
-    const int j = (bx * 256 + threadIdx.x) * 2;
-    if (j >= N) return;
-    const int nrow = rows - i0 < RB ? rows - i0 : RB;
-    // pair (j, j+1) always: j+1 < ld (see k_update)
-    const double2 pr = *reinterpret_cast<const double2 *>(prow + j);
-    const bool fin = skip_zero && isfinite(pr.x) && isfinite(pr.y);
-    double *base = T + (size_t)i0 * ld + j;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(T + (size_t)i0 * ld, 0, (int)(RB * ld * 8), 0x00020000);
-    bool skip[RB];
-    double2 x[RB];
-#pragma unroll
-    for (int k = 0; k < RB; ++k) {
-        skip[k] = k >= nrow || i0 + k == rl || (fin && s_f[k] == 0.0 && i0 + k != pl);
-        if (!skip[k]) x[k] = *reinterpret_cast<const double2 *>(i0 + k == pl ? rprev + j : base + (size_t)k * ld);
-    }
-#pragma unroll
-    for (int k = 0; k < RB; ++k) {
-        if (k < nrow && i0 + k == rl)
-            *reinterpret_cast<double2 *>(rout + j) = make_double2(pr.x / p, pr.y / p);
-        if (skip[k]) continue;
-        x[k].x = fma(s_f[k], pr.x, x[k].x);
-        x[k].y = fma(s_f[k], pr.y, x[k].y);
-        store_pair<SC1>(base + (size_t)k * ld, x[k], rs, (int)(((size_t)k * ld + j) * 8));
-    }
-}
-
-// Phase end: write the last pivot row back from rnew[pivots & 1] (idempotent).
-__global__ void k_flush_row(double *T, int rows, int row0, size_t ld, int Ns, const double *rnew, size_t rnew_stride,
-                            const DevState *st) {
-    const long long q = st->pivots;
-    if (q <= 0) return;
-    const int rl = st->r - row0;
-    if (rl < 0 || rl >= rows) return;
-    const double *src = rnew + (size_t)(q & 1) * rnew_stride;
-    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < Ns; j += gridDim.x * blockDim.x)
-        T[(size_t)rl * ld + j] = src[j];
 }
 
 // Virtual-rank "allreduce": out = sum of the shards' contributions in rank order.  Exact,
@@ -889,37 +776,47 @@ void sx_launch_enter(const double *d, int L, TilePart *parts, DevState *st, hipS
 }
 
 void sx_launch_ratio_select(const double *T, int rows, int row0, size_t ld, TilePart *tiles_local, double *colE,
-                            DevState *st, int *base, const double *rnew, size_t rnew_stride, bool select,
-                            double *slots, size_t slot_stride, Cols c, int *rowlist, int *tile_cnt, int skip_zero,
-                            hipStream_t s) {
+                            DevState *st, int *base, bool select, double *slots, size_t slot_stride, Cols c,
+                            const Pending &pd, hipStream_t s) {
     int g = (rows + SX_TILE - 1) / SX_TILE;
     if (g < 1) g = 1;  // a shard without rows still decides optimality for its own state
     if (select && g > SX_TILE) SX_FATAL("too many ratio tiles for the 512-thread pass 2");
-    k_ratio_select<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, tiles_local, colE, st, base, rnew, rnew_stride,
-                                         select ? 1 : 0, slots, slot_stride, c, rowlist, tile_cnt, skip_zero);
+    if (pd.q < 0 || pd.q >= SX_KMAX) SX_FATAL("pending slot out of range");
+    k_ratio_select<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, tiles_local, colE, st, base, select ? 1 : 0, slots,
+                                         slot_stride, c, pd.F, pd.U, pd.recs, pd.PM, pd.batch, pd.q);
 }
 
 void sx_launch_select_gathered(const double *slots, size_t slot_stride, int B2, int *base, DevState *st,
-                               int tile0, int nslots, hipStream_t s) {
+                               const Pending &pd, hipStream_t s) {
     if (B2 > SX_TILE) SX_FATAL("too many ratio tiles for the 512-thread pass 2");
-    k_select_gathered<<<1, SX_TILE, 0, s>>>(slots, slot_stride, B2, base, st, tile0, nslots);
+    k_select_gathered<<<1, SX_TILE, 0, s>>>(slots, slot_stride, B2, base, st, pd.batch, pd.q);
 }
 
 void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, Cols c, const TilePart *tiles_all, int B2,
-                          double *prow_out, int *base, DevState *st, const double *rnew, size_t rnew_stride,
-                          int tile0, int nslots, hipStream_t s) {
+                          double *prow_out, int *base, DevState *st, const Pending &pd, hipStream_t s) {
     if (B2 > SX_TILE) SX_FATAL("too many ratio tiles for the 512-thread pass 2");
     const int N = c.Ns;
     int g = (N + 4 * SX_TILE - 1) / (4 * SX_TILE);
     if (g < 1) g = 1;
     if (g > 64) g = 64;
-    k_select_row<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, N, tiles_all, B2, prow_out, base, st, rnew, rnew_stride,
-                                       tile0, nslots);
+    k_select_row<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, N, tiles_all, B2, prow_out, base, st, pd.F, pd.U, pd.recs,
+                                       pd.PM, pd.batch, pd.q);
+}
+
+void sx_launch_pivot_row(const double *T, int rows, int row0, size_t ld, Cols c, double *d, const double *prow_buf,
+                         size_t prow_stride, const double *colE, DevState *st, const Pending &pd,
+                         TilePart *enter_parts, hipStream_t s) {
+    const int B1 = (c.N - 1 + SX_TILE - 1) / SX_TILE;
+    if (B1 > 256) SX_FATAL("entering vector too long for the pivot-row kernel's pass 2");
+    if (B1 < 1) SX_FATAL("empty objective row");
+    const int fb = rows > 0 ? (rows + 255) / 256 : 0;
+    k_pivot_row<<<B1 + fb, 256, 0, s>>>(T, rows, row0, ld, c, d, prow_buf, prow_stride, colE, st, pd.U, pd.F, pd.recs,
+                                        pd.PM, enter_parts, pd.batch, pd.q, B1);
 }
 
 // blocks of a kernel resident on the whole device at once
 template <typename K>
-static int update_capacity(K kernel) {
+static int sweep_capacity(K kernel) {
     static int cap = 0;  // per kernel instantiation
     if (cap == 0) {
         int per_cu = 0, dev = 0, cus = 0;
@@ -931,81 +828,57 @@ static int update_capacity(K kernel) {
     return cap;
 }
 
-// row-sweeping blocks per column tile: the whole grid (objective row + G rows of tiles)
-// resident in one wave, each block looping over its share of the row groups
-static float g_update_waves = 2.0f;
-void sx_set_update_waves(float w) { g_update_waves = w > 0.f ? w : 2.0f; }
+// row slots per column tile: waves x (resident blocks) blocks in all, each walking its share
+// of the row groups
+static float g_sweep_waves = 1.0f;
+void sx_set_update_waves(float w) { g_sweep_waves = w > 0.f ? w : 1.0f; }
 
 static int row_slots(int capacity, int col_blocks, int rows, int rb) {
-    long long g = (long long)(g_update_waves * (float)capacity) / col_blocks - 1;
+    long long g = (long long)(g_sweep_waves * (float)capacity) / col_blocks;
     const long long groups = rows > 0 ? (rows + rb - 1) / rb : 1;
     if (g > groups) g = groups;
     if (g < 1) g = 1;
-    if (g > 65535 - 1) g = 65535 - 1;
+    if (g > 65535) g = 65535;
     return (int)g;
 }
 
-template <int RB>
-static void launch_update_rb(dim3 grid, bool snake, bool sc1, double *T, int rows, int row0, size_t ld, Cols N,
-                             double *d, const double *prow_buf, size_t prow_stride, const double *colE, DevState *st,
-                             double *rnew, size_t rnew_stride, TilePart *enter_parts, const int *rowlist,
-                             const int *tile_cnt, int ntiles, int skip_zero, bool one_shot, hipStream_t s) {
-#define SX_UPD(SN, SC)                                                                                           \
-    do {                                                                                                         \
-        if (one_shot) {                                                                                          \
-            grid.y = 1 + (rows > 0 ? (rows + RB - 1) / RB : 0);                                                  \
-            k_update_grid<RB, SN, SC><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow_buf, prow_stride, colE,  \
-                                                           st, rnew, rnew_stride, enter_parts, skip_zero);      \
-        } else {                                                                                                 \
-            grid.y = 1 + row_slots(update_capacity(k_update<RB, SN, SC>), grid.x, rows, RB);                    \
-            k_update<RB, SN, SC><<<grid, 256, 0, s>>>(T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st,   \
-                                                      rnew, rnew_stride, enter_parts, rowlist, tile_cnt, ntiles,  \
-                                                      skip_zero);                                                \
-        }                                                                                                        \
-    } while (0)
-    if (snake) {
-        if (sc1)
-            SX_UPD(true, true);
-        else
-            SX_UPD(true, false);
-    } else {
-        if (sc1)
-            SX_UPD(false, true);
-        else
-            SX_UPD(false, false);
-    }
-#undef SX_UPD
+template <int KT, int RB, bool SC1>
+static void launch_sweep_t(double *T, int rows, size_t ld, int Ns, const Pending &pd, const DevState *st, int rev,
+                           hipStream_t s) {
+    const int cb = (Ns + 511) / 512;
+    dim3 grid(cb, row_slots(sweep_capacity(k_sweep<KT, RB, SC1>), cb, rows, RB));
+    k_sweep<KT, RB, SC1><<<grid, 256, 0, s>>>(T, rows, ld, Ns, pd.F, pd.U, pd.recs, pd.PM, st, pd.batch, rev);
 }
 
-void sx_launch_update(double *T, int rows, int row0, size_t ld, Cols N, double *d, const double *prow_buf,
-                      size_t prow_stride, const double *colE, DevState *st, double *rnew, size_t rnew_stride,
-                      TilePart *enter_parts, const int *rowlist, const int *tile_cnt, UpdateCfg cfg, hipStream_t s) {
-    const int B1 = (N.N - 1 + SX_TILE - 1) / SX_TILE;
-    if (B1 > 256) SX_FATAL("entering vector too long for the update's pass 2");
-    int cols_blocks = (N.Ns + 511) / 512;
-    if (cols_blocks < B1) cols_blocks = B1;
-    const int ntiles = rows > 0 ? (rows + SX_TILE - 1) / SX_TILE : 1;  // k_ratio_select's grid
-    if (ntiles > SX_TILE) SX_FATAL("too many row tiles for the update's list scan");
-    dim3 grid(cols_blocks, 2);
-    const bool sn = cfg.snake != 0, sc = cfg.sc1 != 0;
-#define SX_RB(R)                                                                                             \
-    launch_update_rb<R>(grid, sn, sc, T, rows, row0, ld, N, d, prow_buf, prow_stride, colE, st, rnew, rnew_stride, \
-                        enter_parts, rowlist, tile_cnt, ntiles, cfg.skip_zero, cfg.one_shot != 0, s)
-    switch (cfg.rows_per_block) {
-    case 1: SX_RB(1); break;
-    case 2: SX_RB(2); break;
-    case 4: SX_RB(4); break;
-    default: SX_RB(8); break;
+template <int KT>
+static void launch_sweep_k(int rb, bool sc1, double *T, int rows, size_t ld, int Ns, const Pending &pd,
+                           const DevState *st, int rev, hipStream_t s) {
+    switch (rb) {
+    case 1: sc1 ? launch_sweep_t<KT, 1, true>(T, rows, ld, Ns, pd, st, rev, s)
+                : launch_sweep_t<KT, 1, false>(T, rows, ld, Ns, pd, st, rev, s); break;
+    case 2: sc1 ? launch_sweep_t<KT, 2, true>(T, rows, ld, Ns, pd, st, rev, s)
+                : launch_sweep_t<KT, 2, false>(T, rows, ld, Ns, pd, st, rev, s); break;
+    default: sc1 ? launch_sweep_t<KT, 4, true>(T, rows, ld, Ns, pd, st, rev, s)
+                 : launch_sweep_t<KT, 4, false>(T, rows, ld, Ns, pd, st, rev, s); break;
     }
-#undef SX_RB
 }
 
-void sx_launch_flush_row(double *T, int rows, int row0, size_t ld, int Ns, const double *rnew, size_t rnew_stride,
-                         const DevState *st, hipStream_t s) {
+void sx_launch_sweep(double *T, int rows, size_t ld, int Ns, const Pending &pd, const DevState *st, int rev,
+                     SweepCfg cfg, hipStream_t s) {
     if (rows <= 0) return;
-    int g = (Ns + 255) / 256;
-    if (g > 256) g = 256;
-    k_flush_row<<<g, 256, 0, s>>>(T, rows, row0, ld, Ns, rnew, rnew_stride, st);
+    const int k = cfg.batch;  // pivots the sweep may have to apply (register slots)
+    if (k <= 1)
+        launch_sweep_k<1>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, pd, st, rev, s);
+    else if (k <= 4)
+        launch_sweep_k<4>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, pd, st, rev, s);
+    else if (k <= 8)
+        launch_sweep_k<8>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, pd, st, rev, s);
+    else if (k <= 16)
+        launch_sweep_k<16>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, pd, st, rev, s);
+    else if (k <= SX_KMAX)
+        launch_sweep_k<SX_KMAX>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, pd, st, rev, s);
+    else
+        SX_FATAL("batch larger than SX_KMAX");
 }
 
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s) {

@@ -184,58 +184,87 @@ def test_session_pivots(gpu):
     p = sx.generateRandomProblem(2048, 1024, 205824, 1, 100)
     s = sx.Session(p)
     t = s.pivots(50, time_updates=True)
-    assert t.pivots == 50 and t.status == sx.NOT_ENDED and t.update_launches == 50
+    # 50 pivots = 3 full batches of 16 + one of 2, each ending with a sweep
+    assert t.pivots == 50 and t.status == sx.NOT_ENDED and t.update_launches == 4 and t.swept_pivots == 50
     assert t.update_ms > 0 and t.wall_ms >= t.update_ms
     assert t.stored_width == 1 + 2048 + 1024 and t.width == 1 + 2048 + 2 * 1024
-    assert t.update_bytes == 16.0 * 1024 * t.stored_width + 16.0 * t.width
-    t2 = s.pivots(10000)
+    assert t.update_bytes == 16.0 * 1024 * t.stored_width
+    assert t.swept_bytes == 4 * t.update_bytes
+    applied, us = s.launch_log()
+    assert list(applied) == [16, 16, 16, 2] and (us > 0).all()
+    t2 = s.pivots(10000, time_updates=1)
     assert s.total_pivots() == 2003 and t2.status == sx.FEASIBLE
+    assert t2.swept_pivots == 2003 - 50  # no-op sweeps after the phase ended are not counted
     s.close()
 
 
-@pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("rb", [1, 2, 4, 8])
-@pytest.mark.parametrize("snake", [0, 1])
-@pytest.mark.parametrize("sc1", [0, 1])
-def test_update_configs_bit_exact(gpu, mode, rb, snake, sc1):
-    """every (kernel form, rows per block/iteration, sweep order, store flavour) variant of the
-    update kernel gives the same bits"""
-    T, d, base = _phase1_state(333, 1025, 7)
+def _pivots_with(cfg, T, d, base, k):
     Tg, dg, bg = T.copy(), d.copy(), base.copy()
+    setters = {"batch": (sx.set_batch, 0), "rb": (sx.set_update_rows, 0), "sc1": (sx.set_store_sc1, -1),
+               "waves": (sx.set_update_waves, 0), "W": (sx.set_virtual_ranks, 1)}
     try:
-        sx.set_update_mode(mode)
-        sx.set_update_rows(rb)
-        sx.set_snake(snake)
-        sx.set_store_sc1(sc1)
-        sx.dev_pivots(Tg, dg, bg, 21)
+        for key, val in cfg.items():
+            setters[key][0](val)
+        st, done = sx.dev_pivots(Tg, dg, bg, k)
     finally:
-        sx.set_update_mode(-1)
-        sx.set_update_rows(0)
-        sx.set_snake(-1)
-        sx.set_store_sc1(-1)
-    oracle.solve(T, d, base, max_pivots=21)
+        for key in cfg:
+            setters[key][0](setters[key][1])
+    return Tg, dg, bg, st, done
+
+
+@pytest.mark.parametrize("batch", [1, 2, 3, 7, 16, 17, 32])
+@pytest.mark.parametrize("rb", [1, 2, 4])
+def test_batched_sweep_bit_exact(gpu, batch, rb):
+    """k pivots with the tableau swept every `batch` pivots (pending pivots applied on the fly
+    to the columns and rows the decisions read): the same bits as the oracle's pivot-by-pivot
+    updates, for every register-slot variant of the sweep and a partial last batch"""
+    T, d, base = _phase1_state(333, 1025, 7)
+    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "rb": rb}, T, d, base, 45)
+    oracle.solve(T, d, base, max_pivots=45)
+    assert done == 45
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 
-@pytest.mark.parametrize("waves", [1e-4, 0.3, 2, 64])
-@pytest.mark.parametrize("skip", [0, 1])
-def test_update_row_sweep_slots_bit_exact(gpu, waves, skip):
-    """the resident row sweep with 1 block per column tile (every block walks all row groups,
-    both directions) up to more blocks than row groups"""
+@pytest.mark.parametrize("sc1", [0, 1])
+@pytest.mark.parametrize("waves", [1e-4, 0.3, 1, 4])
+def test_sweep_grid_bit_exact(gpu, sc1, waves):
+    """one block per column tile walking every row group (both directions) up to more blocks
+    than row groups; plain and write-through stores"""
     T, d, base = _phase1_state(210, 1700, 3)
-    Tg, dg, bg = T.copy(), d.copy(), base.copy()
-    try:
-        sx.set_update_mode(0)
-        sx.set_update_waves(waves)
-        sx.set_skip_zero(skip)
-        sx.set_snake(1)
-        sx.dev_pivots(Tg, dg, bg, 90)
-    finally:
-        sx.set_update_mode(-1)
-        sx.set_update_waves(0)
-        sx.set_skip_zero(1)
-        sx.set_snake(-1)
+    Tg, dg, bg, st, done = _pivots_with({"sc1": sc1, "waves": waves, "batch": 16}, T, d, base, 90)
     oracle.solve(T, d, base, max_pivots=90)
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+@pytest.mark.parametrize("batch", [1, 5, 16])
+def test_batched_phase_end_mid_batch(gpu, batch):
+    """the phase ends inside a batch: the pivots selected before the end are swept, the rest of
+    the batch does nothing"""
+    T, d, base = _phase1_state(64, 128, 6528)
+    Tg, dg, bg, st, done = _pivots_with({"batch": batch}, T, d, base, 100000)
+    st_o, done_o = oracle.solve(T, d, base)
+    assert st == st_o == oracle.FEASIBLE and done == done_o
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+@pytest.mark.parametrize("batch", [1, 16])
+def test_same_row_leaves_twice_in_a_batch(gpu, batch):
+    """a row that is the leaving row of two pivots of one batch (the general path of the sweep:
+    x / p for that slot): on this instance the oracle's leaving rows are 7, 6, 1, 7, 7, 7, ..."""
+    T, d, base = _phase1_state(20, 10, 2010)
+    ref = (T.copy(), d.copy(), base.copy())
+    st_o, done_o = oracle.solve(*ref)
+    Tg, dg, bg, st, done = _pivots_with({"batch": batch}, T, d, base, 100000)
+    assert st == st_o and done == done_o
+    assert same(Tg, ref[0]) and same(dg, ref[1]) and np.array_equal(bg, ref[2])
+
+
+@pytest.mark.parametrize("batch", [4, 16])
+@pytest.mark.parametrize("W", [2, 3])
+def test_batched_virtual_ranks(gpu, batch, W):
+    T, d, base = _phase1_state(300, 1100, 11)
+    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "W": W}, T, d, base, 120)
+    oracle.solve(T, d, base, max_pivots=120)
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 
@@ -297,32 +326,10 @@ def test_pivots_without_alias_invariant(gpu):
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 
-# ------------------------------------------------------------------ zero-factor row skipping
-@pytest.mark.parametrize("skip", [0, 1])
-@pytest.mark.parametrize("rb,W", [(1, 1), (2, 1), (8, 1), (2, 3)])
-def test_skip_zero_bit_exact(gpu, skip, rb, W):
-    """rows whose entering-column entry is exactly 0 are left untouched: same bits as the
-    oracle's full sweep (about half of the phase-1 pivots bring in a slack column whose entries
-    are almost all 0)"""
-    T, d, base = _phase1_state(300, 1100, 11)
-    Tg, dg, bg = T.copy(), d.copy(), base.copy()
-    try:
-        sx.set_skip_zero(skip)
-        sx.set_update_rows(rb)
-        sx.set_virtual_ranks(W)
-        sx.dev_pivots(Tg, dg, bg, 120)
-    finally:
-        sx.set_skip_zero(1)
-        sx.set_update_rows(0)
-        sx.set_virtual_ranks(1)
-    oracle.solve(T, d, base, max_pivots=120)
-    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
-
-
 @pytest.mark.parametrize("lo", [-100, 1])
-def test_skip_zero_disengaged_with_negative_zeros(gpu, lo):
-    """a tableau holding -0.0 (the b<0 row negation of the build, or a caller's upload) must be
-    swept in full: fma(0, p, -0.0) is +0.0, so skipping would change bits"""
+def test_negative_zeros_kept(gpu, lo):
+    """a tableau holding -0.0 (the b<0 row negation of the build, or a caller's upload):
+    fma(0, p, -0.0) is +0.0, and every element is swept exactly as the reference does"""
     T, d, base = _phase1_state(200, 700, 5, lo, 100)
     if lo > 0:
         T[T == 0.0] = -0.0
@@ -333,33 +340,11 @@ def test_skip_zero_disengaged_with_negative_zeros(gpu, lo):
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 
-def test_skip_zero_two_phase_negated_rows(gpu):
+def test_two_phase_negated_rows(gpu):
     """generated instances with b_i < 0 (values in [-100, 100]): host and device builds"""
     p = sx.generateRandomProblem(150, 700, 1234, -100, 100)
     _check_two_phase(p)
     s = sx.Session(generated=(150, 700, 1234, -100, 100))
     t = s.pivots(40, time_updates=1)
-    assert t.touched_rows == 40 * 700  # full sweeps: the tableau holds -0.0
+    assert t.pivots == 40 and t.swept_pivots == 40
     s.close()
-
-
-def test_session_touched_rows(gpu):
-    """touched-row accounting of the timed updates: full sweeps with skipping off, fewer rows
-    with it on, and the same pivots either way"""
-    n, m = 2048, 1024
-    res = {}
-    for skip in (0, 1):
-        try:
-            sx.set_skip_zero(skip)
-            s = sx.Session(generated=(n, m, n * 100 + m, 1, 100))
-            t = s.pivots(400, time_updates=1)
-            res[skip] = (t, s.objective())
-            s.close()
-        finally:
-            sx.set_skip_zero(1)
-    t0, t1 = res[0][0], res[1][0]
-    assert t0.touched_rows == 400 * m
-    assert t0.touched_bytes == pytest.approx(400 * t0.update_bytes, rel=1e-3)  # pairs: ceil(width / 2)
-    assert 400 <= t1.touched_rows < t0.touched_rows
-    assert t1.touched_bytes < t0.touched_bytes
-    assert same(res[0][1], res[1][1])
