@@ -18,6 +18,7 @@ extern "C" {
 #define SIMPLEX_NOT_ENDED -10    /* solver.cu:77 */
 #define SIMPLEX_PIVOT_CAP -11    /* opt-in pivot budget reached */
 #define SIMPLEX_NUMERIC_FAIL -12 /* eligible pivot but the ratio argmin found no row */
+#define SIMPLEX_HANG -13         /* fused batch: an in-kernel hand-off timed out (never expected) */
 
 /* ---- configuration ---- */
 int simplex_version(void);
@@ -51,6 +52,10 @@ void simplex_set_force_exchange(int on);
 void simplex_set_exchange_mode(int mode);
 /* store each phase-1 artificial column as its (bit-identical) slack column: 1 on (default), 0 off */
 void simplex_set_alias(int on);
+/* one shard: run each batch of pivots as ONE resident launch (ratio tiles + objective-row tiles
+ * handing off through write-through records) instead of two launches per pivot;
+ * -1 auto (default: when the grid fits the device), 0 off */
+void simplex_set_fused(int mode);
 /* the sweep's grid: waves x (blocks resident on the device) blocks (default 1; <= 0 resets) */
 void simplex_set_update_waves(double waves);
 

@@ -26,7 +26,7 @@ def per_kernel(path, counter):
 
 def main():
     prof, tag = sys.argv[1], sys.argv[2]
-    sub = sys.argv[3] if len(sys.argv) > 3 else "k_update"
+    sub = sys.argv[3] if len(sys.argv) > 3 else "k_sweep"
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = os.path.join(root, "profiles")
     os.makedirs(out, exist_ok=True)

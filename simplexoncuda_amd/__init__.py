@@ -5,9 +5,9 @@ host API (include/problem.h, tabular.h, solver.h, twoPhaseMethod.h).  This packa
 thin Python mirror of that API; see DESIGN.md.
 """
 from .api import (  # noqa: F401
-    DEGENERATE, FEASIBLE, INFEASIBLE, NOT_ENDED, NUMERIC_FAIL, PIVOT_CAP, RAND_GLIBC, RAND_MSVC,
+    DEGENERATE, FEASIBLE, HANG, INFEASIBLE, NOT_ENDED, NUMERIC_FAIL, PIVOT_CAP, RAND_GLIBC, RAND_MSVC,
     STATUS_NAMES, UNBOUNDED, Problem, Result, Session, dev_argmin, dev_build_phase1, dev_pivots,
     dev_build_phase1_generated, dev_update_objective, generateRandomProblem, generateRandomProblemDevice, printProblemToStream, readProblemFromFile,
-    readRandomProblemFromFile, set_alias, set_batch, set_update_waves, set_exchange_mode, set_force_exchange, set_snake, set_store_sc1, set_update_rows, set_verbose, set_virtual_ranks,
+    readRandomProblemFromFile, set_alias, set_batch, set_fused, set_update_waves, set_exchange_mode, set_force_exchange, set_snake, set_store_sc1, set_update_rows, set_verbose, set_virtual_ranks,
     twoPhaseMethod, twoPhaseMethodEx)
 from ._lib import LIB_PATH, load  # noqa: F401

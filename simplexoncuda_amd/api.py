@@ -19,10 +19,11 @@ DEGENERATE = -3
 NOT_ENDED = -10
 PIVOT_CAP = -11
 NUMERIC_FAIL = -12
+HANG = -13
 
 STATUS_NAMES = {FEASIBLE: "FEASIBLE", INFEASIBLE: "INFEASIBLE", UNBOUNDED: "UNBOUNDED",
                 DEGENERATE: "DEGENERATE", NOT_ENDED: "NOT_ENDED", PIVOT_CAP: "PIVOT_CAP",
-                NUMERIC_FAIL: "NUMERIC_FAIL"}
+                NUMERIC_FAIL: "NUMERIC_FAIL", HANG: "HANG"}
 
 RAND_MSVC = 0
 RAND_GLIBC = 1
@@ -279,6 +280,11 @@ def set_exchange_mode(mode):
 
 def set_alias(on):
     _lib.load().simplex_set_alias(1 if on else 0)
+
+
+def set_fused(mode):
+    """-1 auto (one launch per batch of pivots on a single shard), 0 two launches per pivot."""
+    _lib.load().simplex_set_fused(int(mode))
 
 
 def set_update_waves(w):

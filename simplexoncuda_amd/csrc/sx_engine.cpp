@@ -62,6 +62,7 @@ struct Config {
     std::string timer_dir;   // non-empty: write the reference's TIMER CSV there
     int exchange_mode = 0;   // 0 auto, 1 tile allgather + row allreduce, 2 row-gather
     int alias = 1;           // store phase-1 artificial columns as their slack columns
+    int fused = -1;          // whole batches in one resident launch: -1 auto (one shard), 0 off
     int debug = -1;          // -1: from SIMPLEX_DEBUG; 1: print the tableau after every step
     bool benchmark = false;
     // distributed
@@ -174,6 +175,9 @@ struct Shard {
     TilePart *enter_parts = nullptr;
     TilePart *tiles_local = nullptr;
     TilePart *tiles_all = nullptr;
+    BatchChan *chan = nullptr;        // fused batch kernel: hand-off records
+    TileA *tiles_a = nullptr;         // fused batch kernel: ratio-tile winners
+    TilePart *tiles_b = nullptr;      // fused batch kernel: objective-tile winners
     DevState *st = nullptr;
 };
 
@@ -301,6 +305,10 @@ class Engine {
         if (xchg) x.rhs_all = dalloc<double>((size_t)W * rpr);
         x.base = dalloc<int>(m);
         x.enter_parts = dalloc<TilePart>(SX_TILE);
+        x.chan = dalloc<BatchChan>(1);
+        x.tiles_a = dalloc<TileA>(SX_TILE);
+        x.tiles_b = dalloc<TilePart>(SX_TILE);
+        SX_HIP(hipMemsetAsync(x.chan, 0, sizeof(BatchChan), s));
         x.tiles_local = dalloc<TilePart>(slots);
         if (xchg) x.tiles_all = dalloc<TilePart>((size_t)W * slots);
         x.st = dalloc<DevState>(1);
@@ -323,7 +331,8 @@ class Engine {
         for (void *p : {(void *)x.T, (void *)x.d, (void *)x.colE, (void *)x.prow, (void *)x.prow_send,
                         (void *)x.slot_send, (void *)x.slot_all, (void *)x.U, (void *)x.F, (void *)x.recs, (void *)x.PM,
                         (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
-                        (void *)x.rhs_all, (void *)x.base, (void *)x.enter_parts, (void *)x.tiles_local,
+                        (void *)x.rhs_all, (void *)x.base, (void *)x.enter_parts, (void *)x.tiles_local, (void *)x.chan,
+                        (void *)x.tiles_a, (void *)x.tiles_b,
                         (void *)x.tiles_all, (void *)x.st})
             if (p) (void)hipFree(p);
     }
@@ -512,6 +521,19 @@ class Engine {
         ++q_host;
     }
 
+    // a whole batch of up to k pivots in one resident launch (one shard, no exchange)
+    bool fused_ok(int k) const {
+        if (g_cfg.fused == 0 || xchg || sh.size() != 1 || on_pivot) return false;
+        return sx_batch_fits(sh[0].rows, cols(N), k);
+    }
+
+    void enqueue_batch(int k) {
+        Shard &x = sh[0];
+        if (q_host != 0) SX_FATAL("fused batch inside a started batch");
+        sx_launch_batch(x.T, x.rows, ld, cols(N), x.d, x.base, x.st, pending(x), k, x.chan, x.tiles_a, x.tiles_b, s);
+        q_host = k;
+    }
+
     // apply the batch's pivots to the tableau (a no-op kernel when none was selected) and
     // start a new batch
     void enqueue_sweep(hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
@@ -567,9 +589,11 @@ class Engine {
         }
         // batches of K pivots + one sweep; the host polls the status of the batch before the
         // last one, so the device never waits on the host
+        const bool fused = !timed && fused_ok(K);
         long long k = 0;
         for (; !on_pivot; ++k) {
-            for (int b = 0; b < K; ++b) {
+            if (fused) enqueue_batch(K);
+            for (int b = 0; b < K && !fused; ++b) {
                 if (timed) {
                     hipEvent_t e0, e1;
                     SX_HIP(hipEventCreate(&e0));
@@ -751,8 +775,8 @@ int two_phase(problem_t *P, double *solution, double *opt, int *base_out, long l
     std::vector<int> base(m);
     if (st1 == SX_PIVOT_CAP) {
         status = SX_PIVOT_CAP;
-    } else if (st1 == SX_NUMERIC_FAIL) {
-        status = SX_NUMERIC_FAIL;
+    } else if (st1 == SX_NUMERIC_FAIL || st1 == SX_HANG) {
+        status = st1;
     } else if (compare(d0) < 0) {
         status = INFEASIBLE;  // :265-268
     } else {
@@ -822,6 +846,7 @@ void simplex_set_device(int device) {
 void simplex_set_virtual_ranks(int world) { g_cfg.virtual_ranks = world > 1 ? world : 1; }
 void simplex_set_force_exchange(int on) { g_cfg.force_exchange = on ? 1 : 0; }
 void simplex_set_alias(int on) { g_cfg.alias = on ? 1 : 0; }
+void simplex_set_fused(int mode) { g_cfg.fused = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_update_waves(double waves) { sx_set_update_waves((float)waves); }
 void simplex_set_exchange_mode(int mode) { g_cfg.exchange_mode = (mode >= 0 && mode <= 2) ? mode : 0; }
 void simplex_set_timer_dir(const char *dir) { g_cfg.timer_dir = dir ? dir : ""; }
@@ -984,6 +1009,7 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
     SX_HIP(hipEventCreate(&w1));
     const long long before = E.read_state().pivots;
     long long nsw = 0, ntimed = 0;
+    const bool fused = E.fused_ok(K);
     auto sweep = [&]() {
         const bool timed = every && (nsw % every == 0) && ntimed < nt;
         const unsigned id = E.batch_id;
@@ -997,9 +1023,16 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
         ++nsw;
     };
     SX_HIP(hipEventRecord(w0, E.s));
-    for (long long i = 0; i < k; ++i) {
-        E.enqueue_pivot();
-        if (E.q_host >= K) sweep();
+    for (long long i = 0; i < k;) {
+        if (fused) {
+            const int kb = (int)std::min<long long>(K, k - i);
+            E.enqueue_batch(kb);
+            i += kb;
+        } else {
+            E.enqueue_pivot();
+            ++i;
+        }
+        if (E.q_host >= K || (fused && E.q_host > 0)) sweep();
     }
     if (E.q_host > 0) sweep();
     SX_HIP(hipEventRecord(w1, E.s));

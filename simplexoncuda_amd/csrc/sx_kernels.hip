@@ -171,17 +171,74 @@ __device__ __forceinline__ unsigned pend_bits(const unsigned long long *__restri
     return ((unsigned)(w >> 32) == B) ? ((unsigned)w & mask) : 0u;
 }
 
-// value of stored column `col` of a local row after the q pending pivots
-__device__ __forceinline__ double cur_value(double x, int q, unsigned bits, const double *__restrict__ Frow,
-                                            const double *__restrict__ U, size_t ld, int col,
-                                            const PivRec *__restrict__ recs) {
-    for (int s = 0; s < q; ++s) {
-        if ((bits >> s) & 1u)
-            x = x / recs[s].p;
-        else
-            x = fma(Frow[s], U[(size_t)s * ld + col], x);
+// Values of NC stored columns col[] of ONE row after its q pending pivots.  The row's
+// factors sf[s] = F[row][s] and the pivots sp[s] are block-uniform (staged in LDS); the
+// pivot-row values U[s][col] are loaded 8 slots at a time so their latencies overlap (slots
+// >= q are read -- U has SX_KMAX rows -- but not used).
+template <int NC>
+__device__ __forceinline__ void cur_cols(double (&x)[NC], const int (&col)[NC], int q, unsigned bits,
+                                         const double *sf, const double *sp, const double *__restrict__ U,
+                                         size_t ld) {
+    for (int s0 = 0; s0 < q; s0 += 8) {
+        double u[8][NC];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const double *Us = U + (size_t)(s0 + k) * ld;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) u[k][c] = Us[col[c]];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int s = s0 + k;
+            if (s < q) {
+                if ((bits >> s) & 1u) {
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) x[c] = x[c] / sp[s];
+                } else {
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) x[c] = fma(sf[s], u[k][c], x[c]);
+                }
+            }
+        }
     }
-    return x;
+}
+
+__device__ __forceinline__ void cur_pair(double &xa, double &xb, int ca, int cb, int q, unsigned bits,
+                                         const double *sf, const double *sp, const double *__restrict__ U,
+                                         size_t ld) {
+    double x[2] = {xa, xb};
+    const int col[2] = {ca, cb};
+    cur_cols<2>(x, col, q, bits, sf, sp, U, ld);
+    xa = x[0];
+    xb = x[1];
+}
+
+// Block-uniform pending data of one row (the pivot row being formed): its factors, the
+// pivots, and its pivot-slot bits.  All threads of the block must call it.
+__device__ __forceinline__ unsigned stage_row(const double *__restrict__ F, const PivRec *__restrict__ recs,
+                                              const unsigned long long *__restrict__ PM, int rl, unsigned B, int q,
+                                              double *sf, double *sp) {
+    const int t = threadIdx.x;
+    if (t < q) {
+        sf[t] = F[(size_t)rl * SX_KMAX + t];
+        sp[t] = recs[t].p;
+    }
+    __syncthreads();
+    return q > 0 ? pend_bits(PM, rl, B, slot_mask(q)) : 0u;
+}
+
+// current values of row rl, columns [0, Ns), written to out (stride over the block; Ns
+// columns in pairs j, j + blockDim)
+__device__ __forceinline__ void cur_row(const double *__restrict__ src, int Ns, int q, unsigned bits,
+                                        const double *sf, const double *sp, const double *__restrict__ U, size_t ld,
+                                        double *out, int first, int stride) {
+    for (int j = first; j < Ns; j += 2 * stride) {
+        const int jb = j + stride < Ns ? j + stride : j;
+        double xa = src[j], xb = src[jb];
+        cur_pair(xa, xb, j, jb, q, bits, sf, sp, U, ld);
+        out[j] = xa;
+        if (j + stride < Ns) out[jb] = xb;
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -224,25 +281,44 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
     const unsigned mask = slot_mask(q);
     __shared__ double s_v[16];
     __shared__ int s_i[16];
+    // the pending pivot rows' RHS and entering-column entries, and the pivots (uniform)
+    __shared__ double s_u0[SX_KMAX], s_ue[SX_KMAX], s_p[SX_KMAX];
+    if ((int)threadIdx.x < q) {
+        const double *Us = U + (size_t)threadIdx.x * ld;
+        s_u0[threadIdx.x] = Us[0];
+        s_ue[threadIdx.x] = Us[ce];
+        s_p[threadIdx.x] = recs[threadIdx.x].p;
+    }
     const int li = blockIdx.x * SX_TILE + threadIdx.x;
     double rv = DBL_MAX;
     int ri = -1;
     int elig = 0;
+    double b = 0.0, a = 0.0;
+    unsigned bits = 0u;
     if (li < rows) {
         const double *row = T + (size_t)li * ld;
-        double b = row[0], a = row[ce];
-        if (q > 0) {
-            const unsigned bits = pend_bits(PM, li, B, mask);
-            const double *Fr = F + (size_t)li * SX_KMAX;
-            for (int s = 0; s < q; ++s) {
-                if ((bits >> s) & 1u) {
-                    const double p = recs[s].p;
-                    b = b / p;
-                    a = a / p;
-                } else {
-                    const double f = Fr[s];
-                    b = fma(f, U[(size_t)s * ld], b);
-                    a = fma(f, U[(size_t)s * ld + ce], a);
+        b = row[0];
+        a = row[ce];
+        if (q > 0) bits = pend_bits(PM, li, B, mask);
+    }
+    __syncthreads();
+    if (li < rows) {
+        const double *Fr = F + (size_t)li * SX_KMAX;
+        for (int s0 = 0; s0 < q; s0 += 8) {
+            double f[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) f[k] = Fr[s0 + k];  // s0 + k < SX_KMAX
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int s = s0 + k;
+                if (s < q) {
+                    if ((bits >> s) & 1u) {
+                        b = b / s_p[s];
+                        a = a / s_p[s];
+                    } else {
+                        b = fma(f[k], s_u0[s], b);
+                        a = fma(f[k], s_ue[s], a);
+                    }
                 }
             }
         }
@@ -268,6 +344,7 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
         // row-gather exchange: the slot carries the tile winner and that row's current
         // values, so one allgather hands every rank the pivot row whichever tile wins
         __shared__ int s_ri;
+        __shared__ double s_f[SX_KMAX];
         double *slot = slots + (size_t)blockIdx.x * slot_stride;
         if (threadIdx.x == 0) {
             TilePart *h = reinterpret_cast<TilePart *>(slot);
@@ -277,13 +354,10 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
             s_ri = ri;
         }
         __syncthreads();
+        if (s_ri < 0) return;
         const int wl = s_ri - row0;
-        if (s_ri >= 0) {
-            const double *src = T + (size_t)wl * ld;
-            const unsigned bits = pend_bits(PM, wl, B, mask);
-            const double *Fr = F + (size_t)wl * SX_KMAX;
-            for (int j = threadIdx.x; j < c.Ns; j += SX_TILE) slot[2 + j] = cur_value(src[j], q, bits, Fr, U, ld, j, recs);
-        }
+        const unsigned wbits = stage_row(F, recs, PM, wl, B, q, s_f, s_p);
+        cur_row(T + (size_t)wl * ld, c.Ns, q, wbits, s_f, s_p, U, ld, slot + 2, threadIdx.x, SX_TILE);
         return;
     }
     __shared__ int s_last;
@@ -366,11 +440,10 @@ __global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T
     const int rl = r - row0;
     const bool own = rl >= 0 && rl < rows;
     if (own) {
-        const double *src = T + (size_t)rl * ld;
-        const unsigned bits = pend_bits(PM, rl, B, slot_mask(q));
-        const double *Fr = F + (size_t)rl * SX_KMAX;
-        for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < Ns; j += gridDim.x * blockDim.x)
-            prow_out[j] = cur_value(src[j], q, bits, Fr, U, ld, j, recs);
+        __shared__ double s_f[SX_KMAX], s_p[SX_KMAX];
+        const unsigned bits = stage_row(F, recs, PM, rl, B, q, s_f, s_p);
+        cur_row(T + (size_t)rl * ld, Ns, q, bits, s_f, s_p, U, ld, prow_out, blockIdx.x * blockDim.x + threadIdx.x,
+                gridDim.x * blockDim.x);
     } else {
         for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < Ns; j += gridDim.x * blockDim.x) prow_out[j] = -0.0;
     }
@@ -452,12 +525,18 @@ __global__ __launch_bounds__(256) void k_pivot_row(const double *__restrict__ T,
     const double *prow =
         prow_buf ? (prow_stride ? prow_buf + (size_t)(r / SX_TILE) * prow_stride + 2 : prow_buf) : nullptr;
     const double *trow = T + (size_t)(prow ? 0 : rl) * ld;
-    const unsigned bits = prow ? 0u : pend_bits(PM, rl, B, slot_mask(q));
-    const double *Fr = F + (size_t)(prow ? 0 : rl) * SX_KMAX;
-    auto cur = [&](int col) -> double {
-        return prow ? prow[col] : cur_value(trow[col], q, bits, Fr, U, ld, col, recs);
-    };
-    const double p = cur(c.map(1 + e));
+    __shared__ double s_f[SX_KMAX], s_p[SX_KMAX];
+    const unsigned bits = prow ? 0u : stage_row(F, recs, PM, rl, B, q, s_f, s_p);
+    // current values of the pivot row at the entering column (the pivot), column 0 and this
+    // thread's two objective-row columns, with all their loads in flight together
+    const int L = c.N - 1;
+    const int ia = blockIdx.x * SX_TILE + threadIdx.x, ib = ia + 256;
+    const int col[4] = {c.map(1 + e), 0, c.map(1 + (ia < L ? ia : 0)), c.map(1 + (ib < L ? ib : 0))};
+    double x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = prow ? prow[col[k]] : trow[col[k]];
+    if (!prow) cur_cols<4>(x, col, q, bits, s_f, s_p, U, ld);
+    const double p = x[0], u0 = x[1], ua = x[2], ub = x[3];
     if ((int)blockIdx.x >= B1) {
         const int i = ((int)blockIdx.x - B1) * 256 + (int)threadIdx.x;
         if (i < rows) F[(size_t)i * SX_KMAX + q] = -colE[i] / p;
@@ -470,7 +549,6 @@ __global__ __launch_bounds__(256) void k_pivot_row(const double *__restrict__ T,
     double *Uq = U + (size_t)q * ld;
     const double fd = -st->dmin / p;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        const double u0 = cur(0);
         Uq[0] = u0;
         d[0] = fma(fd, u0, d[0]);
         recs[q].r = r;
@@ -481,15 +559,12 @@ __global__ __launch_bounds__(256) void k_pivot_row(const double *__restrict__ T,
     __shared__ double s_v[16];
     __shared__ int s_i[16];
     __shared__ int s_last;
-    const int L = c.N - 1;
     double v0 = DBL_MAX, v1 = DBL_MAX;
     int i0 = -1, i1 = -1;
-    const int ia = blockIdx.x * SX_TILE + threadIdx.x, ib = ia + 256;
     if (ia < L) {
         const int j = 1 + ia;
-        const double u = cur(c.map(j));
-        if (j < c.Ns) Uq[j] = u;
-        const double x = fma(fd, u, d[j]);
+        if (j < c.Ns) Uq[j] = ua;
+        const double x = fma(fd, ua, d[j]);
         d[j] = x;
         if (cmp_eps(x, v0) < 0) {
             v0 = x;
@@ -498,9 +573,8 @@ __global__ __launch_bounds__(256) void k_pivot_row(const double *__restrict__ T,
     }
     if (ib < L) {
         const int j = 1 + ib;
-        const double u = cur(c.map(j));
-        if (j < c.Ns) Uq[j] = u;
-        const double x = fma(fd, u, d[j]);
+        if (j < c.Ns) Uq[j] = ub;
+        const double x = fma(fd, ub, d[j]);
         d[j] = x;
         if (cmp_eps(x, v1) < 0) {
             v1 = x;
@@ -560,6 +634,363 @@ __global__ __launch_bounds__(256) void k_pivot_row(const double *__restrict__ T,
             st->ticket_d = 0;
         }
     }
+}
+
+// ---------------------------------------------------------------------------------------
+// K6: a whole batch of pivots in ONE resident launch (one shard).  Blocks [0, NA) own the
+// 512-row ratio tiles, blocks [NA, NA + NB) the 512-entry objective-row tiles; each block
+// keeps its slice of the state on chip for the whole batch (the ratio blocks: their rows'
+// current RHS and the factor history F[.][s] in LDS; the objective blocks: their columns'
+// d values in registers and the pivot-row history U[s][.] in LDS).  Per pivot q:
+//   ratio blocks     wait for the entering variable of pivot q, form the current entering
+//                    column of their rows (T[i][e] + pending pivots), the ratio vector and
+//                    the tile winner; the last to arrive runs pass 2 and publishes the
+//                    selection (r, p, b_r), or the status that ends the phase;
+//   objective blocks wait for the selection, form the current pivot row on their columns,
+//                    update d and reduce it per tile; the last to arrive runs pass 2 and
+//                    publishes the entering variable of pivot q + 1.
+// The arithmetic and the argmin trees are those of k_ratio_select / k_pivot_row (reference:
+// solver.cu:78-126, reduction.cu:10-140).  Every hand-off is write-through (sc1) data, an
+// `s_waitcnt vmcnt(0)`, then an sc1 sequence-number store; consumers poll the number with sc1
+// loads and read the data with sc1 loads (MI355X_MICROARCH.md "Valid forms", row 1).  Every
+// wait is bounded: past ~0.2 s the block raises abort_w and all blocks leave (status SX_HANG).
+// The grid is launched only when all its blocks are resident at once (sx_batch_fits).
+
+__device__ __forceinline__ void st_sc1(double *p, double v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(int *p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double *p) {
+    return __longlong_as_double((long long)__hip_atomic_load(
+        reinterpret_cast<unsigned long long *>(const_cast<double *>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ int ld_sc1(const int *p) {
+    return __hip_atomic_load(const_cast<int *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned ld_sc1(const unsigned *p) {
+    return __hip_atomic_load(const_cast<unsigned *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long *p) {
+    return __hip_atomic_load(const_cast<unsigned long long *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// one lane polls `seq` until it reads `want`; false if the batch was aborted (or this wait
+// timed out, which aborts it)
+__device__ bool wait_seq(const unsigned long long *seq, unsigned long long want, unsigned *abort_w) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+    for (unsigned it = 0;; ++it) {
+        if (ld_sc1(seq) == want) return true;
+        if ((it & 63) == 63) {
+            if (ld_sc1(abort_w) != 0u) return false;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // 0.2 s
+                __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return false;
+            }
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// arrival at a per-pivot ticket (after every wave of the block drained its stores); true in
+// the last block to arrive, which then owns the ticket until it resets it
+__device__ __forceinline__ bool arrive_last(unsigned *ticket, unsigned n, int *s_flag) {
+    drain();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *s_flag = (t == n - 1);
+    }
+    __syncthreads();
+    return *s_flag != 0;
+}
+
+__global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int rows, size_t ld, Cols c,
+                                               double *__restrict__ d, int *base, DevState *st, double *U, double *F,
+                                               PivRec *recs, unsigned long long *PM, unsigned B, int K, int NA,
+                                               int NB, BatchChan *ch, TileA *tiles_a, TilePart *tiles_b) {
+    extern __shared__ double s_hist[];  // [K][512]: F history (ratio blocks) / U history (objective blocks)
+    __shared__ double s_v[16];
+    __shared__ int s_i[16];
+    __shared__ double s_p[SX_KMAX], s_x[SX_KMAX];  // pivots; per-slot U[s][e] (ratio) / F[r][s] (objective)
+    __shared__ int s_r[SX_KMAX];                   // leaving rows (objective blocks)
+    __shared__ double s_a[SX_TILE], s_b[SX_TILE];  // ratio blocks: entering column, RHS (winner lookup)
+    __shared__ int s_flag, s_ok;
+    __shared__ double s_rp, s_rbr, s_rdmin;
+    __shared__ int s_rrow, s_rstatus;
+    __shared__ double s_edmin;
+    __shared__ int s_ee;
+    const int t = threadIdx.x;
+    const bool isA = (int)blockIdx.x < NA;
+    // state at the start of the batch: nothing writes st during the launch (the last block
+    // to leave writes it)
+    const int status0 = st->status;
+    const long long piv0 = st->pivots, cap = st->max_pivots;
+    int cnt = 0;  // pivots selected so far in this batch
+    if (status0 == SX_NOT_ENDED) {
+        if (isA) {
+            // ---------------------------------------------------------------- ratio tile
+            const int li = blockIdx.x * SX_TILE + t;
+            const bool live = li < rows;
+            double b = live ? T[(size_t)li * ld] : 0.0;  // current RHS of the row
+            unsigned bits = 0u;                           // slots where this row left the basis
+            int e = st->e_next;
+            double dmin = st->dmin_next;
+            for (int q = 0; q < K; ++q) {
+                const unsigned long long seq = ((unsigned long long)B << 8) | (unsigned)q;
+                if (q > 0) {
+                    if (t == 0) {
+                        s_ok = wait_seq(&ch->e_seq, seq, &ch->abort_w);
+                        if (s_ok) {
+                            s_ee = ld_sc1(&ch->e_e);
+                            s_edmin = ld_sc1(&ch->e_dmin);
+                        }
+                    }
+                    __syncthreads();
+                    if (!s_ok) break;
+                    e = s_ee;
+                    dmin = s_edmin;
+                }
+                // ends the phase? (the same decision in every ratio block)
+                int stat = SX_NOT_ENDED;
+                if (cap >= 0 && piv0 + q >= cap)
+                    stat = SX_PIVOT_CAP;
+                else if (!(cmp_eps(dmin, 0.0) < 0))
+                    stat = SX_FEASIBLE;  // solver.cu:88
+                const int ce = c.map(1 + e);
+                double a = 0.0;
+                int elig = 0;
+                double rv = DBL_MAX;
+                int ri = -1;
+                if (stat == SX_NOT_ENDED) {
+                    if (t < q) s_x[t] = ld_sc1(U + (size_t)t * ld + ce);  // pending rows' entering entries
+                    if (live) a = T[(size_t)li * ld + ce];
+                    __syncthreads();
+                    for (int s = 0; s < q; ++s) {
+                        if ((bits >> s) & 1u)
+                            a = a / s_p[s];
+                        else
+                            a = fma(s_hist[s * SX_TILE + t], s_x[s], a);
+                    }
+                    if (live) {
+                        elig = a >= SX_EPS;
+                        const double ratio = cmp_eps(a, 0.0) > 0 ? b / a : DBL_MAX;  // reduction.cu:106-114
+                        if (cmp_eps(ratio, rv) < 0) {
+                            rv = ratio;
+                            ri = li;
+                        }
+                    }
+                    s_a[t] = a;
+                    s_b[t] = b;
+                    const int any = __syncthreads_or(elig);
+                    block_argmin512(rv, ri, s_v, s_i);
+                    if (t == 0) {
+                        TileA *w = tiles_a + blockIdx.x;
+                        const int wl = ri >= 0 ? ri - (int)blockIdx.x * SX_TILE : 0;
+                        st_sc1(&w->v, rv);
+                        st_sc1(&w->a, s_a[wl]);
+                        st_sc1(&w->b, s_b[wl]);
+                        st_sc1(&w->idx, ri);
+                        st_sc1(&w->elig, any);
+                    }
+                }
+                if (arrive_last(&ch->ticket_a, (unsigned)NA, &s_flag)) {
+                    // pass 2 over the tile winners (solver.cu:96-105)
+                    double tv = DBL_MAX;
+                    int ti = -1, te = 0;
+                    if (stat == SX_NOT_ENDED && t < NA) {
+                        const TileA *w = tiles_a + t;
+                        const double cv = ld_sc1(&w->v);
+                        te = ld_sc1(&w->elig);
+                        if (cmp_eps(cv, tv) < 0) {
+                            tv = cv;
+                            ti = ld_sc1(&w->idx);
+                        }
+                        s_a[t] = ld_sc1(&w->a);
+                        s_b[t] = ld_sc1(&w->b);
+                    }
+                    const int anyall = __syncthreads_or(SX_ELIG(te));
+                    if (stat == SX_NOT_ENDED && !anyall) stat = SX_UNBOUNDED;
+                    // the winning tile of row ti: ti / 512 (every tile reports its own rows)
+                    block_argmin512(tv, ti, s_v, s_i);
+                    if (t == 0) {
+                        double p = 0.0, br = 0.0;
+                        if (stat == SX_NOT_ENDED) {
+                            if (ti < 0) {
+                                stat = SX_NUMERIC_FAIL;
+                            } else {
+                                p = s_a[ti / SX_TILE];
+                                br = s_b[ti / SX_TILE];
+                                // write-through: a row can leave twice in one launch, each
+                                // time stored from another CU, and two XCDs' dirty L2 lines
+                                // would reach memory in no defined order
+                                st_sc1(base + ti, e);  // solver.cu:105
+                                st_sc1(&recs[q].r, ti);
+                                st_sc1(&recs[q].e, e);
+                                st_sc1(&recs[q].p, p);
+                                st_sc1(U + (size_t)q * ld, br);  // the pivot row's RHS entry, for the sweep
+                            }
+                        }
+                        const int ncnt = stat == SX_NOT_ENDED ? q + 1 : q;
+                        __hip_atomic_store(&ch->ticket_a, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        st_sc1(&ch->r_p, p);
+                        st_sc1(&ch->r_br, br);
+                        st_sc1(&ch->r_dmin, dmin);
+                        st_sc1(&ch->r_row, ti);
+                        st_sc1(&ch->r_e, e);
+                        st_sc1(&ch->r_status, stat);
+                        st_sc1(&ch->r_cnt, ncnt);
+                        drain();
+                        st_sc1(&ch->r_seq, seq);
+                    }
+                }
+                // the selection (every ratio block, the last arriver included)
+                if (t == 0) {
+                    s_ok = wait_seq(&ch->r_seq, seq, &ch->abort_w);
+                    if (s_ok) {
+                        s_rstatus = ld_sc1(&ch->r_status);
+                        s_rrow = ld_sc1(&ch->r_row);
+                        s_rp = ld_sc1(&ch->r_p);
+                        s_rbr = ld_sc1(&ch->r_br);
+                    }
+                }
+                __syncthreads();
+                if (!s_ok || s_rstatus != SX_NOT_ENDED) break;
+                const int r = s_rrow;
+                const double p = s_rp, br = s_rbr;
+                cnt = q + 1;
+                // this pivot's factor column and the rows' new RHS (solver.cu:34-46, column 0)
+                const double f = -a / p;
+                s_hist[q * SX_TILE + t] = f;
+                if (t == 0) s_p[q] = p;
+                if (live) {
+                    st_sc1(F + (size_t)li * SX_KMAX + q, f);  // read in this launch by the objective blocks
+                    if (li == r) {
+                        b = b / p;
+                        bits |= 1u << q;
+                        const unsigned long long w = PM[li];
+                        PM[li] = (((unsigned)(w >> 32) == B) ? w : ((unsigned long long)B << 32)) | (1ull << q);
+                    } else {
+                        b = fma(f, br, b);
+                    }
+                }
+            }
+        } else {
+            // ---------------------------------------------------------------- objective tile
+            const int tb = blockIdx.x - NA;
+            const int L = c.N - 1;
+            const int ia = tb * SX_TILE + t;  // entry d[1 + ia]
+            const bool live = ia < L;
+            const int mj = c.map(1 + (live ? ia : 0));
+            double dj = live ? d[1 + ia] : 0.0;
+            double d0 = (tb == 0 && t == 0) ? d[0] : 0.0;
+            for (int q = 0; q < K; ++q) {
+                const unsigned long long seq = ((unsigned long long)B << 8) | (unsigned)q;
+                if (t == 0) {
+                    s_ok = wait_seq(&ch->r_seq, seq, &ch->abort_w);
+                    if (s_ok) {
+                        s_rstatus = ld_sc1(&ch->r_status);
+                        s_rrow = ld_sc1(&ch->r_row);
+                        s_rp = ld_sc1(&ch->r_p);
+                        s_rbr = ld_sc1(&ch->r_br);
+                        s_rdmin = ld_sc1(&ch->r_dmin);
+                    }
+                }
+                __syncthreads();
+                if (!s_ok || s_rstatus != SX_NOT_ENDED) break;
+                const int r = s_rrow;
+                const double p = s_rp, br = s_rbr;
+                if (t < q) s_x[t] = ld_sc1(F + (size_t)r * SX_KMAX + t);  // the leaving row's factors
+                double u = live ? T[(size_t)r * ld + mj] : 0.0;
+                __syncthreads();
+                // the leaving row's current value on this column (its pending pivots applied)
+                for (int s = 0; s < q; ++s) {
+                    if (s_r[s] == r)
+                        u = u / s_p[s];
+                    else
+                        u = fma(s_x[s], s_hist[s * SX_TILE + t], u);
+                }
+                s_hist[q * SX_TILE + t] = u;
+                if (t == 0) {
+                    s_p[q] = p;
+                    s_r[q] = r;
+                }
+                if (live && 1 + ia < c.Ns) st_sc1(U + (size_t)q * ld + 1 + ia, u);
+                const double fd = -s_rdmin / p;  // updateCostsVector, solver.cu:48-56
+                if (tb == 0 && t == 0) d0 = fma(fd, br, d0);
+                double v = DBL_MAX;
+                int i = -1;
+                if (live) {
+                    dj = fma(fd, u, dj);
+                    if (cmp_eps(dj, v) < 0) {
+                        v = dj;
+                        i = ia;
+                    }
+                }
+                block_argmin512(v, i, s_v, s_i);  // pass 1 (reduction.cu:51-80)
+                if (t == 0) store_tile_sc1(tiles_b + tb, v, i, 0);
+                if (arrive_last(&ch->ticket_b, (unsigned)NB, &s_flag)) {
+                    // pass 2 over the tile winners, written by other blocks in this launch:
+                    // sc1 loads (a plain load may hit a stale L1 line of an earlier pivot)
+                    double ev = DBL_MAX;
+                    int ei = -1;
+                    if (t < NB) {
+                        double cv;
+                        int ci, cz;
+                        load_tile_sc1(tiles_b + t, cv, ci, cz);
+                        if (cmp_eps(cv, ev) < 0) {
+                            ev = cv;
+                            ei = ci;
+                        }
+                    }
+                    block_argmin512(ev, ei, s_v, s_i);
+                    if (t == 0) {
+                        __hip_atomic_store(&ch->ticket_b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        st_sc1(&ch->e_dmin, ev);
+                        st_sc1(&ch->e_e, ei);
+                        drain();
+                        st_sc1(&ch->e_seq, seq + 1);
+                    }
+                }
+                __syncthreads();
+            }
+            if (live) d[1 + ia] = dj;
+            if (tb == 0 && t == 0) d[0] = d0;
+        }
+    }
+    // leave; the last block out writes the batch's outcome into the state
+    if (arrive_last(&ch->exit_cnt, (unsigned)(NA + NB), &s_flag) && t == 0) {
+        __hip_atomic_store(&ch->exit_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (status0 != SX_NOT_ENDED) return;
+        if (ld_sc1(&ch->abort_w) != 0u) {
+            st->status = SX_HANG;
+            __hip_atomic_store(&ch->abort_w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ch->ticket_a, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ch->ticket_b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        // the last selection record of this batch
+        const int n = ld_sc1(&ch->r_cnt);
+        st->status = ld_sc1(&ch->r_status);
+        st->pivots = piv0 + n;
+        if (n > 0) {
+            st->r = recs[n - 1].r;
+            st->e = recs[n - 1].e;
+            st->batch_tag = B;
+            st->batch_count = n;
+        }
+        if (st->status == SX_NOT_ENDED) {  // the batch ran all K pivots: the next entering variable
+            st->e_next = ld_sc1(&ch->e_e);
+            st->dmin_next = ld_sc1(&ch->e_dmin);
+        }
+    }
+    (void)cnt;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -879,6 +1310,37 @@ void sx_launch_sweep(double *T, int rows, size_t ld, int Ns, const Pending &pd, 
         launch_sweep_k<SX_KMAX>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, pd, st, rev, s);
     else
         SX_FATAL("batch larger than SX_KMAX");
+}
+
+static size_t batch_lds(int k) { return (size_t)k * SX_TILE * sizeof(double); }
+
+bool sx_batch_fits(int rows, Cols c, int k) {
+    if (k < 1 || k > SX_KMAX || rows <= 0) return false;
+    const int NA = (rows + SX_TILE - 1) / SX_TILE, NB = (c.N - 1 + SX_TILE - 1) / SX_TILE;
+    if (NA > SX_TILE || NB > SX_TILE || NB < 1) return false;
+    static int per_cu[SX_KMAX + 1] = {0};
+    static int cus = 0;
+    if (per_cu[k] == 0) {
+        int dev = 0;
+        SX_HIP(hipGetDevice(&dev));
+        SX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        SX_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_batch),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)batch_lds(SX_KMAX)));
+        int n = 0;
+        SX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_batch, SX_TILE, batch_lds(k)));
+        per_cu[k] = n > 0 ? n : -1;
+    }
+    // every block resident at once (one per CU is enough: the hand-offs never wait on a
+    // block that has not started), with a margin of a quarter of the CUs
+    return per_cu[k] > 0 && (long long)(NA + NB) <= (long long)per_cu[k] * cus * 3 / 4;
+}
+
+void sx_launch_batch(const double *T, int rows, size_t ld, Cols c, double *d, int *base, DevState *st,
+                     const Pending &pd, int k, BatchChan *chan, TileA *tiles_a, TilePart *tiles_b, hipStream_t s) {
+    if (!sx_batch_fits(rows, c, k)) SX_FATAL("fused batch grid does not fit the device");
+    const int NA = (rows + SX_TILE - 1) / SX_TILE, NB = (c.N - 1 + SX_TILE - 1) / SX_TILE;
+    k_batch<<<NA + NB, SX_TILE, batch_lds(k), s>>>(T, rows, ld, c, d, base, st, pd.U, pd.F, pd.recs, pd.PM,
+                                                   pd.batch, k, NA, NB, chan, tiles_a, tiles_b);
 }
 
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s) {

@@ -144,9 +144,14 @@ def test_published_pivot_counts_on_gpu(gpu, n, m):
     assert tuple(got.pivots) == (rec["p1_pivots"], rec["p2_pivots"])
 
 
-def test_config2_full_solve_bit_exact(gpu):
+@pytest.mark.parametrize("fused", [-1, 0])
+def test_config2_full_solve_bit_exact(gpu, fused):
     """configs[1]: n=2048, m=1024, seed 205824 -- every bit of the answer vs the oracle."""
-    got, ref = _check_two_phase(sx.generateRandomProblem(2048, 1024, 205824, 1, 100))
+    try:
+        sx.set_fused(fused)
+        got, ref = _check_two_phase(sx.generateRandomProblem(2048, 1024, 205824, 1, 100))
+    finally:
+        sx.set_fused(-1)
     assert tuple(got.pivots) == (2003, 69)
 
 
@@ -201,6 +206,7 @@ def test_session_pivots(gpu):
 def _pivots_with(cfg, T, d, base, k):
     Tg, dg, bg = T.copy(), d.copy(), base.copy()
     setters = {"batch": (sx.set_batch, 0), "rb": (sx.set_update_rows, 0), "sc1": (sx.set_store_sc1, -1),
+               "fused": (sx.set_fused, -1),
                "waves": (sx.set_update_waves, 0), "W": (sx.set_virtual_ranks, 1)}
     try:
         for key, val in cfg.items():
@@ -212,14 +218,16 @@ def _pivots_with(cfg, T, d, base, k):
     return Tg, dg, bg, st, done
 
 
+@pytest.mark.parametrize("fused", [-1, 0])
 @pytest.mark.parametrize("batch", [1, 2, 3, 7, 16, 17, 32])
 @pytest.mark.parametrize("rb", [1, 2, 4])
-def test_batched_sweep_bit_exact(gpu, batch, rb):
+def test_batched_sweep_bit_exact(gpu, batch, rb, fused):
     """k pivots with the tableau swept every `batch` pivots (pending pivots applied on the fly
     to the columns and rows the decisions read): the same bits as the oracle's pivot-by-pivot
-    updates, for every register-slot variant of the sweep and a partial last batch"""
+    updates, for every register-slot variant of the sweep and a partial last batch; each batch
+    as one resident launch (fused) or as two launches per pivot"""
     T, d, base = _phase1_state(333, 1025, 7)
-    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "rb": rb}, T, d, base, 45)
+    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "rb": rb, "fused": fused}, T, d, base, 45)
     oracle.solve(T, d, base, max_pivots=45)
     assert done == 45
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
@@ -236,25 +244,27 @@ def test_sweep_grid_bit_exact(gpu, sc1, waves):
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 
+@pytest.mark.parametrize("fused", [-1, 0])
 @pytest.mark.parametrize("batch", [1, 5, 16])
-def test_batched_phase_end_mid_batch(gpu, batch):
+def test_batched_phase_end_mid_batch(gpu, batch, fused):
     """the phase ends inside a batch: the pivots selected before the end are swept, the rest of
     the batch does nothing"""
     T, d, base = _phase1_state(64, 128, 6528)
-    Tg, dg, bg, st, done = _pivots_with({"batch": batch}, T, d, base, 100000)
+    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "fused": fused}, T, d, base, 100000)
     st_o, done_o = oracle.solve(T, d, base)
     assert st == st_o == oracle.FEASIBLE and done == done_o
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 
+@pytest.mark.parametrize("fused", [-1, 0])
 @pytest.mark.parametrize("batch", [1, 16])
-def test_same_row_leaves_twice_in_a_batch(gpu, batch):
+def test_same_row_leaves_twice_in_a_batch(gpu, batch, fused):
     """a row that is the leaving row of two pivots of one batch (the general path of the sweep:
     x / p for that slot): on this instance the oracle's leaving rows are 7, 6, 1, 7, 7, 7, ..."""
     T, d, base = _phase1_state(20, 10, 2010)
     ref = (T.copy(), d.copy(), base.copy())
     st_o, done_o = oracle.solve(*ref)
-    Tg, dg, bg, st, done = _pivots_with({"batch": batch}, T, d, base, 100000)
+    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "fused": fused}, T, d, base, 100000)
     assert st == st_o and done == done_o
     assert same(Tg, ref[0]) and same(dg, ref[1]) and np.array_equal(bg, ref[2])
 
