@@ -117,6 +117,7 @@ SIGNATURES = {
     "simplex_session_total_pivots": (ctypes.c_longlong, [ctypes.c_void_p]),
     "simplex_session_launch_log": (ctypes.c_longlong, [ctypes.c_void_p, c_ll_p, c_double_p, ctypes.c_longlong]),
     "simplex_session_close": (None, [ctypes.c_void_p]),
+    "simplex_session_stamps": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_ulonglong)]),
     "simplex_dev_argmin": (ctypes.c_longlong, [c_double_p, ctypes.c_longlong, c_double_p]),
     "simplex_dev_pivots": (ctypes.c_int, [c_double_p, ctypes.c_longlong, ctypes.c_longlong, ctypes.c_longlong,
                                           c_double_p, c_int_p, ctypes.c_longlong, c_ll_p]),

@@ -201,6 +201,13 @@ class Session:
                                              _dp(us), n)
         return rows[:n], us[:n]
 
+    def stamps(self, k):
+        """Diagnostic: one fused batch of k pivots with in-kernel timestamps, (k, 8) uint64 in
+        10-ns ticks (see simplex_session_stamps); None when the fused path is not in use."""
+        out = np.zeros((k, 8), dtype=np.uint64)
+        rc = self._lib.simplex_session_stamps(self._h, k, out.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)))
+        return out if rc == 0 else None
+
     def objective(self):
         return self._lib.simplex_session_objective(self._h)
 

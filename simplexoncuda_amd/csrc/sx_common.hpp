@@ -71,35 +71,13 @@ struct Pending {
     int q;                   // slot of the pivot being enqueued (pivots pending before it)
 };
 
-// Hand-off records of the fused batch kernel (k_batch): every field on its own 128-byte
-// line; written with write-through (sc1) stores, read with sc1 loads, each record published
-// by storing its sequence number after the data.
+// Fused batch kernel (k_batch): its exit counter and abort word, each on its own line.
+// (The per-pivot hand-offs are data-tagged granules in two arrays of tile records,
+// sx_batch_granules_a/b() 8-byte words each.)
 struct BatchChan {
-    alignas(128) unsigned long long r_seq;  // selection of pivot q published (seq = batch << 8 | q)
-    alignas(128) double r_p;                // its pivot element
-    double r_br;                            // current RHS of the leaving row
-    double r_dmin;                          // reduced cost of the entering variable
-    int r_row;                              // leaving row (global)
-    int r_e;                                // entering variable
-    int r_status;                           // SX_NOT_ENDED, or the status that ends the phase
-    int r_cnt;                              // pivots selected in this batch so far
-    alignas(128) unsigned long long e_seq;  // entering variable of pivot q published
-    alignas(128) double e_dmin;
-    int e_e;
-    alignas(128) unsigned ticket_a;         // ratio-block arrivals of the current pivot
-    alignas(128) unsigned ticket_b;         // objective-block arrivals of the current pivot
-    alignas(128) unsigned exit_cnt;         // blocks that have left the kernel
-    alignas(128) unsigned abort_w;          // a wait timed out: every block leaves
-};
-
-// ratio-tile winner of the fused kernel: the winning row's ratio, index, entering-column
-// entry (the pivot candidate) and RHS
-struct __attribute__((aligned(32))) TileA {
-    double v;
-    double a;
-    double b;
-    int idx;
-    int elig;
+    alignas(128) unsigned exit_cnt;  // blocks that have left the kernel
+    alignas(128) unsigned abort_w;   // a wait timed out: every block leaves
+    alignas(128) unsigned pad;
 };
 
 #define SX_HANG (-13)  // fused batch kernel: a hand-off wait timed out (never expected)
@@ -148,7 +126,10 @@ void sx_launch_sweep(double *T, int rows, size_t ld, int Ns, const Pending &pd, 
 // grid); returns false (nothing launched) when the grid cannot be resident at once
 bool sx_batch_fits(int rows, Cols c, int k);
 void sx_launch_batch(const double *T, int rows, size_t ld, Cols c, double *d, int *base, DevState *st,
-                     const Pending &pd, int k, BatchChan *chan, TileA *tiles_a, TilePart *tiles_b, hipStream_t s);
+                     const Pending &pd, int k, BatchChan *chan, unsigned long long *ga, unsigned long long *gb,
+                     unsigned long long *stamps, hipStream_t s);
+size_t sx_batch_granules_a();
+size_t sx_batch_granules_b();
 void sx_set_update_waves(float w);  // resident-grid multiple of the sweep (default 1)
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s);
 

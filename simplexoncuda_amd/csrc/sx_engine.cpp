@@ -175,9 +175,9 @@ struct Shard {
     TilePart *enter_parts = nullptr;
     TilePart *tiles_local = nullptr;
     TilePart *tiles_all = nullptr;
-    BatchChan *chan = nullptr;        // fused batch kernel: hand-off records
-    TileA *tiles_a = nullptr;         // fused batch kernel: ratio-tile winners
-    TilePart *tiles_b = nullptr;      // fused batch kernel: objective-tile winners
+    BatchChan *chan = nullptr;        // fused batch kernel: exit counter, abort word
+    unsigned long long *ga = nullptr; // fused batch kernel: ratio-tile records (tagged granules)
+    unsigned long long *gb = nullptr; // fused batch kernel: objective-tile records (tagged granules)
     DevState *st = nullptr;
 };
 
@@ -207,6 +207,7 @@ class Engine {
     // slots inside the current one; every batch ends with a sweep of the tableau
     unsigned batch_id = 1;
     int q_host = 0;
+    unsigned long long *stamps = nullptr;  // diagnostic: in-kernel timestamps of the fused batch
     long long sweeps = 0;
     std::function<void(int)> on_pivot;  // DEBUG trace: called after every pivot (solver.cu:112-116)
 
@@ -306,9 +307,11 @@ class Engine {
         x.base = dalloc<int>(m);
         x.enter_parts = dalloc<TilePart>(SX_TILE);
         x.chan = dalloc<BatchChan>(1);
-        x.tiles_a = dalloc<TileA>(SX_TILE);
-        x.tiles_b = dalloc<TilePart>(SX_TILE);
+        x.ga = dalloc<unsigned long long>(sx_batch_granules_a());
+        x.gb = dalloc<unsigned long long>(sx_batch_granules_b());
         SX_HIP(hipMemsetAsync(x.chan, 0, sizeof(BatchChan), s));
+        SX_HIP(hipMemsetAsync(x.ga, 0, sx_batch_granules_a() * sizeof(unsigned long long), s));
+        SX_HIP(hipMemsetAsync(x.gb, 0, sx_batch_granules_b() * sizeof(unsigned long long), s));
         x.tiles_local = dalloc<TilePart>(slots);
         if (xchg) x.tiles_all = dalloc<TilePart>((size_t)W * slots);
         x.st = dalloc<DevState>(1);
@@ -332,7 +335,7 @@ class Engine {
                         (void *)x.slot_send, (void *)x.slot_all, (void *)x.U, (void *)x.F, (void *)x.recs, (void *)x.PM,
                         (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
                         (void *)x.rhs_all, (void *)x.base, (void *)x.enter_parts, (void *)x.tiles_local, (void *)x.chan,
-                        (void *)x.tiles_a, (void *)x.tiles_b,
+                        (void *)x.ga, (void *)x.gb,
                         (void *)x.tiles_all, (void *)x.st})
             if (p) (void)hipFree(p);
     }
@@ -530,7 +533,7 @@ class Engine {
     void enqueue_batch(int k) {
         Shard &x = sh[0];
         if (q_host != 0) SX_FATAL("fused batch inside a started batch");
-        sx_launch_batch(x.T, x.rows, ld, cols(N), x.d, x.base, x.st, pending(x), k, x.chan, x.tiles_a, x.tiles_b, s);
+        sx_launch_batch(x.T, x.rows, ld, cols(N), x.d, x.base, x.st, pending(x), k, x.chan, x.ga, x.gb, stamps, s);
         q_host = k;
     }
 
@@ -544,8 +547,8 @@ class Engine {
         for (auto &x : sh) sx_launch_sweep(x.T, x.rows, ld, cols(N).Ns, pending(x), x.st, rev, cfg, s);
         if (ev1) SX_HIP(hipEventRecord(ev1, s));
         ++sweeps;
-        ++batch_id;
-        if (batch_id == 0) batch_id = 1;
+        // batch ids tag the fused kernel's granules as (id << 8 | slot) in 32 bits: 24-bit ids, never 0
+        if (++batch_id >= (1u << 24)) batch_id = 1;
         q_host = 0;
     }
 
@@ -1079,6 +1082,22 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
 
 double simplex_session_objective(simplex_session *S) { return S->E->read_d0(); }
 long long simplex_session_total_pivots(simplex_session *S) { return S->E->read_state().pivots; }
+
+int simplex_session_stamps(simplex_session *S, int k, unsigned long long *out) {
+    // one fused batch of k pivots with in-kernel timestamps (diagnostic); out[k][8]
+    Engine &E = *S->E;
+    if (k < 1 || k > SX_KMAX || !E.fused_ok(k)) return -1;
+    unsigned long long *dev = dalloc<unsigned long long>((size_t)k * 8);
+    SX_HIP(hipMemsetAsync(dev, 0, sizeof(unsigned long long) * k * 8, E.s));
+    E.stamps = dev;
+    E.enqueue_batch(k);
+    E.stamps = nullptr;
+    E.enqueue_sweep();
+    SX_HIP(hipMemcpyAsync(out, dev, sizeof(unsigned long long) * k * 8, hipMemcpyDeviceToHost, E.s));
+    SX_HIP(hipStreamSynchronize(E.s));
+    (void)hipFree(dev);
+    return 0;
+}
 
 long long simplex_session_launch_log(simplex_session *S, long long *rows, double *update_us, long long cap) {
     const long long n = (long long)S->log_rows.size();

@@ -638,295 +638,280 @@ __global__ __launch_bounds__(256) void k_pivot_row(const double *__restrict__ T,
 
 // ---------------------------------------------------------------------------------------
 // K6: a whole batch of pivots in ONE resident launch (one shard).  Blocks [0, NA) own the
-// 512-row ratio tiles, blocks [NA, NA + NB) the 512-entry objective-row tiles; each block
-// keeps its slice of the state on chip for the whole batch (the ratio blocks: their rows'
-// current RHS and the factor history F[.][s] in LDS; the objective blocks: their columns'
-// d values in registers and the pivot-row history U[s][.] in LDS).  Per pivot q:
-//   ratio blocks     wait for the entering variable of pivot q, form the current entering
-//                    column of their rows (T[i][e] + pending pivots), the ratio vector and
-//                    the tile winner; the last to arrive runs pass 2 and publishes the
-//                    selection (r, p, b_r), or the status that ends the phase;
-//   objective blocks wait for the selection, form the current pivot row on their columns,
-//                    update d and reduce it per tile; the last to arrive runs pass 2 and
-//                    publishes the entering variable of pivot q + 1.
-// The arithmetic and the argmin trees are those of k_ratio_select / k_pivot_row (reference:
-// solver.cu:78-126, reduction.cu:10-140).  Every hand-off is write-through (sc1) data, an
-// `s_waitcnt vmcnt(0)`, then an sc1 sequence-number store; consumers poll the number with sc1
-// loads and read the data with sc1 loads (MI355X_MICROARCH.md "Valid forms", row 1).  Every
-// wait is bounded: past ~0.2 s the block raises abort_w and all blocks leave (status SX_HANG).
-// The grid is launched only when all its blocks are resident at once (sx_batch_fits).
+// 512-row ratio tiles, blocks [NA, NA + NB) the 512-entry objective-row tiles.  Each block
+// keeps its slice of the state on chip for the whole batch: a ratio block its rows' current
+// RHS and factor history F[.][s] (LDS); an objective block its columns' d values (registers)
+// and pivot-row history U[s][.] (LDS).  Per pivot q:
+//   ratio blocks      form the current entering column of their rows (T[i][e] + pending
+//                     pivots), the ratio vector and the tile winner (reduction.cu:106-140);
+//   every block       reads all ratio-tile winners and runs pass 2 itself (the same tree, so
+//                     the same leaving row r in every block; solver.cu:96-105);
+//   objective blocks  form the current pivot row on their columns, update d and reduce it
+//                     per tile (solver.cu:48-56, reduction.cu:51-80);
+//   every block       reads all objective-tile winners and runs pass 2 itself: the entering
+//                     variable of pivot q + 1.
+// A tile winner is published as data-tagged granules: 8 bytes = {32 data bits, 32-bit tag
+// (batch << 8 | q)}, each a single write-through (sc1) store, so a consumer needs no flag and
+// no ordering between the granules: it polls (sc1 loads) until every granule it needs carries
+// the pivot's tag (MI355X_MICROARCH.md price list: handoff-1to1).  With its winner, a tile
+// also publishes the history the consumer needs of the winning line: the factors F[r][s] of
+// the winning row (ratio tiles) or the pivot-row values U[s][e] of the winning column
+// (objective tiles), so nothing else crosses blocks inside the launch.  Every wait is
+// bounded: past ~0.2 s the block raises abort_w and all blocks leave (status SX_HANG).  The
+// grid is launched only when all its blocks are resident at once (sx_batch_fits).
 
-__device__ __forceinline__ void st_sc1(double *p, double v) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), (unsigned long long)__double_as_longlong(v),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+typedef unsigned long long u64;
+
+__device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ void put_g(u64 *g, unsigned data, unsigned tag) {
+    __hip_atomic_store(g, ((u64)tag << 32) | data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void st_sc1(int *p, int v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void put_gd(u64 *g, double v, unsigned tag) {  // a double: 2 granules
+    const u64 b = (u64)__double_as_longlong(v);
+    put_g(g, (unsigned)b, tag);
+    put_g(g + 1, (unsigned)(b >> 32), tag);
 }
-__device__ __forceinline__ void st_sc1(unsigned long long *p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ double gd(unsigned lo, unsigned hi) {
+    return __longlong_as_double((long long)(((u64)hi << 32) | lo));
 }
-__device__ __forceinline__ double ld_sc1(const double *p) {
-    return __longlong_as_double((long long)__hip_atomic_load(
-        reinterpret_cast<unsigned long long *>(const_cast<double *>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ int ld_sc1(const int *p) {
-    return __hip_atomic_load(const_cast<int *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ u64 ld_sc1(const u64 *p) {
+    return __hip_atomic_load(const_cast<u64 *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ unsigned ld_sc1(const unsigned *p) {
     return __hip_atomic_load(const_cast<unsigned *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long *p) {
-    return __hip_atomic_load(const_cast<unsigned long long *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// one lane polls `seq` until it reads `want`; false if the batch was aborted (or this wait
-// timed out, which aborts it)
-__device__ bool wait_seq(const unsigned long long *seq, unsigned long long want, unsigned *abort_w) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-    for (unsigned it = 0;; ++it) {
-        if (ld_sc1(seq) == want) return true;
-        if ((it & 63) == 63) {
-            if (ld_sc1(abort_w) != 0u) return false;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // 0.2 s
-                __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                return false;
+// Wave 0 reads n granules, granule k at base[off(k)], each until it carries `tag`, into
+// out[k] (LDS).  Block-uniform result: false when the batch was aborted (or this wait timed
+// out, which aborts it).  Every thread of the block must call it.
+template <typename OFF>
+__device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, unsigned *out, unsigned *abort_w,
+                              int *s_ok) {
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        int ok = 1;
+        const u64 t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+        for (int k0 = 0; k0 < n && ok; k0 += 64) {
+            const int k = k0 + lane;
+            bool have = k >= n;
+            unsigned v = 0;
+            for (unsigned it = 0;; ++it) {
+                if (!have) {
+                    const u64 w = ld_sc1(base + off(k));
+                    if ((unsigned)(w >> 32) == tag) {
+                        have = true;
+                        v = (unsigned)w;
+                    }
+                }
+                if (__ballot(!have) == 0ull) break;
+                if ((it & 63) == 63) {
+                    int stop = ld_sc1(abort_w) != 0u;
+                    if (!stop && __builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // 0.2 s
+                        __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        stop = 1;
+                    }
+                    if (__builtin_amdgcn_readfirstlane(stop)) {
+                        ok = 0;
+                        break;
+                    }
+                }
+                __builtin_amdgcn_s_sleep(1);
             }
+            if (ok && k < n) out[k] = v;
         }
-        __builtin_amdgcn_s_sleep(1);
+        if (lane == 0) *s_ok = ok;
     }
+    __syncthreads();
+    return *s_ok != 0;
 }
 
-// arrival at a per-pivot ticket (after every wave of the block drained its stores); true in
-// the last block to arrive, which then owns the ticket until it resets it
-__device__ __forceinline__ bool arrive_last(unsigned *ticket, unsigned n, int *s_flag) {
-    drain();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *s_flag = (t == n - 1);
-    }
-    __syncthreads();
-    return *s_flag != 0;
-}
+// granule layout of one tile record
+#define SX_GA_STRIDE (8 + 2 * SX_KMAX)  // ratio tile: v(2) idx elig a(2) b(2) | F[r][s] (2 per slot)
+#define SX_GB_STRIDE (4 + 2 * SX_KMAX)  // objective tile: v(2) idx pad | U[s][e] (2 per slot)
 
 __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int rows, size_t ld, Cols c,
                                                double *__restrict__ d, int *base, DevState *st, double *U, double *F,
                                                PivRec *recs, unsigned long long *PM, unsigned B, int K, int NA,
-                                               int NB, BatchChan *ch, TileA *tiles_a, TilePart *tiles_b) {
+                                               int NB, BatchChan *ch, u64 *ga, u64 *gb, unsigned long long *stamps) {
     extern __shared__ double s_hist[];  // [K][512]: F history (ratio blocks) / U history (objective blocks)
     __shared__ double s_v[16];
     __shared__ int s_i[16];
-    __shared__ double s_p[SX_KMAX], s_x[SX_KMAX];  // pivots; per-slot U[s][e] (ratio) / F[r][s] (objective)
-    __shared__ int s_r[SX_KMAX];                   // leaving rows (objective blocks)
-    __shared__ double s_a[SX_TILE], s_b[SX_TILE];  // ratio blocks: entering column, RHS (winner lookup)
-    __shared__ int s_flag, s_ok;
-    __shared__ double s_rp, s_rbr, s_rdmin;
-    __shared__ int s_rrow, s_rstatus;
-    __shared__ double s_edmin;
-    __shared__ int s_ee;
+    __shared__ double s_p[SX_KMAX];                  // pivots of the batch
+    __shared__ int s_r[SX_KMAX];                     // leaving rows of the batch
+    __shared__ double s_ue[SX_KMAX], s_fr[SX_KMAX];  // U[s][e] (entering column) / F[r][s] (leaving row)
+    __shared__ double s_a[SX_TILE], s_b[SX_TILE];    // ratio blocks: entering column, RHS (winner lookup)
+    __shared__ unsigned s_g[4 * SX_TILE];            // gathered granules
+    __shared__ int s_ok, s_flag, s_win;
+    __shared__ double s_wv;
     const int t = threadIdx.x;
     const bool isA = (int)blockIdx.x < NA;
-    // state at the start of the batch: nothing writes st during the launch (the last block
-    // to leave writes it)
+    // stamps (diagnostic, normally null): s_memrealtime (100 MHz) at hand-off points of ratio
+    // block 0 and objective block 0, [q][8]
+#define SX_STAMP(k)                                                                           \
+    do {                                                                                       \
+        if (stamps && t == 0) stamps[(size_t)q * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+    // state at the start of the batch (written only by the last block to leave)
     const int status0 = st->status;
     const long long piv0 = st->pivots, cap = st->max_pivots;
-    int cnt = 0;  // pivots selected so far in this batch
+    int e = st->e_next;
+    double dmin = st->dmin_next;
+    int status = SX_NOT_ENDED, cnt = 0, last_r = -1, last_e = -1;
+    bool aborted = false;
     if (status0 == SX_NOT_ENDED) {
-        if (isA) {
-            // ---------------------------------------------------------------- ratio tile
-            const int li = blockIdx.x * SX_TILE + t;
-            const bool live = li < rows;
-            double b = live ? T[(size_t)li * ld] : 0.0;  // current RHS of the row
-            unsigned bits = 0u;                           // slots where this row left the basis
-            int e = st->e_next;
-            double dmin = st->dmin_next;
-            for (int q = 0; q < K; ++q) {
-                const unsigned long long seq = ((unsigned long long)B << 8) | (unsigned)q;
-                if (q > 0) {
-                    if (t == 0) {
-                        s_ok = wait_seq(&ch->e_seq, seq, &ch->abort_w);
-                        if (s_ok) {
-                            s_ee = ld_sc1(&ch->e_e);
-                            s_edmin = ld_sc1(&ch->e_dmin);
-                        }
-                    }
-                    __syncthreads();
-                    if (!s_ok) break;
-                    e = s_ee;
-                    dmin = s_edmin;
+        // ratio block: its row; objective block: its logical column d[1 + ia]
+        const int li = blockIdx.x * SX_TILE + t;
+        const bool liveA = isA && li < rows;
+        const int tb = blockIdx.x - NA;
+        const int L = c.N - 1;
+        const int ia = tb * SX_TILE + t;
+        const bool liveB = !isA && ia < L;
+        const int mj = c.map(1 + (liveB ? ia : 0));
+        double b = liveA ? T[(size_t)li * ld] : 0.0;  // current RHS of the row
+        unsigned bits = 0u;                            // slots where this row left the basis
+        double dj = liveB ? d[1 + ia] : 0.0;
+        double d0 = (!isA && tb == 0 && t == 0) ? d[0] : 0.0;
+        for (int q = 0; q < K; ++q) {
+            const unsigned tag = (B << 8) | (unsigned)q;
+            // ---- does the phase end here?  (the same decision in every block)
+            if (cap >= 0 && piv0 + q >= cap) {
+                status = SX_PIVOT_CAP;
+                break;
+            }
+            if (!(cmp_eps(dmin, 0.0) < 0)) {  // solver.cu:88
+                status = SX_FEASIBLE;
+                break;
+            }
+            const int ce = c.map(1 + e);
+            double a = 0.0;
+            if (isA) {
+                // ---- ratio tile: current entering column, ratios, tile winner
+                if (blockIdx.x == 0) SX_STAMP(0);
+                if (liveA) a = T[(size_t)li * ld + ce];
+                for (int s = 0; s < q; ++s) {
+                    if ((bits >> s) & 1u)
+                        a = a / s_p[s];
+                    else
+                        a = fma(s_hist[s * SX_TILE + t], s_ue[s], a);
                 }
-                // ends the phase? (the same decision in every ratio block)
-                int stat = SX_NOT_ENDED;
-                if (cap >= 0 && piv0 + q >= cap)
-                    stat = SX_PIVOT_CAP;
-                else if (!(cmp_eps(dmin, 0.0) < 0))
-                    stat = SX_FEASIBLE;  // solver.cu:88
-                const int ce = c.map(1 + e);
-                double a = 0.0;
-                int elig = 0;
                 double rv = DBL_MAX;
-                int ri = -1;
-                if (stat == SX_NOT_ENDED) {
-                    if (t < q) s_x[t] = ld_sc1(U + (size_t)t * ld + ce);  // pending rows' entering entries
-                    if (live) a = T[(size_t)li * ld + ce];
-                    __syncthreads();
-                    for (int s = 0; s < q; ++s) {
-                        if ((bits >> s) & 1u)
-                            a = a / s_p[s];
-                        else
-                            a = fma(s_hist[s * SX_TILE + t], s_x[s], a);
-                    }
-                    if (live) {
-                        elig = a >= SX_EPS;
-                        const double ratio = cmp_eps(a, 0.0) > 0 ? b / a : DBL_MAX;  // reduction.cu:106-114
-                        if (cmp_eps(ratio, rv) < 0) {
-                            rv = ratio;
-                            ri = li;
-                        }
-                    }
-                    s_a[t] = a;
-                    s_b[t] = b;
-                    const int any = __syncthreads_or(elig);
-                    block_argmin512(rv, ri, s_v, s_i);
-                    if (t == 0) {
-                        TileA *w = tiles_a + blockIdx.x;
-                        const int wl = ri >= 0 ? ri - (int)blockIdx.x * SX_TILE : 0;
-                        st_sc1(&w->v, rv);
-                        st_sc1(&w->a, s_a[wl]);
-                        st_sc1(&w->b, s_b[wl]);
-                        st_sc1(&w->idx, ri);
-                        st_sc1(&w->elig, any);
+                int ri = -1, elig = 0;
+                if (liveA) {
+                    elig = a >= SX_EPS;
+                    const double ratio = cmp_eps(a, 0.0) > 0 ? b / a : DBL_MAX;  // reduction.cu:106-114
+                    if (cmp_eps(ratio, rv) < 0) {
+                        rv = ratio;
+                        ri = li;
                     }
                 }
-                if (arrive_last(&ch->ticket_a, (unsigned)NA, &s_flag)) {
-                    // pass 2 over the tile winners (solver.cu:96-105)
-                    double tv = DBL_MAX;
-                    int ti = -1, te = 0;
-                    if (stat == SX_NOT_ENDED && t < NA) {
-                        const TileA *w = tiles_a + t;
-                        const double cv = ld_sc1(&w->v);
-                        te = ld_sc1(&w->elig);
-                        if (cmp_eps(cv, tv) < 0) {
-                            tv = cv;
-                            ti = ld_sc1(&w->idx);
-                        }
-                        s_a[t] = ld_sc1(&w->a);
-                        s_b[t] = ld_sc1(&w->b);
-                    }
-                    const int anyall = __syncthreads_or(SX_ELIG(te));
-                    if (stat == SX_NOT_ENDED && !anyall) stat = SX_UNBOUNDED;
-                    // the winning tile of row ti: ti / 512 (every tile reports its own rows)
-                    block_argmin512(tv, ti, s_v, s_i);
-                    if (t == 0) {
-                        double p = 0.0, br = 0.0;
-                        if (stat == SX_NOT_ENDED) {
-                            if (ti < 0) {
-                                stat = SX_NUMERIC_FAIL;
-                            } else {
-                                p = s_a[ti / SX_TILE];
-                                br = s_b[ti / SX_TILE];
-                                // write-through: a row can leave twice in one launch, each
-                                // time stored from another CU, and two XCDs' dirty L2 lines
-                                // would reach memory in no defined order
-                                st_sc1(base + ti, e);  // solver.cu:105
-                                st_sc1(&recs[q].r, ti);
-                                st_sc1(&recs[q].e, e);
-                                st_sc1(&recs[q].p, p);
-                                st_sc1(U + (size_t)q * ld, br);  // the pivot row's RHS entry, for the sweep
-                            }
-                        }
-                        const int ncnt = stat == SX_NOT_ENDED ? q + 1 : q;
-                        __hip_atomic_store(&ch->ticket_a, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        st_sc1(&ch->r_p, p);
-                        st_sc1(&ch->r_br, br);
-                        st_sc1(&ch->r_dmin, dmin);
-                        st_sc1(&ch->r_row, ti);
-                        st_sc1(&ch->r_e, e);
-                        st_sc1(&ch->r_status, stat);
-                        st_sc1(&ch->r_cnt, ncnt);
-                        drain();
-                        st_sc1(&ch->r_seq, seq);
-                    }
-                }
-                // the selection (every ratio block, the last arriver included)
+                s_a[t] = a;
+                s_b[t] = b;
+                const int any = __syncthreads_or(elig);
+                block_argmin512(rv, ri, s_v, s_i);
                 if (t == 0) {
-                    s_ok = wait_seq(&ch->r_seq, seq, &ch->abort_w);
-                    if (s_ok) {
-                        s_rstatus = ld_sc1(&ch->r_status);
-                        s_rrow = ld_sc1(&ch->r_row);
-                        s_rp = ld_sc1(&ch->r_p);
-                        s_rbr = ld_sc1(&ch->r_br);
-                    }
+                    s_win = ri >= 0 ? ri - (int)blockIdx.x * SX_TILE : 0;
+                    s_wv = rv;
                 }
                 __syncthreads();
-                if (!s_ok || s_rstatus != SX_NOT_ENDED) break;
-                const int r = s_rrow;
-                const double p = s_rp, br = s_rbr;
-                cnt = q + 1;
-                // this pivot's factor column and the rows' new RHS (solver.cu:34-46, column 0)
+                u64 *g = ga + (size_t)blockIdx.x * SX_GA_STRIDE;
+                const int wl = s_win;
+                if (t == 0) {
+                    put_gd(g, s_wv, tag);
+                    put_g(g + 2, (unsigned)(ri), tag);
+                    put_g(g + 3, (unsigned)any, tag);
+                    put_gd(g + 4, s_a[wl], tag);
+                    put_gd(g + 6, s_b[wl], tag);
+                } else if (t - 1 < q) {
+                    put_gd(g + 8 + 2 * (t - 1), s_hist[(t - 1) * SX_TILE + wl], tag);  // F[winner][s]
+                }
+                if (blockIdx.x == 0) SX_STAMP(1);
+            }
+            // ---- selection: every block runs pass 2 over the ratio-tile winners
+            if (!gather_tagged(ga, 4 * NA, [](int k) { return (k >> 2) * SX_GA_STRIDE + (k & 3); }, tag, s_g,
+                               &ch->abort_w, &s_ok)) {
+                aborted = true;
+                break;
+            }
+            if (!isA && tb == 0) SX_STAMP(3);
+            double tv = DBL_MAX;
+            int ti = -1, te = 0;
+            if (t < NA) {
+                const double cv = gd(s_g[4 * t], s_g[4 * t + 1]);
+                te = (int)s_g[4 * t + 3];
+                if (cmp_eps(cv, tv) < 0) {
+                    tv = cv;
+                    ti = (int)s_g[4 * t + 2];
+                }
+            }
+            const int anyall = __syncthreads_or(SX_ELIG(te));
+            block_argmin512(tv, ti, s_v, s_i);
+            if (t == 0) s_win = ti;
+            __syncthreads();
+            const int r = s_win;
+            if (!anyall) {  // solver.cu:96-102
+                status = SX_UNBOUNDED;
+                break;
+            }
+            if (r < 0) {
+                status = SX_NUMERIC_FAIL;
+                break;
+            }
+            // the objective blocks' pivot-row load does not wait for the winner's details
+            double u = liveB ? T[(size_t)r * ld + mj] : 0.0;
+            const int wt = r / SX_TILE;
+            if (!gather_tagged(ga + (size_t)wt * SX_GA_STRIDE + 4, 4 + 2 * q, [](int k) { return k; }, tag, s_g,
+                               &ch->abort_w, &s_ok)) {
+                aborted = true;
+                break;
+            }
+            const double p = gd(s_g[0], s_g[1]), br = gd(s_g[2], s_g[3]);
+            if (t < q) s_fr[t] = gd(s_g[4 + 2 * t], s_g[5 + 2 * t]);
+            if (t == 0) {
+                s_p[q] = p;
+                s_r[q] = r;
+            }
+            cnt = q + 1;
+            last_r = r;
+            last_e = e;
+            __syncthreads();
+            if (isA) {
+                // ---- this pivot's factor column and the rows' new RHS (solver.cu:34-46)
                 const double f = -a / p;
                 s_hist[q * SX_TILE + t] = f;
-                if (t == 0) s_p[q] = p;
-                if (live) {
-                    st_sc1(F + (size_t)li * SX_KMAX + q, f);  // read in this launch by the objective blocks
+                if (liveA) {
+                    F[(size_t)li * SX_KMAX + q] = f;
                     if (li == r) {
                         b = b / p;
                         bits |= 1u << q;
-                        const unsigned long long w = PM[li];
-                        PM[li] = (((unsigned)(w >> 32) == B) ? w : ((unsigned long long)B << 32)) | (1ull << q);
+                        const u64 w = PM[li];
+                        PM[li] = (((unsigned)(w >> 32) == B) ? w : ((u64)B << 32)) | (1ull << q);
                     } else {
                         b = fma(f, br, b);
                     }
                 }
-            }
-        } else {
-            // ---------------------------------------------------------------- objective tile
-            const int tb = blockIdx.x - NA;
-            const int L = c.N - 1;
-            const int ia = tb * SX_TILE + t;  // entry d[1 + ia]
-            const bool live = ia < L;
-            const int mj = c.map(1 + (live ? ia : 0));
-            double dj = live ? d[1 + ia] : 0.0;
-            double d0 = (tb == 0 && t == 0) ? d[0] : 0.0;
-            for (int q = 0; q < K; ++q) {
-                const unsigned long long seq = ((unsigned long long)B << 8) | (unsigned)q;
-                if (t == 0) {
-                    s_ok = wait_seq(&ch->r_seq, seq, &ch->abort_w);
-                    if (s_ok) {
-                        s_rstatus = ld_sc1(&ch->r_status);
-                        s_rrow = ld_sc1(&ch->r_row);
-                        s_rp = ld_sc1(&ch->r_p);
-                        s_rbr = ld_sc1(&ch->r_br);
-                        s_rdmin = ld_sc1(&ch->r_dmin);
-                    }
+                if (blockIdx.x == 0 && t == 0) {
+                    base[r] = e;  // solver.cu:105 (one writer per launch: this thread)
+                    recs[q].r = r;
+                    recs[q].e = e;
+                    recs[q].p = p;
+                    U[(size_t)q * ld] = br;  // the pivot row's RHS entry, for the sweep
                 }
-                __syncthreads();
-                if (!s_ok || s_rstatus != SX_NOT_ENDED) break;
-                const int r = s_rrow;
-                const double p = s_rp, br = s_rbr;
-                if (t < q) s_x[t] = ld_sc1(F + (size_t)r * SX_KMAX + t);  // the leaving row's factors
-                double u = live ? T[(size_t)r * ld + mj] : 0.0;
-                __syncthreads();
-                // the leaving row's current value on this column (its pending pivots applied)
+            } else {
+                // ---- objective tile: current pivot row on this column, d, tile winner
                 for (int s = 0; s < q; ++s) {
                     if (s_r[s] == r)
                         u = u / s_p[s];
                     else
-                        u = fma(s_x[s], s_hist[s * SX_TILE + t], u);
+                        u = fma(s_fr[s], s_hist[s * SX_TILE + t], u);
                 }
                 s_hist[q * SX_TILE + t] = u;
-                if (t == 0) {
-                    s_p[q] = p;
-                    s_r[q] = r;
-                }
-                if (live && 1 + ia < c.Ns) st_sc1(U + (size_t)q * ld + 1 + ia, u);
-                const double fd = -s_rdmin / p;  // updateCostsVector, solver.cu:48-56
+                if (liveB && 1 + ia < c.Ns) U[(size_t)q * ld + 1 + ia] = u;
+                const double fd = -dmin / p;  // updateCostsVector, solver.cu:48-56
                 if (tb == 0 && t == 0) d0 = fma(fd, br, d0);
                 double v = DBL_MAX;
                 int i = -1;
-                if (live) {
+                if (liveB) {
                     dj = fma(fd, u, dj);
                     if (cmp_eps(dj, v) < 0) {
                         v = dj;
@@ -934,64 +919,88 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                     }
                 }
                 block_argmin512(v, i, s_v, s_i);  // pass 1 (reduction.cu:51-80)
-                if (t == 0) store_tile_sc1(tiles_b + tb, v, i, 0);
-                if (arrive_last(&ch->ticket_b, (unsigned)NB, &s_flag)) {
-                    // pass 2 over the tile winners, written by other blocks in this launch:
-                    // sc1 loads (a plain load may hit a stale L1 line of an earlier pivot)
-                    double ev = DBL_MAX;
-                    int ei = -1;
-                    if (t < NB) {
-                        double cv;
-                        int ci, cz;
-                        load_tile_sc1(tiles_b + t, cv, ci, cz);
-                        if (cmp_eps(cv, ev) < 0) {
-                            ev = cv;
-                            ei = ci;
-                        }
-                    }
-                    block_argmin512(ev, ei, s_v, s_i);
-                    if (t == 0) {
-                        __hip_atomic_store(&ch->ticket_b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        st_sc1(&ch->e_dmin, ev);
-                        st_sc1(&ch->e_e, ei);
-                        drain();
-                        st_sc1(&ch->e_seq, seq + 1);
-                    }
+                if (t == 0) {
+                    s_win = i >= 0 ? i - tb * SX_TILE : 0;
+                    s_wv = v;
+                    s_flag = i;
                 }
                 __syncthreads();
+                u64 *g = gb + (size_t)tb * SX_GB_STRIDE;
+                if (t == 0) {
+                    put_gd(g, s_wv, tag);
+                    put_g(g + 2, (unsigned)s_flag, tag);
+                } else if (t - 1 <= q) {
+                    put_gd(g + 4 + 2 * (t - 1), s_hist[(t - 1) * SX_TILE + s_win], tag);  // U[s][winner]
+                }
+                if (tb == 0) SX_STAMP(4);
             }
-            if (live) d[1 + ia] = dj;
-            if (tb == 0 && t == 0) d[0] = d0;
+            // ---- entering variable of pivot q + 1: every block runs pass 2 over the objective tiles
+            if (!gather_tagged(gb, 3 * NB, [](int k) { return (k / 3) * SX_GB_STRIDE + (k % 3); }, tag, s_g,
+                               &ch->abort_w, &s_ok)) {
+                aborted = true;
+                break;
+            }
+            double ev = DBL_MAX;
+            int ei = -1;
+            if (t < NB) {
+                const double cv = gd(s_g[3 * t], s_g[3 * t + 1]);
+                if (cmp_eps(cv, ev) < 0) {
+                    ev = cv;
+                    ei = (int)s_g[3 * t + 2];
+                }
+            }
+            block_argmin512(ev, ei, s_v, s_i);
+            if (t == 0) {
+                s_win = ei;
+                s_wv = ev;
+            }
+            __syncthreads();
+            e = s_win;
+            dmin = s_wv;
+            if (isA && blockIdx.x == 0) SX_STAMP(5);
+            // the ratio blocks need the pending pivot rows' entries in the new entering column
+            if (isA && q + 1 < K && e >= 0 && cmp_eps(dmin, 0.0) < 0) {
+                if (!gather_tagged(gb + (size_t)(e / SX_TILE) * SX_GB_STRIDE + 4, 2 * (q + 1), [](int k) { return k; },
+                                   tag, s_g, &ch->abort_w, &s_ok)) {
+                    aborted = true;
+                    break;
+                }
+                if (t <= q) s_ue[t] = gd(s_g[2 * t], s_g[2 * t + 1]);
+                __syncthreads();
+            }
+        }
+        if (liveB) d[1 + ia] = dj;
+        if (!isA && tb == 0 && t == 0) d[0] = d0;
+    }
+    // leave; the last block out writes the batch's outcome into the state (every block holds
+    // the same outcome)
+    drain();
+    __syncthreads();
+    if (t == 0) {
+        const unsigned k = __hip_atomic_fetch_add(&ch->exit_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == (unsigned)(NA + NB) - 1) {
+            __hip_atomic_store(&ch->exit_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (status0 != SX_NOT_ENDED) return;
+            if (ld_sc1(&ch->abort_w) != 0u || aborted) {
+                st->status = SX_HANG;
+                __hip_atomic_store(&ch->abort_w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return;
+            }
+            st->status = status;
+            st->pivots = piv0 + cnt;
+            if (cnt > 0) {
+                st->r = last_r;
+                st->e = last_e;
+                st->batch_tag = B;
+                st->batch_count = cnt;
+            }
+            st->e_next = e;
+            st->dmin_next = dmin;
         }
     }
-    // leave; the last block out writes the batch's outcome into the state
-    if (arrive_last(&ch->exit_cnt, (unsigned)(NA + NB), &s_flag) && t == 0) {
-        __hip_atomic_store(&ch->exit_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (status0 != SX_NOT_ENDED) return;
-        if (ld_sc1(&ch->abort_w) != 0u) {
-            st->status = SX_HANG;
-            __hip_atomic_store(&ch->abort_w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ch->ticket_a, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ch->ticket_b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-        // the last selection record of this batch
-        const int n = ld_sc1(&ch->r_cnt);
-        st->status = ld_sc1(&ch->r_status);
-        st->pivots = piv0 + n;
-        if (n > 0) {
-            st->r = recs[n - 1].r;
-            st->e = recs[n - 1].e;
-            st->batch_tag = B;
-            st->batch_count = n;
-        }
-        if (st->status == SX_NOT_ENDED) {  // the batch ran all K pivots: the next entering variable
-            st->e_next = ld_sc1(&ch->e_e);
-            st->dmin_next = ld_sc1(&ch->e_dmin);
-        }
-    }
-    (void)cnt;
+#undef SX_STAMP
 }
+
 
 // ---------------------------------------------------------------------------------------
 // K5: the sweep -- the batch's pivots applied to every stored element of the shard
@@ -1314,6 +1323,9 @@ void sx_launch_sweep(double *T, int rows, size_t ld, int Ns, const Pending &pd, 
 
 static size_t batch_lds(int k) { return (size_t)k * SX_TILE * sizeof(double); }
 
+size_t sx_batch_granules_a() { return (size_t)SX_TILE * SX_GA_STRIDE; }
+size_t sx_batch_granules_b() { return (size_t)SX_TILE * SX_GB_STRIDE; }
+
 bool sx_batch_fits(int rows, Cols c, int k) {
     if (k < 1 || k > SX_KMAX || rows <= 0) return false;
     const int NA = (rows + SX_TILE - 1) / SX_TILE, NB = (c.N - 1 + SX_TILE - 1) / SX_TILE;
@@ -1336,11 +1348,12 @@ bool sx_batch_fits(int rows, Cols c, int k) {
 }
 
 void sx_launch_batch(const double *T, int rows, size_t ld, Cols c, double *d, int *base, DevState *st,
-                     const Pending &pd, int k, BatchChan *chan, TileA *tiles_a, TilePart *tiles_b, hipStream_t s) {
+                     const Pending &pd, int k, BatchChan *chan, unsigned long long *ga, unsigned long long *gb,
+                     unsigned long long *stamps, hipStream_t s) {
     if (!sx_batch_fits(rows, c, k)) SX_FATAL("fused batch grid does not fit the device");
     const int NA = (rows + SX_TILE - 1) / SX_TILE, NB = (c.N - 1 + SX_TILE - 1) / SX_TILE;
     k_batch<<<NA + NB, SX_TILE, batch_lds(k), s>>>(T, rows, ld, c, d, base, st, pd.U, pd.F, pd.recs, pd.PM,
-                                                   pd.batch, k, NA, NB, chan, tiles_a, tiles_b);
+                                                   pd.batch, k, NA, NB, chan, ga, gb, stamps);
 }
 
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s) {
