@@ -4,7 +4,7 @@ Workload (BASELINE.json configs[2], the config the roofline target is quoted on)
 generateRandomProblem(n=8192, m=4096, seed=823296, [1,100]) -- the reference's own -t
 instance (main.cu:56-64) -- phase-1 tableau 4096 x 16385 fp64 (537 MB) resident in HBM.
 A "step" is one simplex pivot (entering argmin, ratio test, pivot row, objective row, and
-the rank-1 update of the whole tableau -- applied in sweeps of 16 pivots).
+the rank-1 update of the whole tableau -- applied in sweeps of 32 pivots).
 W untimed pivots, then K timed pivots: by default pivots 50..8950 of the instance's 8981
 phase-1 pivots, i.e. the whole phase at its real mix of sparse and dense pivots.
 
@@ -99,7 +99,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=50, help="untimed pivots before timing")
     ap.add_argument("--config", default="config3", choices=sorted(CONFIGS))
     ap.add_argument("--update-rows", type=int, default=0, help="rows per sweep step (0 = auto)")
-    ap.add_argument("--batch", type=int, default=0, help="pivots per tableau sweep (0 = library default, 16)")
+    ap.add_argument("--batch", type=int, default=0, help="pivots per tableau sweep (0 = library default, 32)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--update-events", type=int, default=1,
                     help="bracket every k-th sweep launch with HIP events (0 = none)")

@@ -26,7 +26,7 @@ void simplex_set_verbose(int on);            /* reference progress lines on stdo
 void simplex_set_update_rows(int rb);        /* rows per sweep step: 1, 2, 4; 0 = auto */
 void simplex_set_snake(int mode);            /* kept for ABI compatibility: sweeps always alternate direction */
 void simplex_set_store_sc1(int mode);        /* write-through tableau stores: -1 auto, 0, 1 */
-/* pivots per tableau sweep (1..32, default 16): the pivots of a batch are selected on the
+/* pivots per tableau sweep (1..32, default 32): the pivots of a batch are selected on the
  * current values (pending pivots applied on the fly) and then applied to the tableau in one
  * sweep -- the same IEEE operations in the same order as one sweep per pivot */
 void simplex_set_batch(int pivots);

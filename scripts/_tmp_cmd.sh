@@ -1,6 +1,3 @@
 set -u
 cd $GRAFT_REPO_ROOT
-timeout -k 10 900 python -m pytest tests/test_gpu_parity.py -m gpu -q -x -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 200 python tools/batch_stamps.py > gpurun_out/stamps.log 2>&1 || exit 1; cat gpurun_out/stamps.log
-timeout -k 10 300 python bench.py --no-cpu-baseline --secondary= > gpurun_out/b.log 2>&1 || exit 1
-python3 -c "import json; r=json.loads(open('gpurun_out/b.log').read().strip().splitlines()[-1]); print(round(r['value']), r['roofline']['frac'], r['roofline']['avg_launch_us'], r['roofline']['sweep_share_of_time'])"
+SWEEP_BATCH=32 SWEEP_RB=1,2,4 SWEEP_SC1=0,1 SWEEP_LDS=0,1 timeout -k 10 300 python tools/sweep_update.py config3 128 3 > gpurun_out/sweep.log 2>&1; cat gpurun_out/sweep.log

@@ -34,14 +34,15 @@ def main():
     stats = {}
     with open(os.path.join(prof, "kt", "run_kernel_stats.csv")) as f:
         for r in csv.DictReader(f):
-            if sub in r["Name"]:
+            # the instantiation of the kernel with the most launches
+            if sub in r["Name"] and int(r["Calls"]) > stats.get("calls", 0):
                 stats = {"name": r["Name"], "calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                          "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
     fetch = per_kernel(os.path.join(prof, "FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(prof, "WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE")
     res = {"kernel_trace": stats}
     for k in fetch:
-        if sub in k and k in write:
+        if k == stats.get("name") and k in write:
             fs = sum(fetch[k]) / len(fetch[k])
             ws = sum(write[k]) / len(write[k])
             res.update({"pmc_kernel": k, "launches": len(fetch[k]), "FETCH_SIZE_KB_avg": fs, "WRITE_SIZE_KB_avg": ws,

@@ -2,7 +2,8 @@
 pivot-path kernel (mean / median / p10 / p90, microseconds), the gaps between consecutive
 ones, and the device time per pivot.
 
-usage: python scripts/chain_stats.py <run_kernel_trace.csv>"""
+usage: python scripts/chain_stats.py <run_kernel_trace.csv> [pivots]   (pivots: the count the
+trace covers, for the per-pivot figure when whole batches run in one launch)"""
 import collections
 import csv
 import sys
@@ -36,9 +37,9 @@ def main():
     for k, v in gap.items():
         v = np.array(v) / 1e3
         print(f"gap {k:24s} n={len(v):6d} mean {v.mean():6.2f} us")
-    npiv = len(dur.get("pivot_row", dur.get("batch", [1])))
+    npiv = int(sys.argv[2]) if len(sys.argv) > 2 else len(dur.get("pivot_row", dur.get("batch", [1])))
     tot = (int(seq[-1]["End_Timestamp"]) - int(seq[0]["Start_Timestamp"])) / 1e3
-    print(f"device time {tot:.1f} us over {npiv} pivot-row launches: {tot / max(npiv, 1):.2f} us per pivot")
+    print(f"device time {tot:.1f} us over {npiv} pivots: {tot / max(npiv, 1):.2f} us per pivot")
 
 
 if __name__ == "__main__":

@@ -316,5 +316,5 @@ def set_store_sc1(mode):
 
 
 def set_batch(p):
-    """Pivots per tableau sweep (1..32; <= 0: default 16)."""
+    """Pivots per tableau sweep (1..32; <= 0: default 32)."""
     _lib.load().simplex_set_batch(int(p))

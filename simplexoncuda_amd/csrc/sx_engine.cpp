@@ -55,7 +55,7 @@ struct Config {
     int update_rows = 0;  // 0: auto (by tableau size)
     int snake = -1;       // -1: auto, 0: off, 1: on
     int sc1 = -1;         // write-through tableau stores: -1 auto, 0, 1
-    int batch = 16;          // pivots per tableau sweep (deferred updates), 1..SX_KMAX
+    int batch = 32;          // pivots per tableau sweep (deferred updates), 1..SX_KMAX
     int device = -1;
     int virtual_ranks = 1;
     int force_exchange = 0;  // run the multi-shard exchange path even with one shard
@@ -464,14 +464,15 @@ class Engine {
 
     // ---------------------------------------------------------------- one pivot
     SweepCfg sweep_cfg(int batch) const {
-        // Measured in the real pivot loop (tools/sweep_update.py on MI355X): write-through
-        // (sc1) stores pay once the shard exceeds the 256 MB Infinity Cache.
+        // Measured in the real pivot loop (tools/sweep_update.py on MI355X, config 3):
+        // write-through (sc1) stores pay once the shard exceeds the 256 MB Infinity Cache;
+        // 4 rows per step at 32 pivots per sweep (138 us), 2 rows at 16 (127 us).
         double bytes = 0.0;
         for (auto &x : sh) bytes = std::max(bytes, 8.0 * (double)x.rows * (double)cols(N).Ns);
         const bool big = bytes > 256.0 * 1024 * 1024;
         SweepCfg c;
         c.batch = batch;
-        c.rows_per_block = g_cfg.update_rows > 0 ? std::min(g_cfg.update_rows, 4) : 2;
+        c.rows_per_block = g_cfg.update_rows > 0 ? std::min(g_cfg.update_rows, 4) : (batch > 16 ? 4 : 2);
         c.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : (big ? 1 : 0);
         return c;
     }
@@ -841,7 +842,7 @@ void simplex_set_verbose(int on) { g_cfg.verbose = on; }
 void simplex_set_update_rows(int rb) { g_cfg.update_rows = (rb == 1 || rb == 2 || rb == 4 || rb == 8) ? rb : 0; }
 void simplex_set_snake(int mode) { g_cfg.snake = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_store_sc1(int mode) { g_cfg.sc1 = mode < 0 ? -1 : (mode ? 1 : 0); }
-void simplex_set_batch(int pivots) { g_cfg.batch = pivots > 0 ? std::min(pivots, SX_KMAX) : 16; }
+void simplex_set_batch(int pivots) { g_cfg.batch = pivots > 0 ? std::min(pivots, SX_KMAX) : 32; }
 void simplex_set_device(int device) {
     g_cfg.device = device;
     if (device >= 0) SX_HIP(hipSetDevice(device));

@@ -1051,16 +1051,26 @@ __global__ __launch_bounds__(256) void k_sweep(double *__restrict__ T, int rows,
         for (int k = 0; k < RB; ++k) {
             const int i = i0 + k;
             if (i >= rows) break;
+            // the row's factors: unconditional (wave-uniform, scalar) loads issued together --
+            // F rows hold SX_KMAX allocated doubles; slots >= cnt are loaded but not used
             const double *Fr = F + (size_t)i * SX_KMAX;
+            double f[KT];
+#pragma unroll
+            for (int s = 0; s < KT; ++s) f[s] = Fr[s];
             const unsigned bits = pend_bits(PM, i, B, mask);
             double2 y = x[k];
-            if (bits == 0u) {
+            if (bits == 0u && cnt == KT) {  // a full batch, no leaving row: no per-slot branch
+#pragma unroll
+                for (int s = 0; s < KT; ++s) {
+                    y.x = fma(f[s], u[s].x, y.x);
+                    y.y = fma(f[s], u[s].y, y.y);
+                }
+            } else if (bits == 0u) {
 #pragma unroll
                 for (int s = 0; s < KT; ++s) {
                     if (s < cnt) {
-                        const double f = Fr[s];
-                        y.x = fma(f, u[s].x, y.x);
-                        y.y = fma(f, u[s].y, y.y);
+                        y.x = fma(f[s], u[s].x, y.x);
+                        y.y = fma(f[s], u[s].y, y.y);
                     }
                 }
             } else {
@@ -1072,9 +1082,8 @@ __global__ __launch_bounds__(256) void k_sweep(double *__restrict__ T, int rows,
                             y.x = y.x / p;
                             y.y = y.y / p;
                         } else {
-                            const double f = Fr[s];
-                            y.x = fma(f, u[s].x, y.x);
-                            y.y = fma(f, u[s].y, y.y);
+                            y.x = fma(f[s], u[s].x, y.x);
+                            y.y = fma(f[s], u[s].y, y.y);
                         }
                     }
                 }

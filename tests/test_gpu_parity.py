@@ -189,14 +189,14 @@ def test_session_pivots(gpu):
     p = sx.generateRandomProblem(2048, 1024, 205824, 1, 100)
     s = sx.Session(p)
     t = s.pivots(50, time_updates=True)
-    # 50 pivots = 3 full batches of 16 + one of 2, each ending with a sweep
-    assert t.pivots == 50 and t.status == sx.NOT_ENDED and t.update_launches == 4 and t.swept_pivots == 50
+    # 50 pivots = one full batch of 32 + one of 18, each ending with a sweep
+    assert t.pivots == 50 and t.status == sx.NOT_ENDED and t.update_launches == 2 and t.swept_pivots == 50
     assert t.update_ms > 0 and t.wall_ms >= t.update_ms
     assert t.stored_width == 1 + 2048 + 1024 and t.width == 1 + 2048 + 2 * 1024
     assert t.update_bytes == 16.0 * 1024 * t.stored_width
-    assert t.swept_bytes == 4 * t.update_bytes
+    assert t.swept_bytes == 2 * t.update_bytes
     applied, us = s.launch_log()
-    assert list(applied) == [16, 16, 16, 2] and (us > 0).all()
+    assert list(applied) == [32, 18] and (us > 0).all()
     t2 = s.pivots(10000, time_updates=1)
     assert s.total_pivots() == 2003 and t2.status == sx.FEASIBLE
     assert t2.swept_pivots == 2003 - 50  # no-op sweeps after the phase ended are not counted
@@ -230,6 +230,19 @@ def test_batched_sweep_bit_exact(gpu, batch, rb, fused):
     Tg, dg, bg, st, done = _pivots_with({"batch": batch, "rb": rb, "fused": fused}, T, d, base, 45)
     oracle.solve(T, d, base, max_pivots=45)
     assert done == 45
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+@pytest.mark.parametrize("batch", [20, 32])
+@pytest.mark.parametrize("rb", [1, 2, 4])
+@pytest.mark.parametrize("sc1", [0, 1])
+def test_large_batch_sweeps_bit_exact(gpu, batch, rb, sc1):
+    """batches above 16 pivots (32 register slots per column in the sweep), every row step and
+    store flavour, with a partial last batch"""
+    T, d, base = _phase1_state(333, 1025, 7)
+    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "rb": rb, "sc1": sc1}, T, d, base, 70)
+    oracle.solve(T, d, base, max_pivots=70)
+    assert done == 70
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 
