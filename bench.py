@@ -189,6 +189,8 @@ def main():
             "workload": f"{args.config}: phase-1 pivots, {m}x{N1} fp64 tableau (m={m}, n={n})",
             "m": m, "n": n, "seed": seed, "tableau_width": tim.width, "stored_width": tim.stored_width,
             "rows_per_gpu_rank0": tim.local_rows, "parallelism": f"row-block x{world}",
+            "exchange": ("none (one shard)" if world == 1 else
+                         "peer-memory fused batch (xGMI)" if sx.p2p_ready() else "per-pivot RCCL collectives"),
             "pivots_timed": pivots, "status_after": tim.status, "setup_s": r["setup_s"],
         },
         "roofline": {

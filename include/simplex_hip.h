@@ -56,6 +56,13 @@ void simplex_set_alias(int on);
  * handing off through write-through records) instead of two launches per pivot;
  * -1 auto (default: when the grid fits the device), 0 off */
 void simplex_set_fused(int mode);
+/* several shards: run each batch as ONE launch per rank whose ranks hand off through peer
+ * memory (xGMI; virtual shards: the same device) instead of per-pivot RCCL calls; -1 auto
+ * (default: RCCL ranks when the start-up self-check in simplex_dist_init passed), 0 off,
+ * 1 force (virtual shards: only with 1, and W <= 3, so all W launches can run at once) */
+void simplex_set_p2p(int mode);
+/* 1 when the peer-memory fused path passed simplex_dist_init's self-check on every rank */
+int simplex_p2p_ready(void);
 /* the sweep's grid: waves x (blocks resident on the device) blocks (default 1; <= 0 resets) */
 void simplex_set_update_waves(double waves);
 

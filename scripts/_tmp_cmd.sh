@@ -1,3 +1,4 @@
 set -u
 cd $GRAFT_REPO_ROOT
-SWEEP_BATCH=32 SWEEP_RB=1,2,4 SWEEP_SC1=0,1 SWEEP_LDS=0,1 timeout -k 10 300 python tools/sweep_update.py config3 128 3 > gpurun_out/sweep.log 2>&1; cat gpurun_out/sweep.log
+timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -m gpu -q -x -p no:cacheprovider -k "p2p" > gpurun_out/pytest_p2p.log 2>&1; rc=$?; tail -15 gpurun_out/pytest_p2p.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_gpu.log; exit $rc

@@ -97,6 +97,8 @@ SIGNATURES = {
     "simplex_set_exchange_mode": (None, [ctypes.c_int]),
     "simplex_set_alias": (None, [ctypes.c_int]),
     "simplex_set_fused": (None, [ctypes.c_int]),
+    "simplex_set_p2p": (None, [ctypes.c_int]),
+    "simplex_p2p_ready": (ctypes.c_int, []),
     "simplex_set_update_waves": (None, [ctypes.c_double]),
     "twoPhaseMethodEx": (ctypes.c_int, [P_PROBLEM, c_double_p, c_double_p, c_int_p, c_ll_p, ctypes.c_longlong]),
     "simplex_problem_from_arrays": (P_PROBLEM, [ctypes.c_int, ctypes.c_int, c_double_p, c_double_p, c_double_p]),

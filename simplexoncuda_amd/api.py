@@ -294,6 +294,16 @@ def set_fused(mode):
     _lib.load().simplex_set_fused(int(mode))
 
 
+def set_p2p(mode):
+    """Several shards: fused batches exchanging over peer memory (-1 auto, 0 off, 1 force)."""
+    _lib.load().simplex_set_p2p(int(mode))
+
+
+def p2p_ready():
+    """True when the peer-memory path passed the multi-GPU start-up self-check."""
+    return bool(_lib.load().simplex_p2p_ready())
+
+
 def set_update_waves(w):
     """Blocks of the tableau sweep as a multiple of the device's resident capacity (<= 0: default)."""
     _lib.load().simplex_set_update_waves(float(w))

@@ -80,6 +80,18 @@ struct BatchChan {
     alignas(128) unsigned pad;
 };
 
+// Multi-rank fused batch (k_batch_mr): every rank's buffers as seen from this rank (peer
+// memory over xGMI, or the other virtual shards on one GPU).
+#define SX_MAXW 8
+struct PeerView {
+    const double *T[SX_MAXW];        // tableaux (read: the leaving row)
+    unsigned long long *ga[SX_MAXW]; // ratio-tile records (written)
+    unsigned long long *gb[SX_MAXW]; // objective-tile records (written)
+    unsigned long long *gdone[SX_MAXW];  // batch-end done granules (written)
+    double *U[SX_MAXW];              // pending pivot rows (written)
+    double *d[SX_MAXW];              // objective rows (written)
+};
+
 #define SX_HANG (-13)  // fused batch kernel: a hand-off wait timed out (never expected)
 
 // Error convention of the reference (error.cu:5-12): print "<msg> in <file> at line <n>"
@@ -130,6 +142,13 @@ void sx_launch_batch(const double *T, int rows, size_t ld, Cols c, double *d, in
                      unsigned long long *stamps, hipStream_t s);
 size_t sx_batch_granules_a();
 size_t sx_batch_granules_b();
+// the multi-rank fused batch: `grids` co-resident launches of this shape must fit the device
+bool sx_batch_mr_fits(int slots, int nb_local, int k, int grids);
+void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld, Cols c, double *d, int *base,
+                        DevState *st, const Pending &pd, int k, int slots, int W, int rank, int tb0, int tb1,
+                        BatchChan *chan, const unsigned long long *ga, const unsigned long long *gb,
+                        const unsigned long long *gdone, const PeerView &pv, unsigned long long timeout,
+                        hipStream_t s);
 void sx_set_update_waves(float w);  // resident-grid multiple of the sweep (default 1)
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s);
 

@@ -63,6 +63,8 @@ struct Config {
     int exchange_mode = 0;   // 0 auto, 1 tile allgather + row allreduce, 2 row-gather
     int alias = 1;           // store phase-1 artificial columns as their slack columns
     int fused = -1;          // whole batches in one resident launch: -1 auto (one shard), 0 off
+    int p2p = -1;            // several shards: fused batches exchanging over peer memory: -1 auto, 0 off, 1 force
+    bool p2p_ready = false;  // RCCL ranks: the peer-memory path passed the start-up self-check
     int debug = -1;          // -1: from SIMPLEX_DEBUG; 1: print the tableau after every step
     bool benchmark = false;
     // distributed
@@ -178,6 +180,9 @@ struct Shard {
     BatchChan *chan = nullptr;        // fused batch kernel: exit counter, abort word
     unsigned long long *ga = nullptr; // fused batch kernel: ratio-tile records (tagged granules)
     unsigned long long *gb = nullptr; // fused batch kernel: objective-tile records (tagged granules)
+    unsigned long long *gdone = nullptr;  // multi-rank fused batch: batch-end done granules (one per rank)
+    hipStream_t ss = nullptr;         // virtual shards: the stream its multi-rank fused batch runs on
+    bool uncached = false;            // ga / gb / gdone allocated uncached (polled across devices / XCDs)
     DevState *st = nullptr;
 };
 
@@ -261,10 +266,122 @@ class Engine {
         }
         SX_HIP(hipHostMalloc(reinterpret_cast<void **>(&st_host), 2 * sizeof(DevState), hipHostMallocDefault));
         for (auto &e : poll_ev) SX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        setup_peers();
+    }
+
+    // ---------------------------------------------------------------- peer memory (multi-rank fused batch)
+    PeerView pv;
+    bool p2p = false;
+    hipEvent_t ev_fork = nullptr;
+    std::vector<hipEvent_t> ev_join;
+    std::vector<void *> opened;  // peer allocations mapped through IPC
+
+    void setup_peers() {
+        std::memset(&pv, 0, sizeof(pv));
+        if (!xchg || W > SX_MAXW || g_cfg.p2p == 0) return;
+        if (rccl && !(g_cfg.p2p == 1 || g_cfg.p2p_ready)) return;
+        SX_HIP(hipStreamSynchronize(s));
+        // virtual shards need their W launches to run at once on one device: only when asked for
+        // (a test hook), and for W <= 3 (the engine stream + W streams on 4 hardware queues)
+        if (!rccl && (g_cfg.p2p != 1 || W > 3)) return;
+        if (!rccl) {  // virtual shards: every shard's buffers on this device; one stream per shard
+            for (auto &x : sh) {
+                pv.T[x.rank] = x.T;
+                pv.ga[x.rank] = x.ga;
+                pv.gb[x.rank] = x.gb;
+                pv.gdone[x.rank] = x.gdone;
+                pv.U[x.rank] = x.U;
+                pv.d[x.rank] = x.d;
+                SX_HIP(hipStreamCreateWithFlags(&x.ss, hipStreamNonBlocking));
+                hipEvent_t e;
+                SX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                ev_join.push_back(e);
+            }
+            SX_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+            p2p = true;
+            return;
+        }
+        // one shard per process: exchange IPC handles of the six buffers over RCCL, map the peers'
+        struct Handles {
+            hipIpcMemHandle_t h[6];
+        };
+        // (a failure here is not fatal: every rank learns whether all mapped, and they all fall
+        // back to the RCCL exchange together)
+        Shard &x = sh[0];
+        Handles mine;
+        std::memset(&mine, 0, sizeof(mine));
+        void *bufs[6] = {x.T, x.ga, x.gb, x.gdone, x.U, x.d};
+        int ok = 1;
+        for (int k = 0; k < 6; ++k) ok &= hipIpcGetMemHandle(&mine.h[k], bufs[k]) == hipSuccess;
+        unsigned char *dev = dalloc<unsigned char>(sizeof(Handles) * W);
+        SX_HIP(hipMemcpy(dev + sizeof(Handles) * g_cfg.rank, &mine, sizeof(Handles), hipMemcpyHostToDevice));
+        SX_NCCL(ncclAllGather(dev + sizeof(Handles) * g_cfg.rank, dev, sizeof(Handles), ncclUint8, g_cfg.comm, s));
+        std::vector<Handles> all(W);
+        SX_HIP(hipMemcpyAsync(all.data(), dev, sizeof(Handles) * W, hipMemcpyDeviceToHost, s));
+        SX_HIP(hipStreamSynchronize(s));
+        (void)hipFree(dev);
+        std::vector<void *> mapped((size_t)W * 6, nullptr);
+        for (int r = 0; r < W && ok; ++r)
+            for (int k = 0; k < 6 && ok; ++k) {
+                if (r == g_cfg.rank) {
+                    mapped[(size_t)r * 6 + k] = bufs[k];
+                } else if (hipIpcOpenMemHandle(&mapped[(size_t)r * 6 + k], all[r].h[k],
+                                               hipIpcMemLazyEnablePeerAccess) == hipSuccess) {
+                    opened.push_back(mapped[(size_t)r * 6 + k]);
+                } else {
+                    ok = 0;
+                }
+            }
+        (void)hipGetLastError();
+        if (!all_ranks(ok)) {
+            for (void *p : opened) (void)hipIpcCloseMemHandle(p);
+            opened.clear();
+            if (g_cfg.verbose) say("peer memory unavailable: per-pivot RCCL exchange");
+            return;
+        }
+        for (int r = 0; r < W; ++r) {
+            void *const *p = &mapped[(size_t)r * 6];
+            pv.T[r] = static_cast<const double *>(p[0]);
+            pv.ga[r] = static_cast<unsigned long long *>(p[1]);
+            pv.gb[r] = static_cast<unsigned long long *>(p[2]);
+            pv.gdone[r] = static_cast<unsigned long long *>(p[3]);
+            pv.U[r] = static_cast<double *>(p[4]);
+            pv.d[r] = static_cast<double *>(p[5]);
+        }
+        p2p = true;
+    }
+
+    // 1 on every rank iff `ok` on every rank (an RCCL min-allreduce; RCCL ranks only)
+    bool all_ranks(int ok) {
+        int *dv = dalloc<int>(1);
+        SX_HIP(hipMemcpy(dv, &ok, sizeof(int), hipMemcpyHostToDevice));
+        SX_NCCL(ncclAllReduce(dv, dv, 1, ncclInt, ncclMin, g_cfg.comm, s));
+        int r = 0;
+        SX_HIP(hipMemcpyAsync(&r, dv, sizeof(int), hipMemcpyDeviceToHost, s));
+        SX_HIP(hipStreamSynchronize(s));
+        (void)hipFree(dv);
+        return r != 0;
+    }
+
+    void close_peers() {
+        if (opened.empty()) return;
+        for (void *p : opened) (void)hipIpcCloseMemHandle(p);
+        opened.clear();
+        // every rank has unmapped before any rank frees what the others mapped
+        int *one = dalloc<int>(1);
+        SX_NCCL(ncclAllReduce(one, one, 1, ncclInt, ncclSum, g_cfg.comm, s));
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(one);
     }
 
     ~Engine() {
         (void)hipStreamSynchronize(s);
+        close_peers();
+        for (auto &x : sh)
+            if (x.ss) (void)hipStreamDestroy(x.ss);
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        for (auto &e : ev_join)
+            if (e) (void)hipEventDestroy(e);
         for (auto &x : sh) free_shard(x);
         if (sum_srcs) (void)hipFree(sum_srcs);
         if (c_dev) (void)hipFree(c_dev);
@@ -307,8 +424,19 @@ class Engine {
         x.base = dalloc<int>(m);
         x.enter_parts = dalloc<TilePart>(SX_TILE);
         x.chan = dalloc<BatchChan>(1);
-        x.ga = dalloc<unsigned long long>(sx_batch_granules_a());
-        x.gb = dalloc<unsigned long long>(sx_batch_granules_b());
+        if (xchg) {
+            // polled by other ranks' writers: uncached (no stale line in any L2)
+            x.uncached = true;
+            SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&x.ga), sx_batch_granules_a() * 8,
+                                         hipDeviceMallocUncached));
+            SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&x.gb), sx_batch_granules_b() * 8,
+                                         hipDeviceMallocUncached));
+            SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&x.gdone), SX_MAXW * 8, hipDeviceMallocUncached));
+            SX_HIP(hipMemsetAsync(x.gdone, 0, SX_MAXW * 8, s));
+        } else {
+            x.ga = dalloc<unsigned long long>(sx_batch_granules_a());
+            x.gb = dalloc<unsigned long long>(sx_batch_granules_b());
+        }
         SX_HIP(hipMemsetAsync(x.chan, 0, sizeof(BatchChan), s));
         SX_HIP(hipMemsetAsync(x.ga, 0, sx_batch_granules_a() * sizeof(unsigned long long), s));
         SX_HIP(hipMemsetAsync(x.gb, 0, sx_batch_granules_b() * sizeof(unsigned long long), s));
@@ -335,7 +463,7 @@ class Engine {
                         (void *)x.slot_send, (void *)x.slot_all, (void *)x.U, (void *)x.F, (void *)x.recs, (void *)x.PM,
                         (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
                         (void *)x.rhs_all, (void *)x.base, (void *)x.enter_parts, (void *)x.tiles_local, (void *)x.chan,
-                        (void *)x.ga, (void *)x.gb,
+                        (void *)x.ga, (void *)x.gb, (void *)x.gdone,
                         (void *)x.tiles_all, (void *)x.st})
             if (p) (void)hipFree(p);
     }
@@ -527,14 +655,41 @@ class Engine {
 
     // a whole batch of up to k pivots in one resident launch (one shard, no exchange)
     bool fused_ok(int k) const {
-        if (g_cfg.fused == 0 || xchg || sh.size() != 1 || on_pivot) return false;
-        return sx_batch_fits(sh[0].rows, cols(N), k);
+        if (g_cfg.fused == 0 || on_pivot) return false;
+        if (!xchg) return sh.size() == 1 && sx_batch_fits(sh[0].rows, cols(N), k);
+        if (!p2p) return false;
+        const int NBg = (N - 1 + SX_TILE - 1) / SX_TILE;
+        const int nbl = (NBg + W - 1) / W;
+        return sx_batch_mr_fits(slots, nbl, k, rccl ? 1 : W);
     }
 
     void enqueue_batch(int k) {
-        Shard &x = sh[0];
         if (q_host != 0) SX_FATAL("fused batch inside a started batch");
-        sx_launch_batch(x.T, x.rows, ld, cols(N), x.d, x.base, x.st, pending(x), k, x.chan, x.ga, x.gb, stamps, s);
+        if (!xchg) {
+            Shard &x = sh[0];
+            sx_launch_batch(x.T, x.rows, ld, cols(N), x.d, x.base, x.st, pending(x), k, x.chan, x.ga, x.gb, stamps,
+                            s);
+        } else {
+            // every rank's batch runs at once (virtual shards: one stream each, forked from and
+            // joined back into the engine stream); the ranks hand off through peer memory
+            const int NBg = (N - 1 + SX_TILE - 1) / SX_TILE;
+            const unsigned long long timeout = rccl ? 200000000ull : 100000000ull;  // 2 s / 1 s at 100 MHz
+            if (!rccl) SX_HIP(hipEventRecord(ev_fork, s));
+            for (size_t i = 0; i < sh.size(); ++i) {
+                Shard &x = sh[i];
+                hipStream_t xs = s;
+                if (!rccl) {
+                    xs = x.ss;
+                    SX_HIP(hipStreamWaitEvent(xs, ev_fork, 0));
+                }
+                const int tb0 = (int)((long long)x.rank * NBg / W), tb1 = (int)((long long)(x.rank + 1) * NBg / W);
+                sx_launch_batch_mr(x.T, x.rows, x.row0, rpr, ld, cols(N), x.d, x.base, x.st, pending(x), k, slots, W,
+                                   x.rank, tb0, tb1, x.chan, x.ga, x.gb, x.gdone, pv, timeout, xs);
+                if (!rccl) SX_HIP(hipEventRecord(ev_join[i], xs));
+            }
+            if (!rccl)
+                for (auto &e : ev_join) SX_HIP(hipStreamWaitEvent(s, e, 0));
+        }
         q_host = k;
     }
 
@@ -851,6 +1006,8 @@ void simplex_set_virtual_ranks(int world) { g_cfg.virtual_ranks = world > 1 ? wo
 void simplex_set_force_exchange(int on) { g_cfg.force_exchange = on ? 1 : 0; }
 void simplex_set_alias(int on) { g_cfg.alias = on ? 1 : 0; }
 void simplex_set_fused(int mode) { g_cfg.fused = mode < 0 ? -1 : (mode ? 1 : 0); }
+void simplex_set_p2p(int mode) { g_cfg.p2p = mode < 0 ? -1 : (mode ? 1 : 0); }
+int simplex_p2p_ready(void) { return g_cfg.p2p_ready ? 1 : 0; }
 void simplex_set_update_waves(double waves) { sx_set_update_waves((float)waves); }
 void simplex_set_exchange_mode(int mode) { g_cfg.exchange_mode = (mode >= 0 && mode <= 2) ? mode : 0; }
 void simplex_set_timer_dir(const char *dir) { g_cfg.timer_dir = dir ? dir : ""; }
@@ -867,6 +1024,39 @@ int simplex_dist_get_unique_id(unsigned char *out) {
     return 0;
 }
 
+// The multi-rank fused batch runs over peer memory; before trusting it on this machine, solve
+// a small instance with it and with the per-pivot RCCL exchange: it is used only when every
+// rank gets bit-identical answers from both.
+static void p2p_selftest() {
+    g_cfg.p2p_ready = false;
+    if (g_cfg.world > SX_MAXW || g_cfg.p2p == 0) return;
+    problem_t *P = generateRandomProblem(300, 1100, 41100, 1, 100);
+    const int n = P->vars, m = P->constraints;
+    std::vector<double> xa(n), xb(n);
+    std::vector<int> ba(m), bb(m);
+    long long pa[2] = {0, 0}, pb[2] = {0, 0};
+    double za = 0.0, zb = 0.0;
+    const int save = g_cfg.p2p;
+    g_cfg.p2p = 1;
+    const int sa = two_phase(P, xa.data(), &za, ba.data(), pa, -1);
+    g_cfg.p2p = 0;
+    const int sb = two_phase(P, xb.data(), &zb, bb.data(), pb, -1);
+    g_cfg.p2p = save;
+    int ok = sa == sb && sa != SX_HANG && pa[0] == pb[0] && pa[1] == pb[1] && std::memcmp(&za, &zb, sizeof(za)) == 0 &&
+             ba == bb && std::memcmp(xa.data(), xb.data(), sizeof(double) * n) == 0;
+    freeProblem(P);
+    free(P);
+    int *dv = nullptr;
+    SX_HIP(hipMalloc(reinterpret_cast<void **>(&dv), sizeof(int)));
+    SX_HIP(hipMemcpy(dv, &ok, sizeof(int), hipMemcpyHostToDevice));
+    SX_NCCL(ncclAllReduce(dv, dv, 1, ncclInt, ncclMin, g_cfg.comm, nullptr));
+    SX_HIP(hipMemcpy(&ok, dv, sizeof(int), hipMemcpyDeviceToHost));
+    (void)hipFree(dv);
+    g_cfg.p2p_ready = ok != 0;
+    if (!ok && g_cfg.rank == 0)
+        fprintf(stderr, "simplex: peer-memory fused batches disagree with the RCCL exchange; using RCCL\n");
+}
+
 int simplex_dist_init(int rank, int world, const unsigned char *unique_id, int device) {
     std::lock_guard<std::mutex> lk(g_mu);
     if (device >= 0) {
@@ -880,6 +1070,7 @@ int simplex_dist_init(int rank, int world, const unsigned char *unique_id, int d
         std::memcpy(&id, unique_id, sizeof(id));
         SX_NCCL(ncclCommInitRank(&g_cfg.comm, world, id, rank));
         g_cfg.dist = true;
+        if (world > 1) p2p_selftest();
     }
     return 0;
 }

@@ -685,9 +685,13 @@ __device__ __forceinline__ unsigned ld_sc1(const unsigned *p) {
 // Wave 0 reads n granules, granule k at base[off(k)], each until it carries `tag`, into
 // out[k] (LDS).  Block-uniform result: false when the batch was aborted (or this wait timed
 // out, which aborts it).  Every thread of the block must call it.
-template <typename OFF>
+__device__ __forceinline__ u64 ld_sys(const u64 *p) {
+    return __hip_atomic_load(const_cast<u64 *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <typename OFF, bool SYS = false>
 __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, unsigned *out, unsigned *abort_w,
-                              int *s_ok) {
+                              int *s_ok, unsigned long long timeout = 20000000ull) {
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         int ok = 1;
@@ -698,7 +702,7 @@ __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, uns
             unsigned v = 0;
             for (unsigned it = 0;; ++it) {
                 if (!have) {
-                    const u64 w = ld_sc1(base + off(k));
+                    const u64 w = SYS ? ld_sys(base + off(k)) : ld_sc1(base + off(k));
                     if ((unsigned)(w >> 32) == tag) {
                         have = true;
                         v = (unsigned)w;
@@ -707,7 +711,7 @@ __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, uns
                 if (__ballot(!have) == 0ull) break;
                 if ((it & 63) == 63) {
                     int stop = ld_sc1(abort_w) != 0u;
-                    if (!stop && __builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // 0.2 s
+                    if (!stop && __builtin_amdgcn_s_memrealtime() - t0 > timeout) {  // 100 MHz ticks
                         __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         stop = 1;
                     }
@@ -1001,6 +1005,320 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
 #undef SX_STAMP
 }
 
+
+// ---------------------------------------------------------------------------------------
+// K7: the fused batch on W row-block shards (one per GPU, or virtual shards on one GPU),
+// exchanging over peer memory (xGMI) inside the launch instead of RCCL calls between
+// launches.  Rank k runs `slots` ratio tiles (its rows) and the objective tiles [tb0, tb1)
+// of the logical row (the objective work is split across ranks; every rank still gets every
+// decision).  Per pivot q:
+//   ratio tiles       as k_batch; each tile winner (+ the winning row's factor history) is
+//                     written as tagged granules into EVERY rank's ga[global tile];
+//   every block       reads all W * slots ratio tiles from its own ga and runs pass 2;
+//   objective tiles   read the leaving row's stored values straight from its owner's
+//                     tableau (remote loads), form the current pivot row on their columns,
+//                     write it into every rank's U[q] (the sweep's input), update their d,
+//                     and publish the tile winner (+ the winning column's pivot-row history)
+//                     into every rank's gb;
+//   every block       reads all objective tiles from its own gb and runs pass 2.
+// At the end of the batch the d slices go to every rank, then a done granule per rank: a
+// rank's last block leaves only when every rank's data has landed, so the sweep that follows
+// reads complete U and d.  Cross-rank stores and loads are system-scope (sc0 sc1); the polled
+// arrays are uncached allocations.  The same arithmetic, trees and order as k_batch.
+__device__ __forceinline__ void put_g_sys(u64 *g, unsigned data, unsigned tag) {
+    __hip_atomic_store(g, ((u64)tag << 32) | data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void put_gd_sys(u64 *g, double v, unsigned tag) {
+    const u64 b = (u64)__double_as_longlong(v);
+    put_g_sys(g, (unsigned)b, tag);
+    put_g_sys(g + 1, (unsigned)(b >> 32), tag);
+}
+__device__ __forceinline__ void st_sys(double *p, double v) {
+    __hip_atomic_store(reinterpret_cast<u64 *>(p), (u64)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ double ld_sys(const double *p) {
+    return __longlong_as_double((long long)ld_sys(reinterpret_cast<const u64 *>(p)));
+}
+
+__global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, int rows, int row0, int rpr, size_t ld,
+                                                  Cols c, double *__restrict__ d, int *base, DevState *st, double *U,
+                                                  double *F, PivRec *recs, unsigned long long *PM, unsigned B, int K,
+                                                  int slots, int W, int rank, int tb0, int tb1, int NBg,
+                                                  BatchChan *ch, const u64 *ga, const u64 *gb, const u64 *gdone,
+                                                  PeerView pv, unsigned long long timeout) {
+    extern __shared__ double s_hist[];  // [K][512]: F history (ratio tiles) / U history (objective tiles)
+    __shared__ double s_v[16];
+    __shared__ int s_i[16];
+    __shared__ double s_p[SX_KMAX];
+    __shared__ int s_r[SX_KMAX];
+    __shared__ double s_ue[SX_KMAX], s_fr[SX_KMAX];
+    __shared__ double s_a[SX_TILE], s_b[SX_TILE];
+    __shared__ unsigned s_g[4 * SX_TILE];
+    __shared__ int s_ok, s_flag, s_win;
+    __shared__ double s_wv;
+    const int t = threadIdx.x;
+    const bool isA = (int)blockIdx.x < slots;
+    const int NAg = W * slots;
+    const int status0 = st->status;
+    const long long piv0 = st->pivots, cap = st->max_pivots;
+    int e = st->e_next;
+    double dmin = st->dmin_next;
+    int status = SX_NOT_ENDED, cnt = 0, last_r = -1, last_e = -1;
+    bool aborted = false;
+    auto gather_a = [](int k) { return (k >> 2) * SX_GA_STRIDE + (k & 3); };
+    auto gather_b = [](int k) { return (k / 3) * SX_GB_STRIDE + (k % 3); };
+    auto ident = [](int k) { return k; };
+    const int li = blockIdx.x * SX_TILE + t;
+    const bool liveA = isA && li < rows;
+    const int gt = rank * slots + (int)blockIdx.x;  // global ratio tile of this block
+    const int tb = tb0 + (int)blockIdx.x - slots;   // objective tile of this block
+    const int L = c.N - 1;
+    const int ia = tb * SX_TILE + t;
+    const bool liveB = !isA && ia < L;
+    const int mj = c.map(1 + (liveB ? ia : 0));
+    double dj = liveB ? d[1 + ia] : 0.0;
+    double d0 = (!isA && tb == 0 && t == 0) ? d[0] : 0.0;
+    if (status0 == SX_NOT_ENDED) {
+        double b = liveA ? T[(size_t)li * ld] : 0.0;
+        unsigned bits = 0u;
+        for (int q = 0; q < K; ++q) {
+            const unsigned tag = (B << 8) | (unsigned)q;
+            if (cap >= 0 && piv0 + q >= cap) {
+                status = SX_PIVOT_CAP;
+                break;
+            }
+            if (!(cmp_eps(dmin, 0.0) < 0)) {  // solver.cu:88
+                status = SX_FEASIBLE;
+                break;
+            }
+            const int ce = c.map(1 + e);
+            double a = 0.0;
+            if (isA) {
+                if (liveA) a = T[(size_t)li * ld + ce];
+                for (int s = 0; s < q; ++s) {
+                    if ((bits >> s) & 1u)
+                        a = a / s_p[s];
+                    else
+                        a = fma(s_hist[s * SX_TILE + t], s_ue[s], a);
+                }
+                double rv = DBL_MAX;
+                int ri = -1, elig = 0;
+                if (liveA) {
+                    elig = a >= SX_EPS;
+                    const double ratio = cmp_eps(a, 0.0) > 0 ? b / a : DBL_MAX;  // reduction.cu:106-114
+                    if (cmp_eps(ratio, rv) < 0) {
+                        rv = ratio;
+                        ri = row0 + li;
+                    }
+                }
+                s_a[t] = a;
+                s_b[t] = b;
+                const int any = __syncthreads_or(elig);
+                block_argmin512(rv, ri, s_v, s_i);
+                if (t == 0) {
+                    s_win = ri >= 0 ? ri - row0 - (int)blockIdx.x * SX_TILE : 0;
+                    s_wv = rv;
+                    s_flag = ri;
+                }
+                __syncthreads();
+                const int wl = s_win;
+                for (int k = 0; k < W; ++k) {
+                    u64 *g = pv.ga[k] + (size_t)gt * SX_GA_STRIDE;
+                    if (t == 0) {
+                        put_gd_sys(g, s_wv, tag);
+                        put_g_sys(g + 2, (unsigned)s_flag, tag);
+                        put_g_sys(g + 3, (unsigned)any, tag);
+                        put_gd_sys(g + 4, s_a[wl], tag);
+                        put_gd_sys(g + 6, s_b[wl], tag);
+                    } else if (t - 1 < q) {
+                        put_gd_sys(g + 8 + 2 * (t - 1), s_hist[(t - 1) * SX_TILE + wl], tag);
+                    }
+                }
+            }
+            // ---- selection: pass 2 over every rank's ratio tiles
+            if (!gather_tagged<decltype(gather_a), true>(ga, 4 * NAg, gather_a, tag, s_g, &ch->abort_w, &s_ok,
+                                                         timeout)) {
+                aborted = true;
+                break;
+            }
+            double tv = DBL_MAX;
+            int ti = -1, te = 0;
+            if (t < NAg) {
+                const double cv = gd(s_g[4 * t], s_g[4 * t + 1]);
+                te = (int)s_g[4 * t + 3];
+                if (cmp_eps(cv, tv) < 0) {
+                    tv = cv;
+                    ti = (int)s_g[4 * t + 2];
+                }
+            }
+            const int anyall = __syncthreads_or(SX_ELIG(te));
+            block_argmin512(tv, ti, s_v, s_i);
+            if (t == 0) s_win = ti;
+            __syncthreads();
+            const int r = s_win;
+            if (!anyall) {  // solver.cu:96-102
+                status = SX_UNBOUNDED;
+                break;
+            }
+            if (r < 0) {
+                status = SX_NUMERIC_FAIL;
+                break;
+            }
+            // the leaving row's stored values, from its owner's tableau (read-only in this launch)
+            const int owner = r / rpr;
+            double u = 0.0;
+            if (liveB) {
+                const double *src = pv.T[owner] + (size_t)(r - owner * rpr) * ld + mj;
+                u = owner == rank ? *src : ld_sys(src);
+            }
+            if (!gather_tagged<decltype(ident), true>(ga + (size_t)(r / SX_TILE) * SX_GA_STRIDE + 4, 4 + 2 * q, ident,
+                                                      tag, s_g, &ch->abort_w, &s_ok, timeout)) {
+                aborted = true;
+                break;
+            }
+            const double p = gd(s_g[0], s_g[1]), br = gd(s_g[2], s_g[3]);
+            if (t < q) s_fr[t] = gd(s_g[4 + 2 * t], s_g[5 + 2 * t]);
+            if (t == 0) {
+                s_p[q] = p;
+                s_r[q] = r;
+            }
+            cnt = q + 1;
+            last_r = r;
+            last_e = e;
+            __syncthreads();
+            if (isA) {
+                const double f = -a / p;
+                s_hist[q * SX_TILE + t] = f;
+                if (liveA) {
+                    F[(size_t)li * SX_KMAX + q] = f;
+                    if (row0 + li == r) {
+                        b = b / p;
+                        bits |= 1u << q;
+                        const u64 w = PM[li];
+                        PM[li] = (((unsigned)(w >> 32) == B) ? w : ((u64)B << 32)) | (1ull << q);
+                    } else {
+                        b = fma(f, br, b);
+                    }
+                }
+                if (blockIdx.x == 0 && t == 0) {  // every rank keeps the whole basis and the records
+                    base[r] = e;                  // solver.cu:105
+                    recs[q].r = r;
+                    recs[q].e = e;
+                    recs[q].p = p;
+                    U[(size_t)q * ld] = br;
+                }
+            } else {
+                for (int s = 0; s < q; ++s) {
+                    if (s_r[s] == r)
+                        u = u / s_p[s];
+                    else
+                        u = fma(s_fr[s], s_hist[s * SX_TILE + t], u);
+                }
+                s_hist[q * SX_TILE + t] = u;
+                if (liveB && 1 + ia < c.Ns)
+                    for (int k = 0; k < W; ++k) st_sys(pv.U[k] + (size_t)q * ld + 1 + ia, u);
+                const double fd = -dmin / p;  // updateCostsVector, solver.cu:48-56
+                if (tb == 0 && t == 0) d0 = fma(fd, br, d0);
+                double v = DBL_MAX;
+                int i = -1;
+                if (liveB) {
+                    dj = fma(fd, u, dj);
+                    if (cmp_eps(dj, v) < 0) {
+                        v = dj;
+                        i = ia;
+                    }
+                }
+                block_argmin512(v, i, s_v, s_i);
+                if (t == 0) {
+                    s_win = i >= 0 ? i - tb * SX_TILE : 0;
+                    s_wv = v;
+                    s_flag = i;
+                }
+                __syncthreads();
+                for (int k = 0; k < W; ++k) {
+                    u64 *g = pv.gb[k] + (size_t)tb * SX_GB_STRIDE;
+                    if (t == 0) {
+                        put_gd_sys(g, s_wv, tag);
+                        put_g_sys(g + 2, (unsigned)s_flag, tag);
+                    } else if (t - 1 <= q) {
+                        put_gd_sys(g + 4 + 2 * (t - 1), s_hist[(t - 1) * SX_TILE + s_win], tag);
+                    }
+                }
+            }
+            // ---- entering variable of pivot q + 1: pass 2 over every objective tile
+            if (!gather_tagged<decltype(gather_b), true>(gb, 3 * NBg, gather_b, tag, s_g, &ch->abort_w, &s_ok,
+                                                         timeout)) {
+                aborted = true;
+                break;
+            }
+            double ev = DBL_MAX;
+            int ei = -1;
+            if (t < NBg) {
+                const double cv = gd(s_g[3 * t], s_g[3 * t + 1]);
+                if (cmp_eps(cv, ev) < 0) {
+                    ev = cv;
+                    ei = (int)s_g[3 * t + 2];
+                }
+            }
+            block_argmin512(ev, ei, s_v, s_i);
+            if (t == 0) {
+                s_win = ei;
+                s_wv = ev;
+            }
+            __syncthreads();
+            e = s_win;
+            dmin = s_wv;
+            if (isA && q + 1 < K && e >= 0 && cmp_eps(dmin, 0.0) < 0) {
+                if (!gather_tagged<decltype(ident), true>(gb + (size_t)(e / SX_TILE) * SX_GB_STRIDE + 4, 2 * (q + 1),
+                                                          ident, tag, s_g, &ch->abort_w, &s_ok, timeout)) {
+                    aborted = true;
+                    break;
+                }
+                if (t <= q) s_ue[t] = gd(s_g[2 * t], s_g[2 * t + 1]);
+                __syncthreads();
+            }
+        }
+    }
+    // every rank's d slices to every rank (each rank keeps the whole objective row between batches)
+    if (liveB)
+        for (int k = 0; k < W; ++k) st_sys(pv.d[k] + 1 + ia, dj);
+    if (!isA && tb == 0 && t == 0)
+        for (int k = 0; k < W; ++k) st_sys(pv.d[k], d0);
+    // leave: the last block of this rank tells every rank it is done, waits until every rank
+    // is, and writes the batch's outcome into the state
+    drain();
+    __syncthreads();
+    if (t == 0) {
+        const unsigned k = __hip_atomic_fetch_add(&ch->exit_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_flag = (k == gridDim.x - 1);
+        if (s_flag) __hip_atomic_store(&ch->exit_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!s_flag) return;
+    const unsigned dtag = B << 8;
+    if (t < W) put_g_sys(pv.gdone[t] + rank, aborted ? 1u : 0u, dtag);
+    const bool ok = gather_tagged<decltype(ident), true>(gdone, W, ident, dtag, s_g, &ch->abort_w, &s_ok, timeout);
+    if (t != 0) return;
+    bool peer_abort = false;
+    for (int k = 0; ok && k < W; ++k) peer_abort |= s_g[k] != 0u;
+    if (status0 != SX_NOT_ENDED) return;
+    if (!ok || aborted || peer_abort || ld_sc1(&ch->abort_w) != 0u) {
+        st->status = SX_HANG;
+        __hip_atomic_store(&ch->abort_w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    st->status = status;
+    st->pivots = piv0 + cnt;
+    if (cnt > 0) {
+        st->r = last_r;
+        st->e = last_e;
+        st->batch_tag = B;
+        st->batch_count = cnt;
+    }
+    st->e_next = e;
+    st->dmin_next = dmin;
+}
 
 // ---------------------------------------------------------------------------------------
 // K5: the sweep -- the batch's pivots applied to every stored element of the shard
@@ -1363,6 +1681,36 @@ void sx_launch_batch(const double *T, int rows, size_t ld, Cols c, double *d, in
     const int NA = (rows + SX_TILE - 1) / SX_TILE, NB = (c.N - 1 + SX_TILE - 1) / SX_TILE;
     k_batch<<<NA + NB, SX_TILE, batch_lds(k), s>>>(T, rows, ld, c, d, base, st, pd.U, pd.F, pd.recs, pd.PM,
                                                    pd.batch, k, NA, NB, chan, ga, gb, stamps);
+}
+
+bool sx_batch_mr_fits(int slots, int nb_local, int k, int grids) {
+    if (k < 1 || k > SX_KMAX || slots < 1 || slots > SX_TILE) return false;
+    static int per_cu[SX_KMAX + 1] = {0};
+    static int cus = 0;
+    if (per_cu[k] == 0) {
+        int dev = 0;
+        SX_HIP(hipGetDevice(&dev));
+        SX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        SX_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_batch_mr),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)batch_lds(SX_KMAX)));
+        int n = 0;
+        SX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_batch_mr, SX_TILE, batch_lds(k)));
+        per_cu[k] = n > 0 ? n : -1;
+    }
+    return per_cu[k] > 0 && (long long)grids * (slots + nb_local) <= (long long)per_cu[k] * cus * 3 / 4;
+}
+
+void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld, Cols c, double *d, int *base,
+                        DevState *st, const Pending &pd, int k, int slots, int W, int rank, int tb0, int tb1,
+                        BatchChan *chan, const unsigned long long *ga, const unsigned long long *gb,
+                        const unsigned long long *gdone, const PeerView &pv, unsigned long long timeout,
+                        hipStream_t s) {
+    const int NBg = (c.N - 1 + SX_TILE - 1) / SX_TILE;
+    if (W < 1 || W > SX_MAXW || W * slots > SX_TILE || NBg > SX_TILE || NBg < 1 || tb0 < 0 || tb1 > NBg || tb0 > tb1)
+        SX_FATAL("multi-rank fused batch: bad shape");
+    k_batch_mr<<<slots + (tb1 - tb0), SX_TILE, batch_lds(k), s>>>(T, rows, row0, rpr, ld, c, d, base, st, pd.U, pd.F,
+                                                                  pd.recs, pd.PM, pd.batch, k, slots, W, rank, tb0,
+                                                                  tb1, NBg, chan, ga, gb, gdone, pv, timeout);
 }
 
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s) {

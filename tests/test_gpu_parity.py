@@ -206,7 +206,7 @@ def test_session_pivots(gpu):
 def _pivots_with(cfg, T, d, base, k):
     Tg, dg, bg = T.copy(), d.copy(), base.copy()
     setters = {"batch": (sx.set_batch, 0), "rb": (sx.set_update_rows, 0), "sc1": (sx.set_store_sc1, -1),
-               "fused": (sx.set_fused, -1),
+               "fused": (sx.set_fused, -1), "p2p": (sx.set_p2p, -1),
                "waves": (sx.set_update_waves, 0), "W": (sx.set_virtual_ranks, 1)}
     try:
         for key, val in cfg.items():
@@ -244,6 +244,33 @@ def test_large_batch_sweeps_bit_exact(gpu, batch, rb, sc1):
     oracle.solve(T, d, base, max_pivots=70)
     assert done == 70
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+@pytest.mark.parametrize("batch", [1, 16, 32])
+@pytest.mark.parametrize("W", [2, 3])
+def test_p2p_fused_virtual_ranks(gpu, batch, W):
+    """the multi-rank fused batch (ranks hand off through each other's memory, objective tiles
+    split across ranks): W virtual shards on one GPU, their launches running at once"""
+    T, d, base = _phase1_state(300, 1100, 11)
+    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "W": W, "p2p": 1}, T, d, base, 150)
+    st_o, done_o = oracle.solve(T, d, base, max_pivots=150)
+    assert done == done_o
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+@pytest.mark.parametrize("W", [2, 3])
+@pytest.mark.parametrize("n,m,seed,lo,hi", [(300, 1100, 41100, 1, 100), (129, 1513, 77, -100, 100),
+                                            (64, 128, 6528, 1, 100)])
+def test_p2p_fused_two_phase(gpu, W, n, m, seed, lo, hi):
+    """whole two-phase solves through the multi-rank fused batch, phase ends mid-batch included"""
+    p = sx.generateRandomProblem(n, m, seed, lo, hi)
+    try:
+        sx.set_virtual_ranks(W)
+        sx.set_p2p(1)
+        _check_two_phase(p)
+    finally:
+        sx.set_p2p(-1)
+        sx.set_virtual_ranks(1)
 
 
 @pytest.mark.parametrize("sc1", [0, 1])

@@ -1,0 +1,44 @@
+"""Pivot rate of the multi-rank paths on ONE GPU (diagnostic): virtual shards with the per-pivot
+exchange vs the peer-memory fused batch, and the fused multi-rank kernel at W = 1 (force).
+
+usage: python tools/p2p_probe.py [config] [pivots]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def run(sx, n, m, seed, k, W, p2p, force=0):
+    sx.set_virtual_ranks(W)
+    sx.set_p2p(p2p)
+    sx.set_force_exchange(force)
+    try:
+        s = sx.Session(generated=(n, m, seed, 1, 100))
+        s.pivots(64)
+        t = s.pivots(k, time_updates=1)
+        s.close()
+    finally:
+        sx.set_virtual_ranks(1)
+        sx.set_p2p(-1)
+        sx.set_force_exchange(0)
+    return t
+
+
+def main():
+    import torch
+    torch.cuda.set_device(0)
+    import simplexoncuda_amd as sx
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "config3"
+    k = int(sys.argv[2]) if len(sys.argv) > 2 else 640
+    n, m, seed = bench.CONFIGS[cfg]
+    for W, p2p, force in [(1, -1, 0), (1, 1, 1), (2, 0, 0), (2, 1, 0), (3, 0, 0), (3, 1, 0)]:
+        t = run(sx, n, m, seed, k, W, p2p, force)
+        print(f"{cfg} W={W} p2p={p2p} force_exchange={force}: {t.pivots / t.wall_ms * 1e3:9.1f} pivots/s "
+              f"({t.wall_ms * 1e3 / max(t.pivots, 1):7.2f} us/pivot, sweep {t.update_ms * 1e3 / max(t.update_launches, 1):8.1f} us)"
+              f" status {t.status}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
