@@ -107,8 +107,8 @@ def main():
                     help="per-launch HBM bytes of the sweep kernel from rocprofv3 --pmc (JSON)")
     ap.add_argument("--secondary", default="config5",
                     help="second workload timed in the same run ('' to skip): the m=32768 scaling problem")
-    ap.add_argument("--secondary-steps", type=int, default=40)
-    ap.add_argument("--secondary-warmup", type=int, default=3)
+    ap.add_argument("--secondary-steps", type=int, default=320)
+    ap.add_argument("--secondary-warmup", type=int, default=32)
     args = ap.parse_args()
 
     import torch

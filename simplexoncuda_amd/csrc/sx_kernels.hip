@@ -682,36 +682,37 @@ __device__ __forceinline__ unsigned ld_sc1(const unsigned *p) {
     return __hip_atomic_load(const_cast<unsigned *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Wave 0 reads n granules, granule k at base[off(k)], each until it carries `tag`, into
-// out[k] (LDS).  Block-uniform result: false when the batch was aborted (or this wait timed
-// out, which aborts it).  Every thread of the block must call it.
 __device__ __forceinline__ u64 ld_sys(const u64 *p) {
     return __hip_atomic_load(const_cast<u64 *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The block reads n <= 4 * blockDim granules, granule k at base[off(k)], each until it
+// carries `tag`, into out[k] (LDS): every thread polls its own granules (k = t, t + 512, ...),
+// all of them in flight together, until the block agrees that all have arrived.  Block-uniform
+// result: false when the batch was aborted (or this wait timed out, which aborts it).  Every
+// thread of the block must call it.
 template <typename OFF, bool SYS = false>
 __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, unsigned *out, unsigned *abort_w,
                               int *s_ok, unsigned long long timeout = 20000000ull) {
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        int ok = 1;
-        const u64 t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-        for (int k0 = 0; k0 < n && ok; k0 += 64) {
-            const int k = k0 + lane;
-            bool have = k >= n;
-            unsigned v = 0;
+    const int t = threadIdx.x, nt = blockDim.x;
+    if (n <= 64) {  // one wave polls, no block barrier per poll
+        if (t < 64) {
+            const bool exists = t < n;
+            bool have = !exists;
+            int ok = 1;
+            const u64 t0 = __builtin_amdgcn_s_memrealtime();
             for (unsigned it = 0;; ++it) {
                 if (!have) {
-                    const u64 w = SYS ? ld_sys(base + off(k)) : ld_sc1(base + off(k));
+                    const u64 w = SYS ? ld_sys(base + off(t)) : ld_sc1(base + off(t));
                     if ((unsigned)(w >> 32) == tag) {
                         have = true;
-                        v = (unsigned)w;
+                        out[t] = (unsigned)w;
                     }
                 }
                 if (__ballot(!have) == 0ull) break;
                 if ((it & 63) == 63) {
                     int stop = ld_sc1(abort_w) != 0u;
-                    if (!stop && __builtin_amdgcn_s_memrealtime() - t0 > timeout) {  // 100 MHz ticks
+                    if (!stop && __builtin_amdgcn_s_memrealtime() - t0 > timeout) {
                         __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         stop = 1;
                     }
@@ -722,12 +723,44 @@ __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, uns
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
-            if (ok && k < n) out[k] = v;
+            if (t == 0) *s_ok = ok;
         }
-        if (lane == 0) *s_ok = ok;
+        __syncthreads();
+        return *s_ok != 0;
     }
-    __syncthreads();
-    return *s_ok != 0;
+    unsigned have = 0u;  // bit c: granule t + c * nt has arrived (or does not exist)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        if (t + c * nt >= n) have |= 1u << c;
+    const u64 t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+    for (unsigned it = 0;; ++it) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (!((have >> c) & 1u)) {
+                const int k = t + c * nt;
+                const u64 w = SYS ? ld_sys(base + off(k)) : ld_sc1(base + off(k));
+                if ((unsigned)(w >> 32) == tag) {
+                    have |= 1u << c;
+                    out[k] = (unsigned)w;
+                }
+            }
+        }
+        if (!__syncthreads_or(have != 0xFu)) break;
+        if ((it & 63) == 63) {
+            if (t == 0) {
+                int stop = ld_sc1(abort_w) != 0u;
+                if (!stop && __builtin_amdgcn_s_memrealtime() - t0 > timeout) {  // 100 MHz ticks
+                    __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    stop = 1;
+                }
+                *s_ok = !stop;
+            }
+            __syncthreads();
+            if (!*s_ok) return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return true;  // the vote's barrier made every thread's LDS writes visible
 }
 
 // granule layout of one tile record
@@ -1669,9 +1702,8 @@ bool sx_batch_fits(int rows, Cols c, int k) {
         SX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_batch, SX_TILE, batch_lds(k)));
         per_cu[k] = n > 0 ? n : -1;
     }
-    // every block resident at once (one per CU is enough: the hand-offs never wait on a
-    // block that has not started), with a margin of a quarter of the CUs
-    return per_cu[k] > 0 && (long long)(NA + NB) <= (long long)per_cu[k] * cus * 3 / 4;
+    // every block resident at once (the hand-offs wait on every block), 16 CUs to spare
+    return per_cu[k] > 0 && (long long)(NA + NB) <= (long long)per_cu[k] * cus - 16;
 }
 
 void sx_launch_batch(const double *T, int rows, size_t ld, Cols c, double *d, int *base, DevState *st,
@@ -1697,7 +1729,7 @@ bool sx_batch_mr_fits(int slots, int nb_local, int k, int grids) {
         SX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_batch_mr, SX_TILE, batch_lds(k)));
         per_cu[k] = n > 0 ? n : -1;
     }
-    return per_cu[k] > 0 && (long long)grids * (slots + nb_local) <= (long long)per_cu[k] * cus * 3 / 4;
+    return per_cu[k] > 0 && (long long)grids * (slots + nb_local) <= (long long)per_cu[k] * cus - 16;
 }
 
 void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld, Cols c, double *d, int *base,
