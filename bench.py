@@ -38,6 +38,8 @@ CPU_SAMPLE = {"config2": 200, "config3": 50, "config4": 10, "config5": 3}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # reference: RTX 2070 Super, config 3 phase 1, mean 7607.5 us per pivot
 REF_PIVOTS_PER_S = {"config3": 1e6 / 7607.5}
+# reference: RTX 2070 Super, config 3, pivot-loop totals 68.33 s (phase 1) + 0.94 s (phase 2), 8981 + 255 pivots
+REF_SOLVE = {"config3": {"pivot_loop_s": 68.33 + 0.94, "pivots": [8981, 255]}}
 
 
 def cpu_model():
@@ -107,6 +109,8 @@ def main():
                     help="per-launch HBM bytes of the sweep kernel from rocprofv3 --pmc (JSON)")
     ap.add_argument("--secondary", default="config5",
                     help="second workload timed in the same run ('' to skip): the m=32768 scaling problem")
+    ap.add_argument("--no-full-solve", action="store_true",
+                    help="skip the end-to-end twoPhaseMethod solve of the workload's instance (N=1 only)")
     ap.add_argument("--secondary-steps", type=int, default=320)
     ap.add_argument("--secondary-warmup", type=int, default=32)
     args = ap.parse_args()
@@ -222,6 +226,23 @@ def main():
             "update_GBps_rank0": r2["achieved"], "update_frac_of_peak": r2["achieved"] / HBM_PEAK_GBS
             if r2["achieved"] else None, "avg_update_us": r2["avg_update_s"] * 1e6,
         }
+    if world == 1 and not args.no_full_solve:
+        # the whole drop-in call on the same instance: build + both phases + solution, as the
+        # reference's main.cu -t times it (problem synthesised on the GPU, copied to the host first)
+        prob = sx.generateRandomProblemDevice(n, m, seed, 1, 100)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = sx.twoPhaseMethodEx(prob)
+        dt = time.perf_counter() - t0
+        prob.close()
+        full = {"seconds": dt, "status": sx.STATUS_NAMES.get(res.status, res.status), "pivots": list(res.pivots),
+                "objective": res.optimal_value,
+                "note": "twoPhaseMethod wall time incl. tableau build from host arrays, both phases and the solution"}
+        if args.config in REF_SOLVE:
+            full["reference_pivot_loop_s"] = REF_SOLVE[args.config]["pivot_loop_s"]
+            full["reference_pivots"] = REF_SOLVE[args.config]["pivots"]
+            full["pivots_match_reference"] = list(res.pivots) == REF_SOLVE[args.config]["pivots"]
+        out["full_solve"] = full
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, m, seed, CPU_SAMPLE[args.config], sx)
     if rank == 0:
