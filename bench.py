@@ -1,19 +1,25 @@
 """Benchmark: simplex pivots/s and HBM GB/s of the rank-1 tableau update on MI355X.
 
-Workload (BASELINE.json configs[2], the config the roofline target is quoted on):
-generateRandomProblem(n=8192, m=4096, seed=823296, [1,100]) -- the reference's own -t
-instance (main.cu:56-64) -- phase-1 tableau 4096 x 16385 fp64 (537 MB) resident in HBM.
+Workload (BASELINE.json configs[4], the m=32768 problem north_star's scaling target is
+quoted on): generateRandomProblem(n=8192, m=32768, seed=851968, [1,100]) -- seed n*100+m as
+the reference's -t sweep (main.cu:56-64) -- phase-1 tableau 32768 x 73729 fp64, synthesised
+in HBM (10.7 GB stored: artificial columns aliased to their slack columns).
 A "step" is one simplex pivot (entering argmin, ratio test, pivot row, objective row, and
 the rank-1 update of the whole tableau -- applied in sweeps of 32 pivots).
-W untimed pivots, then K timed pivots: by default pivots 50..8950 of the instance's 8981
-phase-1 pivots, i.e. the whole phase at its real mix of sparse and dense pivots.
+W untimed pivots, then K timed pivots: by default pivots 64..2064 of phase 1 (SURVEY.md §8d:
+the scaling curve is the first 2000 phase-1 pivots).
 
 N GPUs (torchrun, one process per GPU): the constraint rows are split into N contiguous
-512-aligned blocks; every pivot does one tile-winner allgather and one pivot-row
-allreduce over RCCL.  The problem is the same at every N ("strong" scaling).
+512-aligned blocks, each rank sweeps only its rows; per pivot the ranks exchange the tile
+winners and the pivot row (peer memory over xGMI inside one launch per batch, or RCCL).
+The problem is the same at every N ("strong" scaling).
+
+Secondary (same JSON line): config 3, the reference's own 8192 x 4096 -t instance, whose
+4096-row tableau the roofline target is quoted on (8900 of its 8981 phase-1 pivots, with
+its own sweep roofline), and at N=1 its end-to-end twoPhaseMethod solve.
 
 The CPU baseline is the serial C oracle (oracle/, a restatement of the reference's
-algorithm -- the reference has no CPU path) on the first pivots of the same instance,
+algorithm -- the reference has no CPU path) on the first pivots of the primary instance,
 pinned to one core; the same pivots are re-run on the GPU and checked bit for bit.
 """
 import argparse
@@ -34,10 +40,10 @@ CONFIGS = {
     "config5": (8192, 32768, 851968),
 }
 # oracle pivots timed for the CPU baseline (first 50 / 10 / 3 pivots)
-CPU_SAMPLE = {"config2": 200, "config3": 50, "config4": 10, "config5": 3}
+CPU_SAMPLE = {"config2": 200, "config3": 50, "config4": 10, "config5": 5}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # reference: RTX 2070 Super, config 3 phase 1, mean 7607.5 us per pivot
-REF_PIVOTS_PER_S = {"config3": 1e6 / 7607.5}
+REF_PIVOTS_PER_S = {"config3": 1e6 / 7607.5}  # (no published number for configs 4-5)
 # reference: RTX 2070 Super, config 3, pivot-loop totals 68.33 s (phase 1) + 0.94 s (phase 2), 8981 + 255 pivots
 REF_SOLVE = {"config3": {"pivot_loop_s": 68.33 + 0.94, "pivots": [8981, 255]}}
 
@@ -97,22 +103,22 @@ def cpu_baseline(n, m, seed, pivots, sx):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8900, help="timed pivots")
-    ap.add_argument("--warmup", type=int, default=50, help="untimed pivots before timing")
-    ap.add_argument("--config", default="config3", choices=sorted(CONFIGS))
+    ap.add_argument("--steps", type=int, default=2000, help="timed pivots")
+    ap.add_argument("--warmup", type=int, default=64, help="untimed pivots before timing")
+    ap.add_argument("--config", default="config5", choices=sorted(CONFIGS))
     ap.add_argument("--update-rows", type=int, default=0, help="rows per sweep step (0 = auto)")
     ap.add_argument("--batch", type=int, default=0, help="pivots per tableau sweep (0 = library default, 32)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--update-events", type=int, default=1,
                     help="bracket every k-th sweep launch with HIP events (0 = none)")
-    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_sweep_config3.json"),
-                    help="per-launch HBM bytes of the sweep kernel from rocprofv3 --pmc (JSON)")
-    ap.add_argument("--secondary", default="config5",
-                    help="second workload timed in the same run ('' to skip): the m=32768 scaling problem")
+    ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles"),
+                    help="directory of pmc_sweep_<config>.json: per-launch HBM bytes of the sweep (rocprofv3 --pmc)")
+    ap.add_argument("--secondary", default="config3",
+                    help="second workload timed in the same run ('' to skip): the roofline-target tableau")
     ap.add_argument("--no-full-solve", action="store_true",
-                    help="skip the end-to-end twoPhaseMethod solve of the workload's instance (N=1 only)")
-    ap.add_argument("--secondary-steps", type=int, default=320)
-    ap.add_argument("--secondary-warmup", type=int, default=32)
+                    help="skip the end-to-end twoPhaseMethod solve of config 3's instance (N=1 only)")
+    ap.add_argument("--secondary-steps", type=int, default=8900)
+    ap.add_argument("--secondary-warmup", type=int, default=50)
     args = ap.parse_args()
 
     import torch
@@ -167,14 +173,34 @@ def main():
         return {"n": n, "m": m, "seed": seed, "tim": tim, "elapsed": elapsed, "pivots": tim.pivots,
                 "avg_update_s": avg_update_s, "achieved": achieved, "setup_s": t_setup}
 
+    def roofline(cfg, r):
+        tim, achieved = r["tim"], r["achieved"]
+        traffic = None
+        pmc = os.path.join(args.pmc_dir, f"pmc_sweep_{cfg}.json") if args.pmc_dir else None
+        if pmc and os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        return {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS if achieved else None,
+            "traffic": traffic,
+            "kernel": "k_sweep (rank-1 pivot updates of a batch applied to the tableau, rank 0)",
+            "algorithmic_bytes_per_launch": tim.update_bytes,
+            "pivots_per_launch": tim.swept_pivots / max(tim.update_launches, 1),
+            "avg_launch_us": r["avg_update_s"] * 1e6,
+            "timed_launches": tim.update_launches,
+            "sweep_share_of_time": tim.update_ms / max(tim.wall_ms, 1e-9),
+        }
+
+    def workload(cfg, r):
+        return (f"{cfg}: phase-1 pivots, {r['m']}x{1 + r['n'] + 2 * r['m']} fp64 tableau "
+                f"(m={r['m']}, n={r['n']}, seed={r['seed']})")
+
     r = measure(args.config, args.steps, args.warmup, args.update_events)
     n, m, seed, tim, elapsed, pivots = r["n"], r["m"], r["seed"], r["tim"], r["elapsed"], r["pivots"]
-    avg_update_s, achieved = r["avg_update_s"], r["achieved"]
-    traffic = None
-    if args.pmc_file and os.path.exists(args.pmc_file):
-        with open(args.pmc_file) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
-    N1 = 1 + n + 2 * m
     out = {
         "metric": "simplex pivots/sec + HBM GB/s on gaussian update, dense m×n tableau",
         "value": pivots / elapsed,
@@ -187,61 +213,48 @@ def main():
         "scaling": "strong",
         "vs_baseline": (pivots / elapsed) / REF_PIVOTS_PER_S[args.config] if args.config in REF_PIVOTS_PER_S else None,
         "dtype": "f64",
-        "data": f"synthetic: generateRandomProblem(n={n}, m={m}, seed={seed}, [1,100]) -- the reference's -t "
-                "instance (cuRAND-XORWOW + MSVC rand semantics), synthesised on the GPU",
+        "data": f"synthetic: generateRandomProblem(n={n}, m={m}, seed={seed}, [1,100]) -- seed n*100+m as the "
+                "reference's -t sweep (cuRAND-XORWOW + MSVC rand semantics), synthesised on the GPU",
         "config": {
-            "workload": f"{args.config}: phase-1 pivots, {m}x{N1} fp64 tableau (m={m}, n={n})",
+            "workload": workload(args.config, r),
             "m": m, "n": n, "seed": seed, "tableau_width": tim.width, "stored_width": tim.stored_width,
             "rows_per_gpu_rank0": tim.local_rows, "parallelism": f"row-block x{world}",
             "exchange": ("none (one shard)" if world == 1 else
                          "peer-memory fused batch (xGMI)" if sx.p2p_ready() else "per-pivot RCCL collectives"),
             "pivots_timed": pivots, "status_after": tim.status, "setup_s": r["setup_s"],
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS if achieved else None,
-            "traffic": traffic,
-            "kernel": "k_sweep (rank-1 pivot updates of a batch applied to the tableau, rank 0)",
-            "algorithmic_bytes_per_launch": tim.update_bytes,
-            "pivots_per_launch": tim.swept_pivots / max(tim.update_launches, 1),
-            "avg_launch_us": avg_update_s * 1e6,
-            "timed_launches": tim.update_launches,
-            "sweep_share_of_time": tim.update_ms / max(tim.wall_ms, 1e-9),
-        },
+        "roofline": roofline(args.config, r),
         "cpu_baseline": None,
     }
     if args.secondary and args.secondary != args.config:
         r2 = measure(args.secondary, args.secondary_steps, args.secondary_warmup, args.update_events)
-        t2 = r2["tim"]
         out["secondary"] = {
-            "workload": f"{args.secondary}: phase-1 pivots, {r2['m']}x{1 + r2['n'] + 2 * r2['m']} fp64 tableau "
-                        f"(m={r2['m']}, n={r2['n']}, seed={r2['seed']})",
+            "workload": workload(args.secondary, r2),
             "value": r2["pivots"] / r2["elapsed"], "unit": "pivots/s",
+            "vs_baseline": (r2["pivots"] / r2["elapsed"]) / REF_PIVOTS_PER_S[args.secondary]
+            if args.secondary in REF_PIVOTS_PER_S else None,
             "ms_per_step": r2["elapsed"] * 1e3 / max(r2["pivots"], 1),
             "steps": args.secondary_steps, "warmup": args.secondary_warmup, "pivots_timed": r2["pivots"],
-            "rows_per_gpu_rank0": t2.local_rows, "setup_s": r2["setup_s"],
-            "update_GBps_rank0": r2["achieved"], "update_frac_of_peak": r2["achieved"] / HBM_PEAK_GBS
-            if r2["achieved"] else None, "avg_update_us": r2["avg_update_s"] * 1e6,
+            "status_after": r2["tim"].status, "rows_per_gpu_rank0": r2["tim"].local_rows, "setup_s": r2["setup_s"],
+            "roofline": roofline(args.secondary, r2),
         }
     if world == 1 and not args.no_full_solve:
-        # the whole drop-in call on the same instance: build + both phases + solution, as the
-        # reference's main.cu -t times it (problem synthesised on the GPU, copied to the host first)
-        prob = sx.generateRandomProblemDevice(n, m, seed, 1, 100)
+        # the whole drop-in call on config 3's instance (the reference's -t instance with published
+        # timings): build + both phases + solution, as main.cu -t times it (problem synthesised on
+        # the GPU, copied to the host first)
+        fn, fm, fseed = CONFIGS["config3"]
+        prob = sx.generateRandomProblemDevice(fn, fm, fseed, 1, 100)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         res = sx.twoPhaseMethodEx(prob)
         dt = time.perf_counter() - t0
         prob.close()
-        full = {"seconds": dt, "status": sx.STATUS_NAMES.get(res.status, res.status), "pivots": list(res.pivots),
-                "objective": res.optimal_value,
+        full = {"instance": "config3", "seconds": dt, "status": sx.STATUS_NAMES.get(res.status, res.status),
+                "pivots": list(res.pivots), "objective": res.optimal_value,
                 "note": "twoPhaseMethod wall time incl. tableau build from host arrays, both phases and the solution"}
-        if args.config in REF_SOLVE:
-            full["reference_pivot_loop_s"] = REF_SOLVE[args.config]["pivot_loop_s"]
-            full["reference_pivots"] = REF_SOLVE[args.config]["pivots"]
-            full["pivots_match_reference"] = list(res.pivots) == REF_SOLVE[args.config]["pivots"]
+        full["reference_pivot_loop_s"] = REF_SOLVE["config3"]["pivot_loop_s"]
+        full["reference_pivots"] = REF_SOLVE["config3"]["pivots"]
+        full["pivots_match_reference"] = list(res.pivots) == REF_SOLVE["config3"]["pivots"]
         out["full_solve"] = full
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, m, seed, CPU_SAMPLE[args.config], sx)

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
-ARGS=${PROF_ARGS:---steps 2000 --warmup 50 --no-cpu-baseline --secondary= --update-events 0}
+ARGS=${PROF_ARGS:---steps 2000 --warmup 64 --no-cpu-baseline --secondary= --no-full-solve --update-events 0}
 echo "== kernel trace ($(date +%T))"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 bench.py $ARGS > $OUT/kt.log 2>&1 || { echo "kt failed"; tail -20 $OUT/kt.log; exit 1; }
 tail -2 $OUT/kt.log
