@@ -664,6 +664,16 @@ typedef unsigned long long u64;
 
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// Granule tag word: [batch id mod 2^15 | slot q (6 bits) | payload (11 bits)].  A consumer
+// matches on batch and slot and ignores the payload, so a tile winner's value granules also
+// carry its index (and the ratio tiles' eligibility bit): 2 granules per winner instead of 3-4.
+#define SX_PAYBITS 11
+#define SX_PAYMASK ((1u << SX_PAYBITS) - 1u)
+#define SX_NOIDX 0x3FFu  // payload index of a tile without a candidate
+__device__ __forceinline__ unsigned make_tag(unsigned B, int q) {
+    return ((B & 0x7FFFu) << (6 + SX_PAYBITS)) | ((unsigned)q << SX_PAYBITS);
+}
+
 __device__ __forceinline__ void put_g(u64 *g, unsigned data, unsigned tag) {
     __hip_atomic_store(g, ((u64)tag << 32) | data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -693,7 +703,8 @@ __device__ __forceinline__ u64 ld_sys(const u64 *p) {
 // thread of the block must call it.
 template <typename OFF, bool SYS = false>
 __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, unsigned *out, unsigned *abort_w,
-                              int *s_ok, unsigned long long timeout = 20000000ull) {
+                              int *s_ok, unsigned long long timeout = 20000000ull, unsigned *pay = nullptr) {
+    // (pay: the payload of every even granule k goes to pay[k / 2] -- records of two granules)
     const int t = threadIdx.x, nt = blockDim.x;
     if (n <= 64) {  // one wave polls, no block barrier per poll
         if (t < 64) {
@@ -704,9 +715,10 @@ __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, uns
             for (unsigned it = 0;; ++it) {
                 if (!have) {
                     const u64 w = SYS ? ld_sys(base + off(t)) : ld_sc1(base + off(t));
-                    if ((unsigned)(w >> 32) == tag) {
+                    if (((unsigned)(w >> 32) | SX_PAYMASK) == (tag | SX_PAYMASK)) {
                         have = true;
                         out[t] = (unsigned)w;
+                        if (pay && !(t & 1)) pay[t >> 1] = (unsigned)(w >> 32) & SX_PAYMASK;
                     }
                 }
                 if (__ballot(!have) == 0ull) break;
@@ -739,9 +751,10 @@ __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, uns
             if (!((have >> c) & 1u)) {
                 const int k = t + c * nt;
                 const u64 w = SYS ? ld_sys(base + off(k)) : ld_sc1(base + off(k));
-                if ((unsigned)(w >> 32) == tag) {
+                if (((unsigned)(w >> 32) | SX_PAYMASK) == (tag | SX_PAYMASK)) {
                     have |= 1u << c;
                     out[k] = (unsigned)w;
+                    if (pay && !(k & 1)) pay[k >> 1] = (unsigned)(w >> 32) & SX_PAYMASK;
                 }
             }
         }
@@ -764,8 +777,10 @@ __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, uns
 }
 
 // granule layout of one tile record
-#define SX_GA_STRIDE (8 + 2 * SX_KMAX)  // ratio tile: v(2) idx elig a(2) b(2) | F[r][s] (2 per slot)
-#define SX_GB_STRIDE (4 + 2 * SX_KMAX)  // objective tile: v(2) idx pad | U[s][e] (2 per slot)
+#define SX_GA_STRIDE (8 + 2 * SX_KMAX)  // ratio tile: v(2, payload: idx, elig) pad(2) a(2) b(2) | F[r][s] (2 per slot)
+#define SX_GB_STRIDE (4 + 2 * SX_KMAX)  // objective tile: v(2, payload: idx) pad(2) | U[s][e] (2 per slot)
+__device__ __forceinline__ int rec2_a(int k) { return (k >> 1) * SX_GA_STRIDE + (k & 1); }
+__device__ __forceinline__ int rec2_b(int k) { return (k >> 1) * SX_GB_STRIDE + (k & 1); }
 
 __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int rows, size_t ld, Cols c,
                                                double *__restrict__ d, int *base, DevState *st, double *U, double *F,
@@ -779,6 +794,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
     __shared__ double s_ue[SX_KMAX], s_fr[SX_KMAX];  // U[s][e] (entering column) / F[r][s] (leaving row)
     __shared__ double s_a[SX_TILE], s_b[SX_TILE];    // ratio blocks: entering column, RHS (winner lookup)
     __shared__ unsigned s_g[4 * SX_TILE];            // gathered granules
+    __shared__ unsigned s_pay[SX_TILE];              // their payloads (two-granule records)
     __shared__ int s_ok, s_flag, s_win;
     __shared__ double s_wv;
     const int t = threadIdx.x;
@@ -809,8 +825,11 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
         unsigned bits = 0u;                            // slots where this row left the basis
         double dj = liveB ? d[1 + ia] : 0.0;
         double d0 = (!isA && tb == 0 && t == 0) ? d[0] : 0.0;
+        // the entering column's stored value of this row: loaded as soon as the entering
+        // variable is known, so the load overlaps the wait for its pending history
+        double a_pre = liveA ? T[(size_t)li * ld + c.map(1 + (e >= 0 ? e : 0))] : 0.0;
         for (int q = 0; q < K; ++q) {
-            const unsigned tag = (B << 8) | (unsigned)q;
+            const unsigned tag = make_tag(B, q);
             // ---- does the phase end here?  (the same decision in every block)
             if (cap >= 0 && piv0 + q >= cap) {
                 status = SX_PIVOT_CAP;
@@ -820,12 +839,11 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                 status = SX_FEASIBLE;
                 break;
             }
-            const int ce = c.map(1 + e);
             double a = 0.0;
             if (isA) {
                 // ---- ratio tile: current entering column, ratios, tile winner
                 if (blockIdx.x == 0) SX_STAMP(0);
-                if (liveA) a = T[(size_t)li * ld + ce];
+                a = a_pre;
                 for (int s = 0; s < q; ++s) {
                     if ((bits >> s) & 1u)
                         a = a / s_p[s];
@@ -854,9 +872,9 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                 u64 *g = ga + (size_t)blockIdx.x * SX_GA_STRIDE;
                 const int wl = s_win;
                 if (t == 0) {
-                    put_gd(g, s_wv, tag);
-                    put_g(g + 2, (unsigned)(ri), tag);
-                    put_g(g + 3, (unsigned)any, tag);
+                    const unsigned pl = (ri >= 0 ? (unsigned)(ri - (int)blockIdx.x * SX_TILE) : SX_NOIDX) |
+                                        ((unsigned)any << 10);
+                    put_gd(g, s_wv, tag | pl);
                     put_gd(g + 4, s_a[wl], tag);
                     put_gd(g + 6, s_b[wl], tag);
                 } else if (t - 1 < q) {
@@ -865,8 +883,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                 if (blockIdx.x == 0) SX_STAMP(1);
             }
             // ---- selection: every block runs pass 2 over the ratio-tile winners
-            if (!gather_tagged(ga, 4 * NA, [](int k) { return (k >> 2) * SX_GA_STRIDE + (k & 3); }, tag, s_g,
-                               &ch->abort_w, &s_ok)) {
+            if (!gather_tagged(ga, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay)) {
                 aborted = true;
                 break;
             }
@@ -874,11 +891,12 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
             double tv = DBL_MAX;
             int ti = -1, te = 0;
             if (t < NA) {
-                const double cv = gd(s_g[4 * t], s_g[4 * t + 1]);
-                te = (int)s_g[4 * t + 3];
+                const double cv = gd(s_g[2 * t], s_g[2 * t + 1]);
+                const unsigned pl = s_pay[t];
+                te = (int)((pl >> 10) & 1u);
                 if (cmp_eps(cv, tv) < 0) {
                     tv = cv;
-                    ti = (int)s_g[4 * t + 2];
+                    ti = (pl & SX_NOIDX) == SX_NOIDX ? -1 : t * SX_TILE + (int)(pl & SX_NOIDX);
                 }
             }
             const int anyall = __syncthreads_or(SX_ELIG(te));
@@ -963,27 +981,24 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                 }
                 __syncthreads();
                 u64 *g = gb + (size_t)tb * SX_GB_STRIDE;
-                if (t == 0) {
-                    put_gd(g, s_wv, tag);
-                    put_g(g + 2, (unsigned)s_flag, tag);
-                } else if (t - 1 <= q) {
+                if (t == 0) put_gd(g, s_wv, tag | (s_flag >= 0 ? (unsigned)(s_flag - tb * SX_TILE) : SX_NOIDX)); else if (t - 1 <= q) {
                     put_gd(g + 4 + 2 * (t - 1), s_hist[(t - 1) * SX_TILE + s_win], tag);  // U[s][winner]
                 }
                 if (tb == 0) SX_STAMP(4);
             }
             // ---- entering variable of pivot q + 1: every block runs pass 2 over the objective tiles
-            if (!gather_tagged(gb, 3 * NB, [](int k) { return (k / 3) * SX_GB_STRIDE + (k % 3); }, tag, s_g,
-                               &ch->abort_w, &s_ok)) {
+            if (!gather_tagged(gb, 2 * NB, rec2_b, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay)) {
                 aborted = true;
                 break;
             }
             double ev = DBL_MAX;
             int ei = -1;
             if (t < NB) {
-                const double cv = gd(s_g[3 * t], s_g[3 * t + 1]);
+                const double cv = gd(s_g[2 * t], s_g[2 * t + 1]);
+                const unsigned pl = s_pay[t] & SX_NOIDX;
                 if (cmp_eps(cv, ev) < 0) {
                     ev = cv;
-                    ei = (int)s_g[3 * t + 2];
+                    ei = pl == SX_NOIDX ? -1 : t * SX_TILE + (int)pl;
                 }
             }
             block_argmin512(ev, ei, s_v, s_i);
@@ -994,6 +1009,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
             __syncthreads();
             e = s_win;
             dmin = s_wv;
+            if (liveA) a_pre = T[(size_t)li * ld + c.map(1 + (e >= 0 ? e : 0))];
             if (isA && blockIdx.x == 0) SX_STAMP(5);
             // the ratio blocks need the pending pivot rows' entries in the new entering column
             if (isA && q + 1 < K && e >= 0 && cmp_eps(dmin, 0.0) < 0) {
@@ -1088,6 +1104,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
     __shared__ double s_ue[SX_KMAX], s_fr[SX_KMAX];
     __shared__ double s_a[SX_TILE], s_b[SX_TILE];
     __shared__ unsigned s_g[4 * SX_TILE];
+    __shared__ unsigned s_pay[SX_TILE];
     __shared__ int s_ok, s_flag, s_win;
     __shared__ double s_wv;
     const int t = threadIdx.x;
@@ -1099,8 +1116,8 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
     double dmin = st->dmin_next;
     int status = SX_NOT_ENDED, cnt = 0, last_r = -1, last_e = -1;
     bool aborted = false;
-    auto gather_a = [](int k) { return (k >> 2) * SX_GA_STRIDE + (k & 3); };
-    auto gather_b = [](int k) { return (k / 3) * SX_GB_STRIDE + (k % 3); };
+    auto gather_a = [](int k) { return rec2_a(k); };
+    auto gather_b = [](int k) { return rec2_b(k); };
     auto ident = [](int k) { return k; };
     const int li = blockIdx.x * SX_TILE + t;
     const bool liveA = isA && li < rows;
@@ -1115,8 +1132,11 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
     if (status0 == SX_NOT_ENDED) {
         double b = liveA ? T[(size_t)li * ld] : 0.0;
         unsigned bits = 0u;
+        // the entering column's stored value of this row: loaded as soon as the entering
+        // variable is known, so the load overlaps the wait for its pending history
+        double a_pre = liveA ? T[(size_t)li * ld + c.map(1 + (e >= 0 ? e : 0))] : 0.0;
         for (int q = 0; q < K; ++q) {
-            const unsigned tag = (B << 8) | (unsigned)q;
+            const unsigned tag = make_tag(B, q);
             if (cap >= 0 && piv0 + q >= cap) {
                 status = SX_PIVOT_CAP;
                 break;
@@ -1125,10 +1145,9 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
                 status = SX_FEASIBLE;
                 break;
             }
-            const int ce = c.map(1 + e);
             double a = 0.0;
             if (isA) {
-                if (liveA) a = T[(size_t)li * ld + ce];
+                a = a_pre;
                 for (int s = 0; s < q; ++s) {
                     if ((bits >> s) & 1u)
                         a = a / s_p[s];
@@ -1159,9 +1178,9 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
                 for (int k = 0; k < W; ++k) {
                     u64 *g = pv.ga[k] + (size_t)gt * SX_GA_STRIDE;
                     if (t == 0) {
-                        put_gd_sys(g, s_wv, tag);
-                        put_g_sys(g + 2, (unsigned)s_flag, tag);
-                        put_g_sys(g + 3, (unsigned)any, tag);
+                        const unsigned pl = (s_flag >= 0 ? (unsigned)(s_flag - gt * SX_TILE) : SX_NOIDX) |
+                                            ((unsigned)any << 10);
+                        put_gd_sys(g, s_wv, tag | pl);
                         put_gd_sys(g + 4, s_a[wl], tag);
                         put_gd_sys(g + 6, s_b[wl], tag);
                     } else if (t - 1 < q) {
@@ -1170,19 +1189,20 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
                 }
             }
             // ---- selection: pass 2 over every rank's ratio tiles
-            if (!gather_tagged<decltype(gather_a), true>(ga, 4 * NAg, gather_a, tag, s_g, &ch->abort_w, &s_ok,
-                                                         timeout)) {
+            if (!gather_tagged<decltype(gather_a), true>(ga, 2 * NAg, gather_a, tag, s_g, &ch->abort_w, &s_ok,
+                                                         timeout, s_pay)) {
                 aborted = true;
                 break;
             }
             double tv = DBL_MAX;
             int ti = -1, te = 0;
             if (t < NAg) {
-                const double cv = gd(s_g[4 * t], s_g[4 * t + 1]);
-                te = (int)s_g[4 * t + 3];
+                const double cv = gd(s_g[2 * t], s_g[2 * t + 1]);
+                const unsigned pl = s_pay[t];
+                te = (int)((pl >> 10) & 1u);
                 if (cmp_eps(cv, tv) < 0) {
                     tv = cv;
-                    ti = (int)s_g[4 * t + 2];
+                    ti = (pl & SX_NOIDX) == SX_NOIDX ? -1 : t * SX_TILE + (int)(pl & SX_NOIDX);
                 }
             }
             const int anyall = __syncthreads_or(SX_ELIG(te));
@@ -1271,27 +1291,26 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
                 __syncthreads();
                 for (int k = 0; k < W; ++k) {
                     u64 *g = pv.gb[k] + (size_t)tb * SX_GB_STRIDE;
-                    if (t == 0) {
-                        put_gd_sys(g, s_wv, tag);
-                        put_g_sys(g + 2, (unsigned)s_flag, tag);
-                    } else if (t - 1 <= q) {
+                    if (t == 0)
+                        put_gd_sys(g, s_wv, tag | (s_flag >= 0 ? (unsigned)(s_flag - tb * SX_TILE) : SX_NOIDX)); else if (t - 1 <= q) {
                         put_gd_sys(g + 4 + 2 * (t - 1), s_hist[(t - 1) * SX_TILE + s_win], tag);
                     }
                 }
             }
             // ---- entering variable of pivot q + 1: pass 2 over every objective tile
-            if (!gather_tagged<decltype(gather_b), true>(gb, 3 * NBg, gather_b, tag, s_g, &ch->abort_w, &s_ok,
-                                                         timeout)) {
+            if (!gather_tagged<decltype(gather_b), true>(gb, 2 * NBg, gather_b, tag, s_g, &ch->abort_w, &s_ok,
+                                                         timeout, s_pay)) {
                 aborted = true;
                 break;
             }
             double ev = DBL_MAX;
             int ei = -1;
             if (t < NBg) {
-                const double cv = gd(s_g[3 * t], s_g[3 * t + 1]);
+                const double cv = gd(s_g[2 * t], s_g[2 * t + 1]);
+                const unsigned pl = s_pay[t] & SX_NOIDX;
                 if (cmp_eps(cv, ev) < 0) {
                     ev = cv;
-                    ei = (int)s_g[3 * t + 2];
+                    ei = pl == SX_NOIDX ? -1 : t * SX_TILE + (int)pl;
                 }
             }
             block_argmin512(ev, ei, s_v, s_i);
@@ -1302,6 +1321,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
             __syncthreads();
             e = s_win;
             dmin = s_wv;
+            if (liveA) a_pre = T[(size_t)li * ld + c.map(1 + (e >= 0 ? e : 0))];
             if (isA && q + 1 < K && e >= 0 && cmp_eps(dmin, 0.0) < 0) {
                 if (!gather_tagged<decltype(ident), true>(gb + (size_t)(e / SX_TILE) * SX_GB_STRIDE + 4, 2 * (q + 1),
                                                           ident, tag, s_g, &ch->abort_w, &s_ok, timeout)) {
@@ -1329,7 +1349,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
     }
     __syncthreads();
     if (!s_flag) return;
-    const unsigned dtag = B << 8;
+    const unsigned dtag = make_tag(B, 0);
     if (t < W) put_g_sys(pv.gdone[t] + rank, aborted ? 1u : 0u, dtag);
     const bool ok = gather_tagged<decltype(ident), true>(gdone, W, ident, dtag, s_g, &ch->abort_w, &s_ok, timeout);
     if (t != 0) return;
