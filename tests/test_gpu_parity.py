@@ -337,6 +337,19 @@ def test_exchange_path_bit_exact(gpu, W, mode):
     assert got.status == sx.FEASIBLE
 
 
+def test_rccl_one_rank_multirank_paths(gpu):
+    """the multi-GPU code paths over a REAL RCCL communicator (1 rank): the peer-memory fused
+    batch with its IPC-handle exchange, and both per-pivot RCCL exchanges -- whole solves
+    bit-exact vs the oracle (child process: the library's distributed state is process-global)"""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "rccl_one_rank.py")], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "ALL BIT-EXACT" in r.stdout and r.stdout.count("bit-exact") == 9
+
+
 def test_c_caller_drop_in(gpu, tmp_path):
     """a reference-style C program linked against libsimplex_hip.so solves smallProblem.txt"""
     import subprocess
