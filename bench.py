@@ -249,9 +249,14 @@ def main():
         res = sx.twoPhaseMethodEx(prob)
         dt = time.perf_counter() - t0
         prob.close()
+        ph = (ctypes.c_double * 2)()
+        sx.load().simplex_last_phase_seconds(ph)
         full = {"instance": "config3", "seconds": dt, "status": sx.STATUS_NAMES.get(res.status, res.status),
                 "pivots": list(res.pivots), "objective": res.optimal_value,
                 "note": "twoPhaseMethod wall time incl. tableau build from host arrays, both phases and the solution"}
+        full["pivot_loop_s"] = [ph[0], ph[1]]
+        full["pivots_per_s"] = [res.pivots[k] / ph[k] if ph[k] > 0 else None for k in (0, 1)]
+        full["reference_pivots_per_s"] = [8981 / 68.33, 255 / 0.94]  # RTX 2070S, BASELINE.md §1
         full["reference_pivot_loop_s"] = REF_SOLVE["config3"]["pivot_loop_s"]
         full["reference_pivots"] = REF_SOLVE["config3"]["pivots"]
         full["pivots_match_reference"] = list(res.pivots) == REF_SOLVE["config3"]["pivots"]

@@ -63,6 +63,9 @@ void simplex_set_fused(int mode);
 void simplex_set_p2p(int mode);
 /* 1 when the peer-memory fused path passed simplex_dist_init's self-check on every rank */
 int simplex_p2p_ready(void);
+/* wall time (s) of the last twoPhaseMethod call's two pivot loops (solve calls): out[0] phase 1,
+ * out[1] phase 2 -- the reference's TIMER CSV reports the two phases separately */
+void simplex_last_phase_seconds(double *out);
 /* the sweep's grid: waves x (blocks resident on the device) blocks (default 1; <= 0 resets) */
 void simplex_set_update_waves(double waves);
 

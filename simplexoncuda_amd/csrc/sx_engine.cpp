@@ -10,6 +10,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <ctime>
@@ -898,6 +899,12 @@ bool debug_on() {
 }
 
 // ------------------------------------------------------------------ the two-phase driver
+double g_phase_seconds[2] = {0.0, 0.0};  // wall time of the last solve's pivot loops (P1, P2)
+
+static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int two_phase(problem_t *P, double *solution, double *opt, int *base_out, long long *pivots_out,
               long long max_pivots) {
     const int n = P->vars, m = P->constraints;
@@ -925,7 +932,10 @@ int two_phase(problem_t *P, double *solution, double *opt, int *base_out, long l
         print_tableau(stdout, E, E.N1);
     }
     say("Phase 1: Solving auxiliary problem");
+    g_phase_seconds[0] = g_phase_seconds[1] = 0.0;
+    double t0 = now_s();
     const int st1 = E.run_phase(E.N1, max_pivots, &p1, &ch);  // return value ignored by the reference (:258)
+    g_phase_seconds[0] = now_s() - t0;
     if (debug_on()) {
         fprintf(stdout, "\nTableu dopo il lancio del primo solver\n");
         print_tableau(stdout, E, E.N1);
@@ -958,7 +968,9 @@ int two_phase(problem_t *P, double *solution, double *opt, int *base_out, long l
         E.update_objective(E.N2);
         ch.stop(E.s);
         say("Phase 2: Solving original problem");
+        t0 = now_s();
         status = E.run_phase(E.N2, max_pivots, &p2, &ch);
+        g_phase_seconds[1] = now_s() - t0;
         if (debug_on()) {
             fprintf(stdout, "\nTableu dopo seconda esecuzione del solver\n");
             print_tableau(stdout, E, E.N2);
@@ -1008,6 +1020,10 @@ void simplex_set_alias(int on) { g_cfg.alias = on ? 1 : 0; }
 void simplex_set_fused(int mode) { g_cfg.fused = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_p2p(int mode) { g_cfg.p2p = mode < 0 ? -1 : (mode ? 1 : 0); }
 int simplex_p2p_ready(void) { return g_cfg.p2p_ready ? 1 : 0; }
+void simplex_last_phase_seconds(double *out) {
+    out[0] = g_phase_seconds[0];
+    out[1] = g_phase_seconds[1];
+}
 void simplex_set_update_waves(double waves) { sx_set_update_waves((float)waves); }
 void simplex_set_exchange_mode(int mode) { g_cfg.exchange_mode = (mode >= 0 && mode <= 2) ? mode : 0; }
 void simplex_set_timer_dir(const char *dir) { g_cfg.timer_dir = dir ? dir : ""; }
