@@ -52,6 +52,10 @@ void simplex_set_force_exchange(int on);
 void simplex_set_exchange_mode(int mode);
 /* store each phase-1 artificial column as its (bit-identical) slack column: 1 on (default), 0 off */
 void simplex_set_alias(int on);
+/* slack compaction (default on): the slack column of a row that has never left the basis is
+ * an untouched unit vector, so it is kept past the swept block of the tableau and skipped by
+ * every sweep -- bit-identical results; active only when no row is negated (b >= 0) */
+void simplex_set_compact(int on);
 /* one shard: run each batch of pivots as ONE resident launch (ratio tiles + objective-row tiles
  * handing off through write-through records) instead of two launches per pivot;
  * -1 auto (default: when the grid fits the device), 0 off */
@@ -95,9 +99,11 @@ typedef struct {
     long long update_launches; /* sweeps timed (those that applied at least one pivot) */
     int status;                /* phase status after the call (SIMPLEX_NOT_ENDED while running) */
     int width;                 /* tableau width N of the phase (reference counting) */
-    int stored_width;          /* columns actually stored and swept (artificials alias slacks in phase 1) */
+    int stored_width;          /* columns stored (artificials alias slacks in phase 1); a sweep moves all
+                                * of them, or 1+n+(touched slacks) under slack compaction */
     long long local_rows;      /* constraint rows owned by this process */
-    double update_bytes;       /* bytes per sweep: 16 * local_rows * stored_width (read + write of T) */
+    double update_bytes;       /* bytes per sweep: 16 * local_rows * swept width (read + write of T),
+                                * the mean over the timed sweeps */
     long long swept_pivots;    /* timed sweeps: pivots they applied */
     double swept_bytes;        /* timed sweeps: bytes they moved */
 } simplex_timing_t;
@@ -111,6 +117,12 @@ simplex_session *simplex_session_open_generated(int n, int m, unsigned int seed,
  * time_updates = s > 0 brackets every s-th sweep with HIP events */
 int simplex_session_pivots(simplex_session *s, long long k, int time_updates, simplex_timing_t *out);
 double simplex_session_objective(simplex_session *s);   /* d[0] */
+/* the resident tableau in logical column order (m rows of the phase's width at stride ld),
+ * the objective row d and the basis; returns the width, or -1 when rows live on other ranks
+ * or the buffer is too narrow */
+long long simplex_session_tableau(simplex_session *s, double *T, long long ld, double *d, int *base);
+/* slack columns the sweeps currently move (m without slack compaction) */
+long long simplex_session_active_slacks(simplex_session *s);
 long long simplex_session_total_pivots(simplex_session *s);
 /* per timed sweep of the last simplex_session_pivots call: pivots it applied and its
  * duration in microseconds; returns the number of sweeps logged (at most cap are copied) */

@@ -8,6 +8,6 @@ from .api import (  # noqa: F401
     DEGENERATE, FEASIBLE, HANG, INFEASIBLE, NOT_ENDED, NUMERIC_FAIL, PIVOT_CAP, RAND_GLIBC, RAND_MSVC,
     STATUS_NAMES, UNBOUNDED, Problem, Result, Session, dev_argmin, dev_build_phase1, dev_pivots,
     dev_build_phase1_generated, dev_update_objective, generateRandomProblem, generateRandomProblemDevice, printProblemToStream, readProblemFromFile,
-    readRandomProblemFromFile, set_alias, set_batch, set_fused, set_p2p, p2p_ready, set_update_waves, set_exchange_mode, set_force_exchange, set_snake, set_store_sc1, set_update_rows, set_verbose, set_virtual_ranks,
+    readRandomProblemFromFile, set_alias, set_batch, set_compact, set_fused, set_p2p, p2p_ready, set_update_waves, set_exchange_mode, set_force_exchange, set_snake, set_store_sc1, set_update_rows, set_verbose, set_virtual_ranks,
     twoPhaseMethod, twoPhaseMethodEx)
 from ._lib import LIB_PATH, load  # noqa: F401

@@ -96,6 +96,7 @@ SIGNATURES = {
     "simplex_set_force_exchange": (None, [ctypes.c_int]),
     "simplex_set_exchange_mode": (None, [ctypes.c_int]),
     "simplex_set_alias": (None, [ctypes.c_int]),
+    "simplex_set_compact": (None, [ctypes.c_int]),
     "simplex_set_fused": (None, [ctypes.c_int]),
     "simplex_last_phase_seconds": (None, [ctypes.POINTER(ctypes.c_double)]),
     "simplex_set_p2p": (None, [ctypes.c_int]),
@@ -117,6 +118,10 @@ SIGNATURES = {
     "simplex_session_pivots": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int,
                                               ctypes.POINTER(TimingT)]),
     "simplex_session_objective": (ctypes.c_double, [ctypes.c_void_p]),
+    "simplex_session_tableau": (ctypes.c_longlong, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                                    ctypes.c_longlong, ctypes.POINTER(ctypes.c_double),
+                                                    ctypes.POINTER(ctypes.c_int)]),
+    "simplex_session_active_slacks": (ctypes.c_longlong, [ctypes.c_void_p]),
     "simplex_session_total_pivots": (ctypes.c_longlong, [ctypes.c_void_p]),
     "simplex_session_launch_log": (ctypes.c_longlong, [ctypes.c_void_p, c_ll_p, c_double_p, ctypes.c_longlong]),
     "simplex_session_close": (None, [ctypes.c_void_p]),

@@ -211,6 +211,20 @@ class Session:
     def objective(self):
         return self._lib.simplex_session_objective(self._h)
 
+    def tableau(self, m, width):
+        """(T, d, base): the resident tableau in logical column order (rows on this process)."""
+        T = np.zeros((m, width), dtype=np.float64)
+        d = np.zeros(width, dtype=np.float64)
+        base = np.zeros(m, dtype=np.int32)
+        w = self._lib.simplex_session_tableau(self._h, _dp(T), width, _dp(d), _ip(base))
+        if w != width:
+            raise RuntimeError(f"simplex_session_tableau: width {w}, expected {width}")
+        return T, d, base
+
+    def active_slacks(self):
+        """Slack columns the sweeps move (m without slack compaction)."""
+        return self._lib.simplex_session_active_slacks(self._h)
+
     def total_pivots(self):
         return self._lib.simplex_session_total_pivots(self._h)
 
@@ -287,6 +301,11 @@ def set_exchange_mode(mode):
 
 def set_alias(on):
     _lib.load().simplex_set_alias(1 if on else 0)
+
+
+def set_compact(on):
+    """Slack compaction (default on): sweeps skip slack columns no pivot has touched."""
+    _lib.load().simplex_set_compact(1 if on else 0)
 
 
 def set_fused(mode):

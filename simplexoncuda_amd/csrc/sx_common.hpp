@@ -105,12 +105,23 @@ void sx_fatal(const char *msg, const char *file, int line);
 // to its slack column n+k (both unit vectors, both negated by the b<0 quirk) and receives
 // exactly the same IEEE operations at every pivot, so the two stay bit-identical: only
 // Ns = 1+n+m columns are stored and logical column j >= art0 reads stored column j - shift.
+//
+// Slack compaction: while row k has never been a leaving row, its slack
+// column is exactly e_k and every pivot leaves it bit-identical (its pivot-row entry is +0).
+// Such columns are kept at the end of the stored slack block and the sweep stops before
+// them: stored slack position s0 + perm[k] holds logical slack k, and the first *nact
+// positions are the columns that have ever been touched.
 struct Cols {
     int N;      // logical columns of the phase (reference width: 1+n+2m or 1+n+m)
-    int Ns;     // stored columns (swept by the update)
+    int Ns;     // stored columns
     int art0;   // first aliased logical column, or INT_MAX
     int shift;  // alias distance (m)
-    __host__ __device__ __forceinline__ int map(int j) const { return j >= art0 ? j - shift : j; }
+    int s0;     // first slack column (1+n)
+    const int *perm;  // device: logical slack -> stored slack offset, or null (identity)
+    __host__ __device__ __forceinline__ int map(int j) const {
+        const int k = j >= art0 ? j - shift : j;
+        return (perm && k >= s0) ? s0 + perm[k - s0] : k;
+    }
 };
 
 // ---- kernel launchers (sx_kernels.hip) ----
@@ -132,8 +143,13 @@ void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, Cols c
 void sx_launch_pivot_row(const double *T, int rows, int row0, size_t ld, Cols c, double *d, const double *prow_buf,
                          size_t prow_stride, const double *colE, DevState *st, const Pending &pd,
                          TilePart *enter_parts, hipStream_t s);
-void sx_launch_sweep(double *T, int rows, size_t ld, int Ns, const Pending &pd, const DevState *st, int rev,
-                     SweepCfg cfg, hipStream_t s);
+// nact (device, or null): sweep only the columns [0, s0 + *nact) (slack compaction)
+void sx_launch_sweep(double *T, int rows, size_t ld, int Ns, const int *nact, int s0, const Pending &pd,
+                     const DevState *st, int rev, SweepCfg cfg, hipStream_t s);
+// slack compaction, after a batch's selections and before its sweep: move the slack column
+// of every row that left the basis for the first time into the swept block
+void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, int m, double *T, int rows, int row0,
+                        size_t ld, int s0, const Pending &pd, const DevState *st, hipStream_t s);
 // fused batch of up to k pivots on one shard (ratio tiles + objective tiles in one resident
 // grid); returns false (nothing launched) when the grid cannot be resident at once
 bool sx_batch_fits(int rows, Cols c, int k);

@@ -63,6 +63,7 @@ struct Config {
     std::string timer_dir;   // non-empty: write the reference's TIMER CSV there
     int exchange_mode = 0;   // 0 auto, 1 tile allgather + row allreduce, 2 row-gather
     int alias = 1;           // store phase-1 artificial columns as their slack columns
+    int compact = 1;         // sweep only the slack columns pivots have touched (when exact)
     int fused = -1;          // whole batches in one resident launch: -1 auto (one shard), 0 off
     int p2p = -1;            // several shards: fused batches exchanging over peer memory: -1 auto, 0 off, 1 force
     bool p2p_ready = false;  // RCCL ranks: the peer-memory path passed the start-up self-check
@@ -166,6 +167,10 @@ struct Shard {
     double *slot_send = nullptr;  // row-gather: per tile [TilePart header | winner row]
     double *slot_all = nullptr;
     double *U = nullptr;              // pending pivot rows [SX_KMAX][ld]
+    int *perm = nullptr;              // slack compaction (Cols): logical slack -> stored offset [m]
+    int *iperm = nullptr;             //   stored offset -> logical slack [m]
+    unsigned char *act = nullptr;     //   slack column ever touched [m]
+    int *nact = nullptr;              //   touched slack columns (the swept block's width past 1+n)
     double *F = nullptr;              // pending row factors [rows][SX_KMAX]
     PivRec *recs = nullptr;           // pending pivot records [SX_KMAX]
     unsigned long long *PM = nullptr; // [rows] pending leaving-row slots (batch-tagged)
@@ -197,6 +202,7 @@ class Engine {
     size_t slot_stride = 0;  // doubles per row-gather slot (16-byte header + ld)
     int N1 = 0, N2 = 0, N = 0;
     bool alias = false;    // phase-1 artificial columns stored as their slack columns (sx_common.hpp Cols)
+    bool compact = false;  // untouched slack columns kept past the swept block (sx_common.hpp Cols)
     int Ns1 = 0;           // stored columns in phase 1
     size_t ld = 0;         // row stride in doubles
     int rpr = 0;           // rows per rank (multiple of 512)
@@ -464,7 +470,8 @@ class Engine {
                         (void *)x.slot_send, (void *)x.slot_all, (void *)x.U, (void *)x.F, (void *)x.recs, (void *)x.PM,
                         (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
                         (void *)x.rhs_all, (void *)x.base, (void *)x.enter_parts, (void *)x.tiles_local, (void *)x.chan,
-                        (void *)x.ga, (void *)x.gb, (void *)x.gdone,
+                        (void *)x.ga, (void *)x.gb, (void *)x.gdone, (void *)x.perm, (void *)x.iperm,
+                        (void *)x.act, (void *)x.nact,
                         (void *)x.tiles_all, (void *)x.st})
             if (p) (void)hipFree(p);
     }
@@ -492,6 +499,9 @@ class Engine {
             if (n > 0)
                 SX_HIP(hipMemcpy(c_dev, P->objectiveFunction, sizeof(double) * n, hipMemcpyHostToDevice));
         }
+        bool nonneg = true;  // no row negated (k_fill_rows negates b < -eps; b < 0 is stricter)
+        for (int i = 0; i < m; ++i) nonneg = nonneg && !(P->knownTermsVector[i] < 0.0);
+        set_compact(nonneg);
     }
 
     // the same tableau as build_phase1(generateRandomProblem(n, m, seed, lo, hi)), synthesised
@@ -510,6 +520,7 @@ class Engine {
         }
         SX_HIP(hipStreamSynchronize(s));
         (void)hipFree(b_dev);
+        set_compact(lo >= 0);  // b in [lo, hi]: no row negated
     }
 
     // ---------------------------------------------------------------- collectives
@@ -573,7 +584,7 @@ class Engine {
         }
         if (xchg) allgather_doubles(&Shard::gemv_local, &Shard::gemv_all, part);
         const int nblk = (m + SX_TILE - 1) / SX_TILE;
-        for (auto &x : sh) sx_launch_gemv_apply(x.d, c, xchg ? x.gemv_all : x.gemv_local, nblk, s);
+        for (auto &x : sh) sx_launch_gemv_apply(x.d, cols(width, x), xchg ? x.gemv_all : x.gemv_local, nblk, s);
     }
 
     void phase2_costs() {
@@ -588,7 +599,50 @@ class Engine {
         c.Ns = a ? Ns1 : width;
         c.art0 = a ? 1 + n + m : 0x7fffffff;
         c.shift = m;
+        c.s0 = 1 + n;
+        c.perm = nullptr;
         return c;
+    }
+    // the same, with the shard's slack permutation (device pointer) when compacting
+    Cols cols(int width, const Shard &x) const {
+        Cols c = cols(width);
+        if (compact) c.perm = x.perm;
+        return c;
+    }
+
+    // Slack compaction (sx_common.hpp Cols): valid while every slack column is built as +e_k
+    // -- no row negated by the b < 0 quirk (its -0.0 entries would let a pivot flip the sign
+    // of a zero) -- and phase 1 stores artificials as their slacks.  Off for a caller's
+    // tableau (upload).
+    void set_compact(bool on) {
+        on = on && alias && m > 0 && g_cfg.compact != 0;
+        if (on) {
+            std::vector<int> id((size_t)m);
+            for (int k = 0; k < m; ++k) id[k] = k;
+            for (auto &x : sh) {
+                if (!x.perm) {
+                    x.perm = dalloc<int>(m);
+                    x.iperm = dalloc<int>(m);
+                    x.act = dalloc<unsigned char>(m);
+                    x.nact = dalloc<int>(1);
+                }
+                SX_HIP(hipMemcpyAsync(x.perm, id.data(), sizeof(int) * m, hipMemcpyHostToDevice, s));
+                SX_HIP(hipMemcpyAsync(x.iperm, id.data(), sizeof(int) * m, hipMemcpyHostToDevice, s));
+                SX_HIP(hipMemsetAsync(x.act, 0, m, s));
+                SX_HIP(hipMemsetAsync(x.nact, 0, sizeof(int), s));
+            }
+            SX_HIP(hipStreamSynchronize(s));
+        }
+        compact = on;
+    }
+
+    // swept slack columns (m when not compacting)
+    int active_slacks() {
+        if (!compact) return m;
+        int v = 0;
+        SX_HIP(hipMemcpyAsync(&v, sh[0].nact, sizeof(int), hipMemcpyDeviceToHost, s));
+        SX_HIP(hipStreamSynchronize(s));
+        return v;
     }
 
     // ---------------------------------------------------------------- one pivot
@@ -632,23 +686,22 @@ class Engine {
     // one pivot into slot q_host of the current batch: ratio test + selection, the pivot
     // row, the objective row and the next entering variable.  The tableau is not touched.
     void enqueue_pivot() {
-        const Cols c = cols(N);
         for (auto &x : sh)
             sx_launch_ratio_select(x.T, x.rows, x.row0, ld, x.tiles_local, x.colE, x.st, x.base, !xchg,
-                                   rowgather ? x.slot_send : nullptr, slot_stride, c, pending(x), s);
+                                   rowgather ? x.slot_send : nullptr, slot_stride, cols(N, x), pending(x), s);
         if (rowgather) {
             allgather_slots();
             for (auto &x : sh) sx_launch_select_gathered(x.slot_all, slot_stride, W * slots, x.base, x.st, pending(x), s);
         } else if (xchg) {
             allgather_tiles();
             for (auto &x : sh)
-                sx_launch_select_row(x.T, x.rows, x.row0, ld, c, x.tiles_all, W * slots, x.prow_send, x.base, x.st,
+                sx_launch_select_row(x.T, x.rows, x.row0, ld, cols(N, x), x.tiles_all, W * slots, x.prow_send, x.base, x.st,
                                      pending(x), s);
             allreduce_prow();
         }
         for (auto &x : sh) {
             const double *pb = rowgather ? x.slot_all : (xchg ? x.prow : nullptr);
-            sx_launch_pivot_row(x.T, x.rows, x.row0, ld, c, x.d, pb, rowgather ? slot_stride : 0, x.colE, x.st,
+            sx_launch_pivot_row(x.T, x.rows, x.row0, ld, cols(N, x), x.d, pb, rowgather ? slot_stride : 0, x.colE, x.st,
                                 pending(x), x.enter_parts, s);
         }
         ++q_host;
@@ -668,7 +721,7 @@ class Engine {
         if (q_host != 0) SX_FATAL("fused batch inside a started batch");
         if (!xchg) {
             Shard &x = sh[0];
-            sx_launch_batch(x.T, x.rows, ld, cols(N), x.d, x.base, x.st, pending(x), k, x.chan, x.ga, x.gb, stamps,
+            sx_launch_batch(x.T, x.rows, ld, cols(N, x), x.d, x.base, x.st, pending(x), k, x.chan, x.ga, x.gb, stamps,
                             s);
         } else {
             // every rank's batch runs at once (virtual shards: one stream each, forked from and
@@ -684,7 +737,7 @@ class Engine {
                     SX_HIP(hipStreamWaitEvent(xs, ev_fork, 0));
                 }
                 const int tb0 = (int)((long long)x.rank * NBg / W), tb1 = (int)((long long)(x.rank + 1) * NBg / W);
-                sx_launch_batch_mr(x.T, x.rows, x.row0, rpr, ld, cols(N), x.d, x.base, x.st, pending(x), k, slots, W,
+                sx_launch_batch_mr(x.T, x.rows, x.row0, rpr, ld, cols(N, x), x.d, x.base, x.st, pending(x), k, slots, W,
                                    x.rank, tb0, tb1, x.chan, x.ga, x.gb, x.gdone, pv, timeout, xs);
                 if (!rccl) SX_HIP(hipEventRecord(ev_join[i], xs));
             }
@@ -701,7 +754,12 @@ class Engine {
         const SweepCfg cfg = sweep_cfg(q_host);
         const int rev = (int)(sweeps & 1);  // alternate the sweep direction (Infinity-Cache reuse)
         if (ev0) SX_HIP(hipEventRecord(ev0, s));
-        for (auto &x : sh) sx_launch_sweep(x.T, x.rows, ld, cols(N).Ns, pending(x), x.st, rev, cfg, s);
+        for (auto &x : sh) {
+            if (compact) sx_launch_activate(x.perm, x.iperm, x.act, x.nact, m, x.T, x.rows, x.row0, ld, 1 + n, pending(x),
+                                            x.st, s);
+            sx_launch_sweep(x.T, x.rows, ld, cols(N).Ns, compact ? x.nact : nullptr, 1 + n, pending(x), x.st, rev, cfg,
+                            s);
+        }
         if (ev1) SX_HIP(hipEventRecord(ev1, s));
         ++sweeps;
         // batch ids tag the fused kernel's granules as (id << 8 | slot) in 32 bits: 24-bit ids, never 0
@@ -826,6 +884,13 @@ class Engine {
     void download(double *T_host, size_t ld_host, int width, double *d_host) {
         const Cols c = cols(width);
         std::vector<double> tmp;
+        std::vector<int> perm;
+        if (compact) {
+            perm.resize((size_t)m);
+            SX_HIP(hipMemcpyAsync(perm.data(), sh[0].perm, sizeof(int) * m, hipMemcpyDeviceToHost, s));
+            SX_HIP(hipStreamSynchronize(s));
+        }
+        const int s0 = 1 + n;
         for (auto &x : sh) {
             if (x.rows <= 0) continue;
             tmp.assign((size_t)x.rows * c.Ns, 0.0);
@@ -835,7 +900,10 @@ class Engine {
             for (int i = 0; i < x.rows; ++i) {
                 double *dst = T_host + (size_t)(x.row0 + i) * ld_host;
                 const double *src = tmp.data() + (size_t)i * c.Ns;
-                for (int j = 0; j < width; ++j) dst[j] = src[c.map(j)];
+                for (int j = 0; j < width; ++j) {
+                    const int k = c.map(j);
+                    dst[j] = src[(compact && k >= s0) ? s0 + perm[k - s0] : k];
+                }
             }
         }
         if (d_host) SX_HIP(hipMemcpyAsync(d_host, sh[0].d, sizeof(double) * width, hipMemcpyDeviceToHost, s));
@@ -845,6 +913,7 @@ class Engine {
     // logical columns in; with aliasing only the stored columns are taken (the caller's
     // artificial columns must equal the slack columns, checked by the callers below)
     void upload(const double *T_host, size_t ld_host, int width, const double *d_host, const int *base_host) {
+        set_compact(false);  // a caller's tableau: any column may be touched
         const Cols c = cols(width);
         for (auto &x : sh) {
             if (x.rows > 0)
@@ -1017,6 +1086,7 @@ void simplex_set_device(int device) {
 void simplex_set_virtual_ranks(int world) { g_cfg.virtual_ranks = world > 1 ? world : 1; }
 void simplex_set_force_exchange(int on) { g_cfg.force_exchange = on ? 1 : 0; }
 void simplex_set_alias(int on) { g_cfg.alias = on ? 1 : 0; }
+void simplex_set_compact(int on) { g_cfg.compact = on ? 1 : 0; }
 void simplex_set_fused(int mode) { g_cfg.fused = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_p2p(int mode) { g_cfg.p2p = mode < 0 ? -1 : (mode ? 1 : 0); }
 int simplex_p2p_ready(void) { return g_cfg.p2p_ready ? 1 : 0; }
@@ -1213,8 +1283,9 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
     std::vector<hipEvent_t> evs(2 * (size_t)nt);
     for (auto &e : evs) SX_HIP(hipEventCreate(&e));
     std::vector<unsigned> ids((size_t)(nt > 0 ? nt : 1), 0u);
-    // (batch_tag, batch_count) after each timed sweep: the pivots it applied
-    int *tag_dev = dalloc<int>((size_t)(nt > 0 ? nt : 1) * 2);
+    // (batch_tag, batch_count, swept slack columns) after each timed sweep: the pivots it
+    // applied and its width
+    int *tag_dev = dalloc<int>((size_t)(nt > 0 ? nt : 1) * 3);
     hipEvent_t w0, w1;
     SX_HIP(hipEventCreate(&w0));
     SX_HIP(hipEventCreate(&w1));
@@ -1227,8 +1298,11 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
         E.enqueue_sweep(timed ? evs[2 * ntimed] : nullptr, timed ? evs[2 * ntimed + 1] : nullptr);
         if (timed) {
             ids[(size_t)ntimed] = id;
-            SX_HIP(hipMemcpyAsync(tag_dev + 2 * ntimed, &E.sh[0].st->batch_tag, 2 * sizeof(int),
+            SX_HIP(hipMemcpyAsync(tag_dev + 3 * ntimed, &E.sh[0].st->batch_tag, 2 * sizeof(int),
                                   hipMemcpyDeviceToDevice, E.s));
+            if (E.compact)
+                SX_HIP(hipMemcpyAsync(tag_dev + 3 * ntimed + 2, E.sh[0].nact, sizeof(int), hipMemcpyDeviceToDevice,
+                                      E.s));
             ++ntimed;
         }
         ++nsw;
@@ -1261,25 +1335,29 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
     for (auto &x : E.sh) rows += x.rows;
     t.local_rows = rows;
     t.stored_width = E.cols(E.N).Ns;
-    t.update_bytes = 16.0 * (double)rows * (double)t.stored_width;
-    std::vector<int> tags((size_t)(nt > 0 ? nt : 1) * 2, 0);
+    std::vector<int> tags((size_t)(nt > 0 ? nt : 1) * 3, 0);
     SX_HIP(hipMemcpy(tags.data(), tag_dev, sizeof(int) * tags.size(), hipMemcpyDeviceToHost));
     (void)hipFree(tag_dev);
     S->log_rows.clear();
     S->log_us.clear();
     for (long long i = 0; i < ntimed; ++i) {
         // a sweep whose batch selected no pivot (the phase had ended) is a no-op launch
-        const int applied = (unsigned)tags[2 * i] == ids[(size_t)i] ? tags[2 * i + 1] : 0;
+        const int applied = (unsigned)tags[3 * i] == ids[(size_t)i] ? tags[3 * i + 1] : 0;
         if (applied <= 0) continue;
         float us = 0.f;
         SX_HIP(hipEventElapsedTime(&us, evs[2 * i], evs[2 * i + 1]));
+        // columns the sweep moved: all stored ones, or 1+n+nact under slack compaction
+        const int width = E.compact ? std::min(t.stored_width, 1 + E.n + tags[3 * i + 2]) : t.stored_width;
         t.update_ms += us;
         t.update_launches += 1;
         t.swept_pivots += applied;
-        t.swept_bytes += t.update_bytes;
+        t.swept_bytes += 16.0 * (double)rows * (double)width;
         S->log_rows.push_back(applied);
         S->log_us.push_back(1e3 * (double)us);
     }
+    // bytes per timed sweep (their mean, when compaction grows the swept block)
+    t.update_bytes = t.update_launches ? t.swept_bytes / (double)t.update_launches
+                                       : 16.0 * (double)rows * (double)t.stored_width;
     for (auto &e : evs) (void)hipEventDestroy(e);
     (void)hipEventDestroy(w0);
     (void)hipEventDestroy(w1);
@@ -1289,6 +1367,16 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
 }
 
 double simplex_session_objective(simplex_session *S) { return S->E->read_d0(); }
+
+long long simplex_session_tableau(simplex_session *S, double *T, long long ld, double *d, int *base) {
+    Engine &E = *S->E;
+    if (E.rccl || ld < E.N) return -1;
+    E.download(T, (size_t)ld, E.N, d);
+    E.read_base(base);
+    return E.N;
+}
+
+long long simplex_session_active_slacks(simplex_session *S) { return S->E->active_slacks(); }
 long long simplex_session_total_pivots(simplex_session *S) { return S->E->read_state().pivots; }
 
 int simplex_session_stamps(simplex_session *S, int k, unsigned long long *out) {

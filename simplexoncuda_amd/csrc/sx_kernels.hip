@@ -563,7 +563,7 @@ __global__ __launch_bounds__(256) void k_pivot_row(const double *__restrict__ T,
     int i0 = -1, i1 = -1;
     if (ia < L) {
         const int j = 1 + ia;
-        if (j < c.Ns) Uq[j] = ua;
+        if (j < c.Ns) Uq[col[2]] = ua;  // stored position (slack compaction)
         const double x = fma(fd, ua, d[j]);
         d[j] = x;
         if (cmp_eps(x, v0) < 0) {
@@ -573,7 +573,7 @@ __global__ __launch_bounds__(256) void k_pivot_row(const double *__restrict__ T,
     }
     if (ib < L) {
         const int j = 1 + ib;
-        if (j < c.Ns) Uq[j] = ub;
+        if (j < c.Ns) Uq[col[3]] = ub;
         const double x = fma(fd, ub, d[j]);
         d[j] = x;
         if (cmp_eps(x, v1) < 0) {
@@ -961,7 +961,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                         u = fma(s_fr[s], s_hist[s * SX_TILE + t], u);
                 }
                 s_hist[q * SX_TILE + t] = u;
-                if (liveB && 1 + ia < c.Ns) U[(size_t)q * ld + 1 + ia] = u;
+                if (liveB && 1 + ia < c.Ns) U[(size_t)q * ld + mj] = u;
                 const double fd = -dmin / p;  // updateCostsVector, solver.cu:48-56
                 if (tb == 0 && t == 0) d0 = fma(fd, br, d0);
                 double v = DBL_MAX;
@@ -1270,7 +1270,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
                 }
                 s_hist[q * SX_TILE + t] = u;
                 if (liveB && 1 + ia < c.Ns)
-                    for (int k = 0; k < W; ++k) st_sys(pv.U[k] + (size_t)q * ld + 1 + ia, u);
+                    for (int k = 0; k < W; ++k) st_sys(pv.U[k] + (size_t)q * ld + mj, u);
                 const double fd = -dmin / p;  // updateCostsVector, solver.cu:48-56
                 if (tb == 0 && t == 0) d0 = fma(fd, br, d0);
                 double v = DBL_MAX;
@@ -1388,15 +1388,22 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 template <int KT, int RB, bool SC1>
 __global__ __launch_bounds__(256) void k_sweep(double *__restrict__ T, int rows, size_t ld, int Ns,
+                                               const int *__restrict__ nact, int s0,
                                                const double *__restrict__ F, const double *__restrict__ U,
                                                const PivRec *__restrict__ recs,
                                                const unsigned long long *__restrict__ PM,
                                                const DevState *__restrict__ st, unsigned B, int rev) {
     const int cnt = st->batch_tag == B ? st->batch_count : 0;
     if (cnt <= 0) return;
+    // slack compaction: the columns past s0 + *nact are untouched unit vectors (not swept);
+    // the grid's blocks are re-dealt over the active column tiles
+    if (nact && s0 + *nact < Ns) Ns = s0 + *nact;
     const int cb = (Ns + 511) / 512;
-    if ((int)blockIdx.x >= cb) return;
-    const int bx = rev ? cb - 1 - (int)blockIdx.x : (int)blockIdx.x;
+    const int lin = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    const int G = (int)(gridDim.x * gridDim.y) / cb;
+    const int tile = lin % cb, gy = lin / cb;
+    if (gy >= G) return;
+    const int bx = rev ? cb - 1 - tile : tile;
     const int j = (bx * 256 + (int)threadIdx.x) * 2;
     if (j >= Ns) return;  // the thread of an odd last column moves (j, j+1): j+1 < ld is padding
     const unsigned mask = slot_mask(cnt);
@@ -1404,10 +1411,9 @@ __global__ __launch_bounds__(256) void k_sweep(double *__restrict__ T, int rows,
 #pragma unroll
     for (int s = 0; s < KT; ++s)
         u[s] = s < cnt ? *reinterpret_cast<const double2 *>(U + (size_t)s * ld + j) : make_double2(0.0, 0.0);
-    const int G = gridDim.y;
     const int ng = (rows + RB - 1) / RB;
     const int oob = (int)(ld * 8);
-    for (int g = blockIdx.y; g < ng; g += G) {
+    for (int g = gy; g < ng; g += G) {
         const int i0 = (rev ? ng - 1 - g : g) * RB;
         double2 x[RB];
 #pragma unroll
@@ -1464,6 +1470,117 @@ __global__ __launch_bounds__(256) void k_sweep(double *__restrict__ T, int rows,
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, j * 8, 0, SC1 ? 16 : 0);
         }
     }
+}
+
+// Slack compaction (sx_common.hpp Cols), between a batch's selections and its
+// sweep.  The first time row r leaves the basis, its slack column -- still the unit vector e_r
+// as built, never swept -- is exchanged with the slack column at the first untouched stored
+// position s0 + nact (also a unit vector), so the swept block [0, s0 + nact) grows by one.
+// The exchanges of one batch are resolved in slot order by wave 0, one list entry per lane
+// (stored offset, slack held before the batch, slack held now); their net effect is then
+// applied at once: to the pending pivot rows U[s] (whose entries at the two columns are
+// the leaving rows' current values there), to T (zeros and ones of the unit vectors, this
+// shard's rows only) and to perm / iperm / act / nact.  The shards run it alike.
+__global__ __launch_bounds__(256) void k_activate(int *__restrict__ perm, int *__restrict__ iperm,
+                                                  unsigned char *__restrict__ act, int *__restrict__ nact_p, int m,
+                                                  double *__restrict__ T, int rows, int row0, size_t ld, int s0,
+                                                  double *__restrict__ U, const PivRec *__restrict__ recs,
+                                                  const DevState *__restrict__ st, unsigned B) {
+    const int cnt = st->batch_tag == B ? st->batch_count : 0;
+    if (cnt <= 0) return;
+    const int t = threadIdx.x;
+    const int na0 = *nact_p;
+    __shared__ int s_pl[64], s_ol[64], s_cl[64], s_src[64];
+    __shared__ int s_nl, s_added;
+    __shared__ double s_u[SX_KMAX * 64];
+    if (t < 64) {
+        // lane s: slot s's leaving row, whether its slack was ever touched, its stored offset,
+        // and the slack at window offset na0 + s
+        int r = 0, a = 1, pr = 0, win = -1;
+        if (t < cnt) {
+            r = recs[t].r;
+            a = act[r];
+            pr = perm[r];
+            if (na0 + t < m) win = iperm[na0 + t];
+        }
+        int pl = -1, ol = -1, cl = -1;  // this lane's list entry
+        int nl = 0, added = 0;
+        for (int s = 0; s < cnt; ++s) {
+            const int rs = __shfl(r, s);
+            if (__shfl(a, s)) continue;  // its slack was touched in an earlier batch
+            // already moved into the window in this batch?
+            if (__ballot(t < nl && cl == rs && pl >= na0 && pl < na0 + added)) continue;
+            const unsigned long long hP = __ballot(t < nl && cl == rs);
+            int iP;
+            if (hP) {
+                iP = __ffsll((long long)hP) - 1;
+            } else {  // untouched in this batch: at its pre-batch offset
+                iP = nl++;
+                const int P = __shfl(pr, s);
+                if (t == iP) {
+                    pl = P;
+                    ol = rs;
+                    cl = rs;
+                }
+            }
+            const int pos = na0 + added;
+            const unsigned long long hW = __ballot(t < nl && pl == pos);
+            int iW;
+            if (hW) {
+                iW = __ffsll((long long)hW) - 1;
+            } else {
+                iW = nl++;
+                const int w = __shfl(win, added);
+                if (t == iW) {
+                    pl = pos;
+                    ol = w;
+                    cl = w;
+                }
+            }
+            const int cP = __shfl(cl, iP), cW = __shfl(cl, iW);
+            if (t == iP) cl = cW;
+            if (t == iW) cl = cP;
+            ++added;
+        }
+        if (t < nl) {
+            s_pl[t] = pl;
+            s_ol[t] = ol;
+            s_cl[t] = cl;
+        }
+        if (t == 0) {
+            s_nl = nl;
+            s_added = added;
+        }
+    }
+    __syncthreads();
+    const int nl = s_nl;
+    if (nl == 0) return;
+    if (t < nl) {  // the entry whose pre-batch slack this position holds now
+        int j = 0;
+        while (s_ol[j] != s_cl[t]) ++j;
+        s_src[t] = j;
+    }
+    __syncthreads();
+    for (int k = t; k < cnt * nl; k += blockDim.x) {
+        const int s = k / nl, i = k - s * nl;
+        s_u[k] = U[(size_t)s * ld + s0 + s_pl[s_src[i]]];
+    }
+    __syncthreads();
+    for (int k = t; k < cnt * nl; k += blockDim.x) {
+        const int s = k / nl, i = k - s * nl;
+        U[(size_t)s * ld + s0 + s_pl[i]] = s_u[k];
+    }
+    if (t < nl) {
+        const int x = s_pl[t], o = s_ol[t], c = s_cl[t];
+        if (o != c) {
+            if (o >= row0 && o < row0 + rows) T[(size_t)(o - row0) * ld + s0 + x] = 0.0;
+            if (c >= row0 && c < row0 + rows) T[(size_t)(c - row0) * ld + s0 + x] = 1.0;
+        }
+        iperm[x] = c;
+        perm[c] = x;
+        if (x >= na0 && x < na0 + s_added) act[c] = 1;
+    }
+    if (t == 0) *nact_p = na0 + s_added;
 }
 
 // Virtual-rank "allreduce": out = sum of the shards' contributions in rank order.  Exact,
@@ -1663,40 +1780,46 @@ static int row_slots(int capacity, int col_blocks, int rows, int rb) {
 }
 
 template <int KT, int RB, bool SC1>
-static void launch_sweep_t(double *T, int rows, size_t ld, int Ns, const Pending &pd, const DevState *st, int rev,
-                           hipStream_t s) {
+static void launch_sweep_t(double *T, int rows, size_t ld, int Ns, const int *nact, int s0, const Pending &pd,
+                           const DevState *st, int rev, hipStream_t s) {
     const int cb = (Ns + 511) / 512;
     dim3 grid(cb, row_slots(sweep_capacity(k_sweep<KT, RB, SC1>), cb, rows, RB));
-    k_sweep<KT, RB, SC1><<<grid, 256, 0, s>>>(T, rows, ld, Ns, pd.F, pd.U, pd.recs, pd.PM, st, pd.batch, rev);
+    k_sweep<KT, RB, SC1><<<grid, 256, 0, s>>>(T, rows, ld, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st, pd.batch,
+                                              rev);
 }
 
 template <int KT>
-static void launch_sweep_k(int rb, bool sc1, double *T, int rows, size_t ld, int Ns, const Pending &pd,
-                           const DevState *st, int rev, hipStream_t s) {
+static void launch_sweep_k(int rb, bool sc1, double *T, int rows, size_t ld, int Ns, const int *nact, int s0,
+                           const Pending &pd, const DevState *st, int rev, hipStream_t s) {
     switch (rb) {
-    case 1: sc1 ? launch_sweep_t<KT, 1, true>(T, rows, ld, Ns, pd, st, rev, s)
-                : launch_sweep_t<KT, 1, false>(T, rows, ld, Ns, pd, st, rev, s); break;
-    case 2: sc1 ? launch_sweep_t<KT, 2, true>(T, rows, ld, Ns, pd, st, rev, s)
-                : launch_sweep_t<KT, 2, false>(T, rows, ld, Ns, pd, st, rev, s); break;
-    default: sc1 ? launch_sweep_t<KT, 4, true>(T, rows, ld, Ns, pd, st, rev, s)
-                 : launch_sweep_t<KT, 4, false>(T, rows, ld, Ns, pd, st, rev, s); break;
+    case 1: sc1 ? launch_sweep_t<KT, 1, true>(T, rows, ld, Ns, nact, s0, pd, st, rev, s)
+                : launch_sweep_t<KT, 1, false>(T, rows, ld, Ns, nact, s0, pd, st, rev, s); break;
+    case 2: sc1 ? launch_sweep_t<KT, 2, true>(T, rows, ld, Ns, nact, s0, pd, st, rev, s)
+                : launch_sweep_t<KT, 2, false>(T, rows, ld, Ns, nact, s0, pd, st, rev, s); break;
+    default: sc1 ? launch_sweep_t<KT, 4, true>(T, rows, ld, Ns, nact, s0, pd, st, rev, s)
+                 : launch_sweep_t<KT, 4, false>(T, rows, ld, Ns, nact, s0, pd, st, rev, s); break;
     }
 }
 
-void sx_launch_sweep(double *T, int rows, size_t ld, int Ns, const Pending &pd, const DevState *st, int rev,
-                     SweepCfg cfg, hipStream_t s) {
+void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, int m, double *T, int rows, int row0,
+                        size_t ld, int s0, const Pending &pd, const DevState *st, hipStream_t s) {
+    k_activate<<<1, 256, 0, s>>>(perm, iperm, act, nact, m, T, rows, row0, ld, s0, pd.U, pd.recs, st, pd.batch);
+}
+
+void sx_launch_sweep(double *T, int rows, size_t ld, int Ns, const int *nact, int s0, const Pending &pd,
+                     const DevState *st, int rev, SweepCfg cfg, hipStream_t s) {
     if (rows <= 0) return;
     const int k = cfg.batch;  // pivots the sweep may have to apply (register slots)
     if (k <= 1)
-        launch_sweep_k<1>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, pd, st, rev, s);
+        launch_sweep_k<1>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, nact, s0, pd, st, rev, s);
     else if (k <= 4)
-        launch_sweep_k<4>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, pd, st, rev, s);
+        launch_sweep_k<4>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, nact, s0, pd, st, rev, s);
     else if (k <= 8)
-        launch_sweep_k<8>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, pd, st, rev, s);
+        launch_sweep_k<8>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, nact, s0, pd, st, rev, s);
     else if (k <= 16)
-        launch_sweep_k<16>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, pd, st, rev, s);
+        launch_sweep_k<16>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, nact, s0, pd, st, rev, s);
     else if (k <= SX_KMAX)
-        launch_sweep_k<SX_KMAX>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, pd, st, rev, s);
+        launch_sweep_k<SX_KMAX>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, nact, s0, pd, st, rev, s);
     else
         SX_FATAL("batch larger than SX_KMAX");
 }

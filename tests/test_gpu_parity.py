@@ -193,7 +193,8 @@ def test_session_pivots(gpu):
     assert t.pivots == 50 and t.status == sx.NOT_ENDED and t.update_launches == 2 and t.swept_pivots == 50
     assert t.update_ms > 0 and t.wall_ms >= t.update_ms
     assert t.stored_width == 1 + 2048 + 1024 and t.width == 1 + 2048 + 2 * 1024
-    assert t.update_bytes == 16.0 * 1024 * t.stored_width
+    # slack compaction: a sweep moves 1+n columns plus the slacks of rows that have left
+    assert 16.0 * 1024 * (1 + 2048) < t.update_bytes <= 16.0 * 1024 * (1 + 2048 + 50)
     assert t.swept_bytes == 2 * t.update_bytes
     applied, us = s.launch_log()
     assert list(applied) == [32, 18] and (us > 0).all()
@@ -411,3 +412,74 @@ def test_two_phase_negated_rows(gpu):
     t = s.pivots(40, time_updates=1)
     assert t.pivots == 40 and t.swept_pivots == 40
     s.close()
+
+
+# ------------------------------------------------------------------ slack compaction
+def _oracle_after(p, k):
+    A, b, c = p.arrays()
+    T, d, base = oracle.build_phase1(A, b)
+    oracle.update_objective(T, d, base)
+    _, done = oracle.solve(T, d, base, max_pivots=k)
+    return T, d, base, done
+
+
+@pytest.mark.parametrize("compact", [1, 0])
+@pytest.mark.parametrize("n,m,k,fused,W,p2p", [
+    (300, 1100, 200, -1, 1, -1),   # fused batches
+    (300, 1100, 200, 0, 1, -1),    # per-pivot launches
+    (64, 700, 400, -1, 1, -1),     # many pivots per row: rows leave again
+    (200, 1500, 150, -1, 2, 0),    # two shards, RCCL-style exchange
+    (200, 1500, 150, -1, 2, 1),    # two shards, fused batches over peer memory
+])
+def test_slack_compaction_tableau_bit_exact(gpu, n, m, k, fused, W, p2p, compact):
+    """sweeps that skip the untouched slack columns leave every logical entry of the
+    tableau -- the untouched unit vectors included -- bit-identical to the oracle's"""
+    p = sx.generateRandomProblem(n, m, n * 100 + m, 1, 100)
+    try:
+        sx.set_compact(compact)
+        sx.set_fused(fused)
+        sx.set_p2p(p2p)
+        sx.set_virtual_ranks(W)
+        s = sx.Session(problem=p)
+        t = s.pivots(k)
+        Tg, dg, bg = s.tableau(m, 1 + n + 2 * m)
+        active = s.active_slacks()
+        s.close()
+    finally:
+        sx.set_virtual_ranks(1)
+        sx.set_p2p(-1)
+        sx.set_fused(-1)
+        sx.set_compact(1)
+    T, d, base, done = _oracle_after(p, k)
+    assert t.pivots == done
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+    if compact:
+        assert 0 < active <= done and active < m
+    else:
+        assert active == m
+
+
+def test_slack_compaction_off_for_negated_rows(gpu):
+    """a b < 0 row is negated at build (its -0.0 entries could flip a zero's sign in an
+    untouched column): no compaction, still bit-exact"""
+    p = sx.generateRandomProblem(150, 700, 1234, -100, 100)
+    s = sx.Session(problem=p)
+    s.pivots(60)
+    Tg, dg, bg = s.tableau(700, 1 + 150 + 1400)
+    assert s.active_slacks() == 700
+    s.close()
+    T, d, base, _ = _oracle_after(p, 60)
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+def test_slack_compaction_generated_session_width(gpu):
+    """device-built tableau: the timed sweeps move 1+n+(touched slacks) columns"""
+    n, m = 512, 2048
+    s = sx.Session(generated=(n, m, n * 100 + m, 1, 100))
+    t = s.pivots(96, time_updates=1)
+    active = s.active_slacks()
+    s.close()
+    assert 0 < active <= 96
+    assert t.update_launches == 3 and t.swept_pivots == 96
+    assert t.update_bytes <= 16.0 * m * (1 + n + active) + 1e-6
+    assert t.update_bytes < 16.0 * m * t.stored_width
