@@ -753,13 +753,16 @@ class Engine {
         if (q_host == 0) return;
         const SweepCfg cfg = sweep_cfg(q_host);
         const int rev = (int)(sweeps & 1);  // alternate the sweep direction (Infinity-Cache reuse)
+        // the slack exchanges first (each shard's own buffers), so the events bracket the
+        // sweeps alone
+        if (compact)
+            for (auto &x : sh)
+                sx_launch_activate(x.perm, x.iperm, x.act, x.nact, m, x.T, x.rows, x.row0, ld, 1 + n, pending(x), x.st,
+                                   s);
         if (ev0) SX_HIP(hipEventRecord(ev0, s));
-        for (auto &x : sh) {
-            if (compact) sx_launch_activate(x.perm, x.iperm, x.act, x.nact, m, x.T, x.rows, x.row0, ld, 1 + n, pending(x),
-                                            x.st, s);
+        for (auto &x : sh)
             sx_launch_sweep(x.T, x.rows, ld, cols(N).Ns, compact ? x.nact : nullptr, 1 + n, pending(x), x.st, rev, cfg,
                             s);
-        }
         if (ev1) SX_HIP(hipEventRecord(ev1, s));
         ++sweeps;
         // batch ids tag the fused kernel's granules as (id << 8 | slot) in 32 bits: 24-bit ids, never 0
