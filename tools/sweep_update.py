@@ -46,8 +46,12 @@ def main():
                                           t.swept_bytes / max(t.update_ms, 1e-9) / 1e6))
     for f, v in ((sx.set_batch, 0), (sx.set_update_rows, 0), (sx.set_store_sc1, -1), (sx.set_update_waves, 0)):
         f(v)
-    print(f"{cfg}: {k} pivots x {rounds} rounds, stored width {t.stored_width}, bytes/sweep "
-          f"{t.update_bytes/1e9:.3f} GB; final status {t.status}")
+    print(f"{cfg}: {k} pivots x {rounds} rounds, stored width {t.stored_width}, swept bytes/sweep (last round) "
+          f"{t.swept_bytes / max(t.update_launches, 1) / 1e9:.3f} GB; final status {t.status}")
+    # settings run in a fixed order inside each round, so with slack compaction the later ones
+    # sweep more active columns: compare the GB/s column, not the sweep time
+    print("ranked by pivots/s; with slack compaction compare the GB/s column (later settings of a round "
+          "sweep more columns)")
     for key in sorted(res, key=lambda x: -statistics.median(r[0] for r in res[x])):
         pv = statistics.median(r[0] for r in res[key])
         up = statistics.median(r[1] for r in res[key])
