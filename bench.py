@@ -4,10 +4,12 @@ Workload (BASELINE.json configs[4], the m=32768 problem north_star's scaling tar
 quoted on): generateRandomProblem(n=8192, m=32768, seed=851968, [1,100]) -- seed n*100+m as
 the reference's -t sweep (main.cu:56-64) -- phase-1 tableau 32768 x 73729 fp64, synthesised
 in HBM (10.7 GB stored: artificial columns aliased to their slack columns).
-A "step" is one simplex pivot (entering argmin, ratio test, pivot row, objective row, and
-the rank-1 update of the whole tableau -- applied in sweeps of 32 pivots).
-W untimed pivots, then K timed pivots: by default pivots 64..2064 of phase 1 (SURVEY.md §8d:
-the scaling curve is the first 2000 phase-1 pivots).
+A "step" is one pass of the hot path over the tableau: one batch of 32 simplex pivots
+(entering argmin, ratio test, pivot row and objective row of each) followed by
+one sweep that applies their rank-1 updates to every stored tableau element.  W untimed
+steps, then K timed steps: by default pivots 64..2080 of phase 1 (the scaling
+curve is the first 2000 phase-1 pivots).  Every timed step is a full batch, so the timed
+window runs exactly the kernels the warmup ran.
 
 N GPUs (torchrun, one process per GPU): the constraint rows are split into N contiguous
 512-aligned blocks, each rank sweeps only its rows; per pivot the ranks exchange the tile
@@ -103,8 +105,9 @@ def cpu_baseline(n, m, seed, pivots, sx):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2000, help="timed pivots")
-    ap.add_argument("--warmup", type=int, default=64, help="untimed pivots before timing")
+    ap.add_argument("--steps", type=int, default=63,
+                    help="timed steps; a step = one batch of --batch pivots + one tableau sweep")
+    ap.add_argument("--warmup", type=int, default=2, help="untimed steps before timing")
     ap.add_argument("--config", default="config5", choices=sorted(CONFIGS))
     ap.add_argument("--update-rows", type=int, default=0, help="rows per sweep step (0 = auto)")
     ap.add_argument("--batch", type=int, default=0, help="pivots per tableau sweep (0 = library default, 32)")
@@ -115,10 +118,12 @@ def main():
                     help="directory of pmc_sweep_<config>.json: per-launch HBM bytes of the sweep (rocprofv3 --pmc)")
     ap.add_argument("--secondary", default="config3",
                     help="second workload timed in the same run ('' to skip): the roofline-target tableau")
-    ap.add_argument("--no-full-solve", action="store_true",
-                    help="skip the end-to-end twoPhaseMethod solve of config 3's instance (N=1 only)")
-    ap.add_argument("--secondary-steps", type=int, default=8900)
-    ap.add_argument("--secondary-warmup", type=int, default=50)
+    ap.add_argument("--secondary-steps", type=int, default=278, help="config 3: 278 steps = pivots 64..8960 of 8981")
+    ap.add_argument("--secondary-warmup", type=int, default=2)
+    ap.add_argument("--full-solves", default="config3,config4,config5",
+                    help="instances solved end to end by twoPhaseMethod at N=1 ('' to skip)")
+    ap.add_argument("--no-update-bench", action="store_true",
+                    help="skip the synthetic 4096x8192 sweep bench (SURVEY.md §8d config 3')")
     args = ap.parse_args()
 
     import torch
@@ -145,8 +150,10 @@ def main():
         if world > 1:
             dist.barrier()
 
+    K = args.batch if args.batch > 0 else 32  # pivots per step (the library clamps to 1..32)
+
     def measure(config, steps, warmup, events):
-        """W untimed + K timed phase-1 pivots of `config`; returns timing + roofline."""
+        """W untimed + K timed steps (batches of K pivots + one sweep) of `config`'s phase 1."""
         n, m, seed = CONFIGS[config]
         t_setup = time.perf_counter()
         # generateRandomProblem(n, m, seed, 1, 100) synthesised directly in HBM, each rank its rows
@@ -154,11 +161,11 @@ def main():
         torch.cuda.synchronize()
         t_setup = time.perf_counter() - t_setup
         if warmup > 0:
-            sess.pivots(warmup)
+            sess.pivots(warmup * K)
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        tim = sess.pivots(steps, time_updates=events)
+        tim = sess.pivots(steps * K, time_updates=events)
         torch.cuda.synchronize()
         barrier()
         elapsed = time.perf_counter() - t0
@@ -168,18 +175,23 @@ def main():
             elapsed = float(tt.item())
         sess.close()
         avg_update_s = tim.update_ms / 1e3 / max(tim.update_launches, 1)
-        # algorithmic bytes of a sweep: every stored tableau element read and written once
+        # algorithmic bytes of a sweep: every stored tableau element it moves, read and written once
         achieved = tim.swept_bytes / (tim.update_ms / 1e3) / 1e9 if tim.update_launches else None
         return {"n": n, "m": m, "seed": seed, "tim": tim, "elapsed": elapsed, "pivots": tim.pivots,
-                "avg_update_s": avg_update_s, "achieved": achieved, "setup_s": t_setup}
+                "avg_update_s": avg_update_s, "achieved": achieved, "setup_s": t_setup,
+                "steps": steps, "warmup": warmup}
 
     def roofline(cfg, r):
         tim, achieved = r["tim"], r["achieved"]
-        traffic = None
+        traffic, source = None, None
         pmc = os.path.join(args.pmc_dir, f"pmc_sweep_{cfg}.json") if args.pmc_dir else None
         if pmc and os.path.exists(pmc):
             with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                rec = json.load(f)
+            traffic = rec.get("hbm_bytes_per_launch")
+            source = (f"committed profile profiles/pmc_sweep_{cfg}.json ({rec.get('tag')}: rocprofv3 --pmc "
+                      f"FETCH_SIZE and WRITE_SIZE passes of `{rec.get('command', 'bench.py')}`, "
+                      "(2*FETCH_SIZE+WRITE_SIZE)*1024 per launch) -- not measured in this run")
         return {
             "bound": "hbm",
             "achieved": achieved,
@@ -187,11 +199,17 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS if achieved else None,
             "traffic": traffic,
+            "traffic_source": source,
             "kernel": "k_sweep (rank-1 pivot updates of a batch applied to the tableau, rank 0)",
+            "bytes_definition": "16 * rows * (1 + n + touched slack columns) per sweep: every stored tableau "
+                                "element the sweep moves, read and written once (SURVEY.md §8d 16(m+1)N over the "
+                                "swept columns; artificial columns alias their slacks and untouched slack columns "
+                                "are exact unit vectors, DESIGN.md §2, §3.4)",
             "algorithmic_bytes_per_launch": tim.update_bytes,
             "pivots_per_launch": tim.swept_pivots / max(tim.update_launches, 1),
             "avg_launch_us": r["avg_update_s"] * 1e6,
             "timed_launches": tim.update_launches,
+            "timing": "HIP events on the engine stream around every timed sweep",
             "sweep_share_of_time": tim.update_ms / max(tim.wall_ms, 1e-9),
         }
 
@@ -208,7 +226,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed * 1e3 / max(pivots, 1),
+        "ms_per_step": elapsed * 1e3 / max(args.steps, 1),
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": (pivots / elapsed) / REF_PIVOTS_PER_S[args.config] if args.config in REF_PIVOTS_PER_S else None,
@@ -217,11 +235,15 @@ def main():
                 "reference's -t sweep (cuRAND-XORWOW + MSVC rand semantics), synthesised on the GPU",
         "config": {
             "workload": workload(args.config, r),
+            "step": f"one batch of {K} pivots + one sweep of the tableau",
+            "pivots_per_step": K,
             "m": m, "n": n, "seed": seed, "tableau_width": tim.width, "stored_width": tim.stored_width,
             "rows_per_gpu_rank0": tim.local_rows, "parallelism": f"row-block x{world}",
             "exchange": ("none (one shard)" if world == 1 else
-                         "peer-memory fused batch (xGMI)" if sx.p2p_ready() else "per-pivot RCCL collectives"),
-            "pivots_timed": pivots, "status_after": tim.status, "setup_s": r["setup_s"],
+                         "peer-memory fused batch (xGMI)" if sx.p2p_ready() else
+                         "per-pivot RCCL collectives (FALLBACK: the peer-memory self-check failed; slower than 1 GPU)"),
+            "pivots_timed": pivots, "first_timed_pivot": args.warmup * K, "status_after": tim.status,
+            "setup_s": r["setup_s"],
         },
         "roofline": roofline(args.config, r),
         "cpu_baseline": None,
@@ -233,34 +255,50 @@ def main():
             "value": r2["pivots"] / r2["elapsed"], "unit": "pivots/s",
             "vs_baseline": (r2["pivots"] / r2["elapsed"]) / REF_PIVOTS_PER_S[args.secondary]
             if args.secondary in REF_PIVOTS_PER_S else None,
-            "ms_per_step": r2["elapsed"] * 1e3 / max(r2["pivots"], 1),
+            "ms_per_step": r2["elapsed"] * 1e3 / max(args.secondary_steps, 1),
             "steps": args.secondary_steps, "warmup": args.secondary_warmup, "pivots_timed": r2["pivots"],
+            "first_timed_pivot": args.secondary_warmup * K,
             "status_after": r2["tim"].status, "rows_per_gpu_rank0": r2["tim"].local_rows, "setup_s": r2["setup_s"],
             "roofline": roofline(args.secondary, r2),
         }
-    if world == 1 and not args.no_full_solve:
-        # the whole drop-in call on config 3's instance (the reference's -t instance with published
-        # timings): build + both phases + solution, as main.cu -t times it (problem synthesised on
-        # the GPU, copied to the host first)
-        fn, fm, fseed = CONFIGS["config3"]
-        prob = sx.generateRandomProblemDevice(fn, fm, fseed, 1, 100)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        res = sx.twoPhaseMethodEx(prob)
-        dt = time.perf_counter() - t0
-        prob.close()
-        ph = (ctypes.c_double * 2)()
-        sx.load().simplex_last_phase_seconds(ph)
-        full = {"instance": "config3", "seconds": dt, "status": sx.STATUS_NAMES.get(res.status, res.status),
-                "pivots": list(res.pivots), "objective": res.optimal_value,
-                "note": "twoPhaseMethod wall time incl. tableau build from host arrays, both phases and the solution"}
-        full["pivot_loop_s"] = [ph[0], ph[1]]
-        full["pivots_per_s"] = [res.pivots[k] / ph[k] if ph[k] > 0 else None for k in (0, 1)]
-        full["reference_pivots_per_s"] = [8981 / 68.33, 255 / 0.94]  # RTX 2070S, BASELINE.md §1
-        full["reference_pivot_loop_s"] = REF_SOLVE["config3"]["pivot_loop_s"]
-        full["reference_pivots"] = REF_SOLVE["config3"]["pivots"]
-        full["pivots_match_reference"] = list(res.pivots) == REF_SOLVE["config3"]["pivots"]
-        out["full_solve"] = full
+    if world == 1 and not args.no_update_bench:
+        # SURVEY.md §8d config 3': the sweep kernel alone on a synthetic 4096 x 8192 fp64 matrix
+        # (uniform [1,100], seed 823296) with 32 random pending pivots
+        us, nbytes = sx.bench_sweep(4096, 8192, 823296, 1, 100, 32, warmup=5, iters=50)
+        gbs = nbytes / (us * 1e-6) / 1e9
+        out["update_bench"] = {
+            "workload": "config3': k_sweep on a synthetic 4096x8192 fp64 matrix (uniform [1,100], seed 823296), "
+                        "32 random pending pivots per sweep, 50 timed sweeps (HIP events)",
+            "avg_launch_us": us, "bytes_per_launch": nbytes, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": gbs / HBM_PEAK_GBS, "per_pivot_equivalent_us": us / 32,
+            "note": "the matrix (268 MB) is about the size of the 256 MB Infinity Cache, so sweeps partly hit it",
+        }
+    if world == 1 and args.full_solves:
+        # the whole drop-in call, as main.cu -t times it: build + both phases + solution (problem
+        # synthesised on the GPU and copied to the host first, outside the clock)
+        out["full_solve"] = []
+        for name in [c for c in args.full_solves.split(",") if c]:
+            fn, fm, fseed = CONFIGS[name]
+            prob = sx.generateRandomProblemDevice(fn, fm, fseed, 1, 100)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            res = sx.twoPhaseMethodEx(prob)
+            dt = time.perf_counter() - t0
+            prob.close()
+            ph = (ctypes.c_double * 2)()
+            sx.load().simplex_last_phase_seconds(ph)
+            full = {"instance": name, "n": fn, "m": fm, "seed": fseed, "seconds": dt,
+                    "status": sx.STATUS_NAMES.get(res.status, res.status), "pivots": list(res.pivots),
+                    "objective": res.optimal_value,
+                    "note": "twoPhaseMethod wall time incl. tableau build from host arrays, both phases and the solution",
+                    "pivot_loop_s": [ph[0], ph[1]],
+                    "pivots_per_s": [res.pivots[k] / ph[k] if ph[k] > 0 else None for k in (0, 1)]}
+            if name in REF_SOLVE:
+                full["reference_pivots_per_s"] = [8981 / 68.33, 255 / 0.94]  # RTX 2070S, BASELINE.md §1
+                full["reference_pivot_loop_s"] = REF_SOLVE[name]["pivot_loop_s"]
+                full["reference_pivots"] = REF_SOLVE[name]["pivots"]
+                full["pivots_match_reference"] = list(res.pivots) == REF_SOLVE[name]["pivots"]
+            out["full_solve"].append(full)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, m, seed, CPU_SAMPLE[args.config], sx)
     if rank == 0:

@@ -73,9 +73,22 @@ void simplex_last_phase_seconds(double *out);
 /* the sweep's grid: waves x (blocks resident on the device) blocks (default 1; <= 0 resets) */
 void simplex_set_update_waves(double waves);
 
+/* ---- fault handling and test hooks ---- */
+/* a fused batch whose in-kernel hand-off wait times out (SIMPLEX_HANG, never expected) is
+ * undone and re-run on the per-pivot path; this counts such recoveries in the process */
+long long simplex_hang_recoveries(void);
+long long simplex_fused_batches(void);           /* fused batch launches in the process */
+/* test hook: make the n-th fused batch from now abort as if a wait had timed out (-1 off) */
+void simplex_set_hang_inject(long long batches);
+/* test hook: batch id of the next engine's first batch (1 .. 32767; ids wrap at 32768) */
+void simplex_set_first_batch_id(unsigned int id);
+
 /* ---- extended drop-in entry ---- */
 /* twoPhaseMethod + final basis (base_out[m]) and per-phase pivot counts (pivots_out[2]);
- * max_pivots < 0 = no cap (parity mode), else per-phase cap (status SIMPLEX_PIVOT_CAP). */
+ * max_pivots < 0 = no cap (parity mode), else per-phase cap (status SIMPLEX_PIVOT_CAP).
+ * It returns the engine-only statuses (SIMPLEX_PIVOT_CAP, SIMPLEX_NUMERIC_FAIL, SIMPLEX_HANG)
+ * as such; twoPhaseMethod and solve keep the reference contract (0/-1/-2/-3, solve 0/-2) and
+ * treat NUMERIC_FAIL and HANG as fatal errors (print, exit; error.cu:5-12). */
 int twoPhaseMethodEx(problem_t *problem, double *solution, double *optimalValue, int *base_out,
                      long long *pivots_out, long long max_pivots);
 
@@ -133,6 +146,14 @@ long long simplex_session_launch_log(simplex_session *s, long long *rows, double
  * next entering variable; -1 when the fused path is not in use */
 int simplex_session_stamps(simplex_session *s, int k, unsigned long long *out);
 void simplex_session_close(simplex_session *s);
+
+/* ---- kernel bench (SURVEY.md §8d config 3') ---- */
+/* the sweep kernel (solver.cu:34-46's update, `pivots` pending pivots per pass) on a synthetic
+ * rows x cols fp64 matrix drawn like generateRandomProblem's A (seed, values in [lo, hi]) with
+ * random pending pivots; `warmup` untimed then `iters` timed sweeps (HIP events); returns the
+ * average microseconds per sweep (< 0 on bad arguments), *bytes = 16 * rows * cols */
+double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi, int pivots, int warmup, int iters,
+                           double *bytes);
 
 /* ---- kernel-level parity hooks (host arrays in/out, device compute) ---- */
 /* epsilon argmin of v[0..L) with the reference combine tree; returns index (or -1) */

@@ -13,7 +13,7 @@ step() {  # step <name> <seconds> <cmd...>
     tail -5 "gpurun_out/$name.log"
     return $rc
 }
-step pytest_gpu 900 python -m pytest tests -m gpu -q --maxfail=5 -p no:cacheprovider
+step pytest_gpu 900 python -u -m pytest tests -m gpu -q --maxfail=5 -p no:cacheprovider --timeout 300 --timeout-method thread
 rc=$?; [ $rc -gt 1 ] && exit $rc
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 step bench 600 python bench.py ${BENCH_ARGS:-} || exit $?

@@ -102,6 +102,10 @@ SIGNATURES = {
     "simplex_set_p2p": (None, [ctypes.c_int]),
     "simplex_p2p_ready": (ctypes.c_int, []),
     "simplex_set_update_waves": (None, [ctypes.c_double]),
+    "simplex_hang_recoveries": (ctypes.c_longlong, []),
+    "simplex_fused_batches": (ctypes.c_longlong, []),
+    "simplex_set_hang_inject": (None, [ctypes.c_longlong]),
+    "simplex_set_first_batch_id": (None, [ctypes.c_uint]),
     "twoPhaseMethodEx": (ctypes.c_int, [P_PROBLEM, c_double_p, c_double_p, c_int_p, c_ll_p, ctypes.c_longlong]),
     "simplex_problem_from_arrays": (P_PROBLEM, [ctypes.c_int, ctypes.c_int, c_double_p, c_double_p, c_double_p]),
     "simplex_generate_problem_ex": (P_PROBLEM, [ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_int,
@@ -126,6 +130,8 @@ SIGNATURES = {
     "simplex_session_launch_log": (ctypes.c_longlong, [ctypes.c_void_p, c_ll_p, c_double_p, ctypes.c_longlong]),
     "simplex_session_close": (None, [ctypes.c_void_p]),
     "simplex_session_stamps": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_ulonglong)]),
+    "simplex_bench_sweep": (ctypes.c_double, [ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_int, ctypes.c_int, c_double_p]),
     "simplex_dev_argmin": (ctypes.c_longlong, [c_double_p, ctypes.c_longlong, c_double_p]),
     "simplex_dev_pivots": (ctypes.c_int, [c_double_p, ctypes.c_longlong, ctypes.c_longlong, ctypes.c_longlong,
                                           c_double_p, c_int_p, ctypes.c_longlong, c_ll_p]),

@@ -240,6 +240,17 @@ class Session:
             pass
 
 
+def bench_sweep(rows, cols, seed, lo=1, hi=100, pivots=32, warmup=3, iters=20):
+    """SURVEY.md §8d config 3': the sweep kernel on a synthetic rows x cols matrix;
+    returns (average microseconds per sweep, algorithmic bytes per sweep)."""
+    b = ctypes.c_double(0.0)
+    us = _lib.load().simplex_bench_sweep(rows, cols, seed & 0xFFFFFFFF, lo, hi, pivots, warmup, iters,
+                                         ctypes.byref(b))
+    if us < 0:
+        raise ValueError("simplex_bench_sweep: bad arguments")
+    return us, b.value
+
+
 # ---- kernel-level parity hooks ----
 def dev_argmin(v):
     lib = _lib.load()

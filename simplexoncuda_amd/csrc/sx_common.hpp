@@ -52,6 +52,10 @@ struct __attribute__((aligned(16))) DevState {
 
 // Deferred pivots: at most SX_KMAX pivots between two sweeps of the tableau.
 #define SX_KMAX 32
+// Batch ids run 1 .. SX_BATCH_IDS - 1: the fused kernels' granule tags keep 15 bits of the id
+// (sx_kernels.hip make_tag).  When the ids wrap, the engine clears every id-tagged word (the
+// PM pending-leaving masks and the granule records) first, so no stale tag can match.
+#define SX_BATCH_IDS (1u << 15)
 
 // Record of one pending pivot (slot s of the current batch).
 struct __attribute__((aligned(16))) PivRec {
@@ -92,7 +96,8 @@ struct PeerView {
     double *d[SX_MAXW];              // objective rows (written)
 };
 
-#define SX_HANG (-13)  // fused batch kernel: a hand-off wait timed out (never expected)
+#define SX_HANG (-13)  // fused batch kernel: a hand-off wait timed out (never expected; the host
+                       // restores the batch's start state and re-runs it on the per-pivot path)
 
 // Error convention of the reference (error.cu:5-12): print "<msg> in <file> at line <n>"
 // and exit(EXIT_FAILURE).
@@ -153,15 +158,17 @@ void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, in
 // fused batch of up to k pivots on one shard (ratio tiles + objective tiles in one resident
 // grid); returns false (nothing launched) when the grid cannot be resident at once
 bool sx_batch_fits(int rows, Cols c, int k);
-void sx_launch_batch(const double *T, int rows, size_t ld, Cols c, double *d, int *base, DevState *st,
-                     const Pending &pd, int k, BatchChan *chan, unsigned long long *ga, unsigned long long *gb,
-                     unsigned long long *stamps, hipStream_t s);
+// d_save: the objective row as the batch found it (restored by the host after SX_HANG); the
+// basis is written only by a batch that completed
+void sx_launch_batch(const double *T, int rows, size_t ld, Cols c, double *d, double *d_save, int *base,
+                     DevState *st, const Pending &pd, int k, BatchChan *chan, unsigned long long *ga,
+                     unsigned long long *gb, unsigned long long *stamps, hipStream_t s);
 size_t sx_batch_granules_a();
 size_t sx_batch_granules_b();
 // the multi-rank fused batch: `grids` co-resident launches of this shape must fit the device
 bool sx_batch_mr_fits(int slots, int nb_local, int k, int grids);
-void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld, Cols c, double *d, int *base,
-                        DevState *st, const Pending &pd, int k, int slots, int W, int rank, int tb0, int tb1,
+void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld, Cols c, double *d, double *d_save,
+                        int *base, DevState *st, const Pending &pd, int k, int slots, int W, int rank, int tb0, int tb1,
                         BatchChan *chan, const unsigned long long *ga, const unsigned long long *gb,
                         const unsigned long long *gdone, const PeerView &pv, unsigned long long timeout,
                         hipStream_t s);

@@ -69,6 +69,11 @@ struct Config {
     bool p2p_ready = false;  // RCCL ranks: the peer-memory path passed the start-up self-check
     int debug = -1;          // -1: from SIMPLEX_DEBUG; 1: print the tableau after every step
     bool benchmark = false;
+    bool no_timer = false;         // the multi-GPU self-check: never write TIMER CSVs
+    long long inject_hang = -1;    // test hook: abort the n-th fused batch from now (-1 off)
+    unsigned first_batch_id = 1;   // test hook: batch id of a new engine's first batch
+    long long hang_recoveries = 0; // fused batches aborted and re-run on the per-pivot path
+    long long fused_batches = 0;   // fused batch launches (every shard's counted once)
     // distributed
     bool dist = false;
     int rank = 0;
@@ -109,6 +114,7 @@ struct Chrono {
     bool on() const { return f != nullptr; }
 
     void open(int n, int m) {
+        if (g_cfg.no_timer) return;
         std::string dir = g_cfg.timer_dir;
         if (dir.empty()) {
             const char *e = getenv("SIMPLEX_TIMER_DIR");
@@ -161,6 +167,7 @@ struct Shard {
     int rows = 0;
     double *T = nullptr;
     double *d = nullptr;
+    double *d_save = nullptr;         // fused batch: d as the batch found it (restored after SX_HANG)
     double *colE = nullptr;
     double *prow = nullptr;
     double *prow_send = nullptr;
@@ -217,7 +224,7 @@ class Engine {
     long long phase_pivots[2] = {0, 0};
     // deferred pivots: the host numbers batches (ids never repeat, 0 is never used) and the
     // slots inside the current one; every batch ends with a sweep of the tableau
-    unsigned batch_id = 1;
+    unsigned batch_id = 1;  // 1 .. 2^15 - 1 (the granule tags keep 15 bits; see enqueue_sweep)
     int q_host = 0;
     unsigned long long *stamps = nullptr;  // diagnostic: in-kernel timestamps of the fused batch
     long long sweeps = 0;
@@ -230,6 +237,7 @@ class Engine {
         alias = alias_ && g_cfg.alias && m > 0;
         Ns1 = alias ? N2 : N1;
         ld = round_up((size_t)Ns1, 16);
+        batch_id = (g_cfg.first_batch_id >= 1 && g_cfg.first_batch_id < SX_BATCH_IDS) ? g_cfg.first_batch_id : 1;
         if (g_cfg.dist && g_cfg.comm) {
             rccl = true;
             W = g_cfg.world;
@@ -401,7 +409,19 @@ class Engine {
     void alloc_shard(Shard &x) {
         const size_t rows_alloc = x.rows > 0 ? (size_t)x.rows : 1;
         x.T = dalloc<double>(rows_alloc * ld);
-        x.d = dalloc<double>(round_up((size_t)N1, 16));
+        // several shards: d and U are written by other ranks' batches (peer memory over xGMI,
+        // system-scope stores) and read here by plain loads -- uncached, so no L2 of this
+        // device keeps a stale line of them
+        if (xchg) {
+            SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&x.d), round_up((size_t)N1, 16) * sizeof(double),
+                                         hipDeviceMallocUncached));
+            SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&x.U), (size_t)SX_KMAX * ld * sizeof(double),
+                                         hipDeviceMallocUncached));
+        } else {
+            x.d = dalloc<double>(round_up((size_t)N1, 16));
+            x.U = dalloc<double>((size_t)SX_KMAX * ld);
+        }
+        x.d_save = dalloc<double>(round_up((size_t)N1, 16));
         x.colE = dalloc<double>(rows_alloc);
         x.prow = dalloc<double>(ld);
         if (xchg) x.prow_send = dalloc<double>(ld);
@@ -417,7 +437,6 @@ class Engine {
             }
             SX_HIP(hipMemcpy(x.slot_send, init.data(), sizeof(double) * init.size(), hipMemcpyHostToDevice));
         }
-        x.U = dalloc<double>((size_t)SX_KMAX * ld);
         x.F = dalloc<double>(rows_alloc * SX_KMAX);
         x.recs = dalloc<PivRec>(SX_KMAX);
         x.PM = dalloc<unsigned long long>(rows_alloc);
@@ -466,7 +485,7 @@ class Engine {
     }
 
     void free_shard(Shard &x) {
-        for (void *p : {(void *)x.T, (void *)x.d, (void *)x.colE, (void *)x.prow, (void *)x.prow_send,
+        for (void *p : {(void *)x.T, (void *)x.d, (void *)x.d_save, (void *)x.colE, (void *)x.prow, (void *)x.prow_send,
                         (void *)x.slot_send, (void *)x.slot_all, (void *)x.U, (void *)x.F, (void *)x.recs, (void *)x.PM,
                         (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
                         (void *)x.rhs_all, (void *)x.base, (void *)x.enter_parts, (void *)x.tiles_local, (void *)x.chan,
@@ -657,6 +676,9 @@ class Engine {
         c.batch = batch;
         c.rows_per_block = g_cfg.update_rows > 0 ? std::min(g_cfg.update_rows, 4) : (batch > 16 ? 4 : 2);
         c.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : (big ? 1 : 0);
+        // peer ranks read leaving rows straight from this tableau (system-scope loads over
+        // xGMI): its stores must write through to memory, not stay dirty in an L2 of this device
+        if (p2p && rccl) c.sc1 = 1;
         return c;
     }
 
@@ -719,10 +741,13 @@ class Engine {
 
     void enqueue_batch(int k) {
         if (q_host != 0) SX_FATAL("fused batch inside a started batch");
+        ++g_cfg.fused_batches;
+        if (g_cfg.inject_hang >= 0 && g_cfg.inject_hang-- == 0)  // test hook: this batch aborts
+            for (auto &x : sh) SX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&x.chan->abort_w), 1u, 1, s));
         if (!xchg) {
             Shard &x = sh[0];
-            sx_launch_batch(x.T, x.rows, ld, cols(N, x), x.d, x.base, x.st, pending(x), k, x.chan, x.ga, x.gb, stamps,
-                            s);
+            sx_launch_batch(x.T, x.rows, ld, cols(N, x), x.d, x.d_save, x.base, x.st, pending(x), k, x.chan, x.ga, x.gb,
+                            stamps, s);
         } else {
             // every rank's batch runs at once (virtual shards: one stream each, forked from and
             // joined back into the engine stream); the ranks hand off through peer memory
@@ -737,7 +762,8 @@ class Engine {
                     SX_HIP(hipStreamWaitEvent(xs, ev_fork, 0));
                 }
                 const int tb0 = (int)((long long)x.rank * NBg / W), tb1 = (int)((long long)(x.rank + 1) * NBg / W);
-                sx_launch_batch_mr(x.T, x.rows, x.row0, rpr, ld, cols(N, x), x.d, x.base, x.st, pending(x), k, slots, W,
+                sx_launch_batch_mr(x.T, x.rows, x.row0, rpr, ld, cols(N, x), x.d, x.d_save, x.base, x.st, pending(x), k,
+                                   slots, W,
                                    x.rank, tb0, tb1, x.chan, x.ga, x.gb, x.gdone, pv, timeout, xs);
                 if (!rccl) SX_HIP(hipEventRecord(ev_join[i], xs));
             }
@@ -765,9 +791,25 @@ class Engine {
                             s);
         if (ev1) SX_HIP(hipEventRecord(ev1, s));
         ++sweeps;
-        // batch ids tag the fused kernel's granules as (id << 8 | slot) in 32 bits: 24-bit ids, never 0
-        if (++batch_id >= (1u << 24)) batch_id = 1;
         q_host = 0;
+        if (++batch_id >= SX_BATCH_IDS) wrap_batch_ids();
+    }
+
+    // The granule tags keep 15 bits of the batch id ([id | slot (6) | payload (11)],
+    // sx_kernels.hip make_tag) and PM[i] the whole id: before ids repeat, every id-tagged word
+    // is cleared (0 is never an id), once per 32767 batches (about a million pivots).
+    void wrap_batch_ids() {
+        batch_id = 1;
+        for (auto &x : sh) {
+            SX_HIP(hipMemsetAsync(x.PM, 0, sizeof(unsigned long long) * (x.rows > 0 ? (size_t)x.rows : 1), s));
+            SX_HIP(hipMemsetAsync(x.ga, 0, sx_batch_granules_a() * sizeof(unsigned long long), s));
+            SX_HIP(hipMemsetAsync(x.gb, 0, sx_batch_granules_b() * sizeof(unsigned long long), s));
+            if (x.gdone) SX_HIP(hipMemsetAsync(x.gdone, 0, SX_MAXW * sizeof(unsigned long long), s));
+        }
+        // peer ranks write into these records: no rank starts its next batch before every rank
+        // has cleared its own (an RCCL all-reduce behind the memsets on every rank)
+        if (rccl) all_ranks(1);
+        SX_HIP(hipStreamSynchronize(s));
     }
 
     void reset_state(long long max_pivots) {
@@ -810,7 +852,8 @@ class Engine {
         }
         // batches of K pivots + one sweep; the host polls the status of the batch before the
         // last one, so the device never waits on the host
-        const bool fused = !timed && fused_ok(K);
+        bool fused = !timed && fused_ok(K);
+        int hangs = 0;
         long long k = 0;
         for (; !on_pivot; ++k) {
             if (fused) enqueue_batch(K);
@@ -835,7 +878,17 @@ class Engine {
             SX_HIP(hipEventRecord(poll_ev[slot], s));
             if (k >= 1) {
                 SX_HIP(hipEventSynchronize(poll_ev[slot ^ 1]));
-                if (st_host[slot ^ 1].status != SX_NOT_ENDED) break;
+                const int st = st_host[slot ^ 1].status;
+                if (st == SX_HANG) {
+                    // a fused batch's hand-off wait timed out (every rank sees it at the same
+                    // batch): restore the state it found, re-run it on the per-pivot path
+                    recover_hang(K);
+                    if (++hangs >= 2) fused = false;  // not twice more: stay on the per-pivot path
+                    if (read_state().status != SX_NOT_ENDED) break;
+                    k = -1;  // restart the lagged polling
+                    continue;
+                }
+                if (st != SX_NOT_ENDED) break;
             }
         }
         DevState f = read_state();
@@ -850,6 +903,23 @@ class Engine {
         }
         if (pivots) *pivots = f.pivots;
         return f.status;
+    }
+
+    // After SX_HANG: the aborted batch changed neither T (its sweep found no pivot to apply),
+    // the basis (written only by a completed batch) nor the state (only the status); its
+    // objective row is restored from d_save.  The batch behind it saw the SX_HANG status and
+    // did nothing.  The batch is then re-run on the per-pivot path, under fresh batch ids.
+    void recover_hang(int K) {
+        SX_HIP(hipStreamSynchronize(s));
+        ++g_cfg.hang_recoveries;
+        const int ne = SX_NOT_ENDED;
+        for (auto &x : sh) {
+            SX_HIP(hipMemcpyAsync(x.d, x.d_save, sizeof(double) * N, hipMemcpyDeviceToDevice, s));
+            SX_HIP(hipMemcpyAsync(&x.st->status, &ne, sizeof(int), hipMemcpyHostToDevice, s));
+        }
+        for (int b = 0; b < K; ++b) enqueue_pivot();
+        enqueue_sweep();
+        SX_HIP(hipStreamSynchronize(s));
     }
 
     double read_d0() {
@@ -968,6 +1038,16 @@ void print_tableau(FILE *out, Engine &E, int width) {
 bool debug_on() {
     if (g_cfg.debug < 0) g_cfg.debug = getenv("SIMPLEX_DEBUG") ? 1 : 0;
     return g_cfg.debug > 0;
+}
+
+// The reference's entry points return only FEASIBLE / INFEASIBLE / UNBOUNDED / DEGENERATE
+// (twoPhaseMethod.h:5-8; solve: FEASIBLE / UNBOUNDED, solver.cu:119-125); every other failure
+// prints and exits (error.cu:5-12).  The engine-only outcomes follow that convention there
+// (twoPhaseMethodEx keeps them as statuses).
+int public_status(int st) {
+    if (st == SX_NUMERIC_FAIL) SX_FATAL("simplex: the ratio test found no leaving row although a pivot is eligible");
+    if (st == SX_HANG) SX_FATAL("simplex: a fused-batch hand-off between GPUs timed out");
+    return st;
 }
 
 // ------------------------------------------------------------------ the two-phase driver
@@ -1101,6 +1181,11 @@ void simplex_set_update_waves(double waves) { sx_set_update_waves((float)waves);
 void simplex_set_exchange_mode(int mode) { g_cfg.exchange_mode = (mode >= 0 && mode <= 2) ? mode : 0; }
 void simplex_set_timer_dir(const char *dir) { g_cfg.timer_dir = dir ? dir : ""; }
 
+void simplex_set_hang_inject(long long batches) { g_cfg.inject_hang = batches >= 0 ? batches : -1; }
+long long simplex_hang_recoveries(void) { return g_cfg.hang_recoveries; }
+long long simplex_fused_batches(void) { return g_cfg.fused_batches; }
+void simplex_set_first_batch_id(unsigned int id) { g_cfg.first_batch_id = (id >= 1 && id < SX_BATCH_IDS) ? id : 1; }
+
 void enableBenchmarkMode(void) { g_cfg.benchmark = true; }
 void disableBenchmarkMode(void) { g_cfg.benchmark = false; }
 
@@ -1126,13 +1211,19 @@ static void p2p_selftest() {
     long long pa[2] = {0, 0}, pb[2] = {0, 0};
     double za = 0.0, zb = 0.0;
     const int save = g_cfg.p2p;
+    const bool save_nt = g_cfg.no_timer;
+    g_cfg.no_timer = true;  // (timing would switch both solves to the per-pivot path; no CSVs either)
     g_cfg.p2p = 1;
+    const long long fb0 = g_cfg.fused_batches, hr0 = g_cfg.hang_recoveries;
     const int sa = two_phase(P, xa.data(), &za, ba.data(), pa, -1);
+    const bool went_fused = g_cfg.fused_batches > fb0 && g_cfg.hang_recoveries == hr0;
     g_cfg.p2p = 0;
     const int sb = two_phase(P, xb.data(), &zb, bb.data(), pb, -1);
     g_cfg.p2p = save;
-    int ok = sa == sb && sa != SX_HANG && pa[0] == pb[0] && pa[1] == pb[1] && std::memcmp(&za, &zb, sizeof(za)) == 0 &&
-             ba == bb && std::memcmp(xa.data(), xb.data(), sizeof(double) * n) == 0;
+    g_cfg.no_timer = save_nt;
+    int ok = went_fused && sa == sb && sa != SX_HANG && pa[0] == pb[0] && pa[1] == pb[1] &&
+             std::memcmp(&za, &zb, sizeof(za)) == 0 && ba == bb &&
+             std::memcmp(xa.data(), xb.data(), sizeof(double) * n) == 0;
     freeProblem(P);
     free(P);
     int *dv = nullptr;
@@ -1177,7 +1268,7 @@ int simplex_dist_finalize(void) {
 }
 
 int twoPhaseMethod(problem_t *problem, TYPE *solution, TYPE *optimalValue) {
-    return two_phase(problem, solution, optimalValue, nullptr, nullptr, -1);
+    return public_status(two_phase(problem, solution, optimalValue, nullptr, nullptr, -1));
 }
 
 int twoPhaseMethodEx(problem_t *problem, double *solution, double *optimalValue, int *base_out,
@@ -1186,8 +1277,12 @@ int twoPhaseMethodEx(problem_t *problem, double *solution, double *optimalValue,
 }
 
 // ---------------------------------------------------------------- tabular_t API
+// tabular.cu:25-39.  The caller fills the tableau itself, so every one of its 1+n+2m columns is
+// stored (no artificial-column aliasing: the caller's artificial columns need not equal the
+// slacks) and slack compaction stays off (any column may hold anything): row i occupies
+// `rows` doubles at table + i * pitch bytes, exactly as include/tabular.h states.
 tabular_t *newTabular(problem_t *problem) {
-    Engine *E = new Engine(problem->vars, problem->constraints);
+    Engine *E = new Engine(problem->vars, problem->constraints, /*alias_=*/false);
     tabular_t *t = (tabular_t *)malloc(sizeof(tabular_t));
     t->problem = problem;
     t->cols = problem->constraints;
@@ -1215,11 +1310,16 @@ int solve(tabular_t *tabular, int *base) {
     auto it = g_tabs.find(tabular);
     if (it == g_tabs.end()) SX_FATAL("solve: unknown tabular");
     Engine *E = it->second;
+    // the phase width: 1+n+2m as built, 1+n+m after the caller's `rows -= cols` (phase 2,
+    // twoPhaseMethod.cu:288); anything wider than the allocation is refused
+    if (tabular->rows < 2 || tabular->rows > E->N1 || tabular->cols != E->m ||
+        tabular->pitch != E->ld * sizeof(double))
+        SX_FATAL("solve: tabular_t fields do not match its newTabular allocation");
     E->write_base(base);
     long long piv = 0;
     int st = E->run_phase(tabular->rows, -1, &piv);
     E->read_base(base);
-    return st;
+    return public_status(st);
 }
 
 // tabular.cu:41-98, reference (transposed) orientation
@@ -1411,6 +1511,91 @@ void simplex_session_close(simplex_session *S) {
     if (!S) return;
     delete S->E;
     delete S;
+}
+
+// ---------------------------------------------------------------- synthetic sweep bench
+// SURVEY.md §8d config 3': the production sweep kernel (k_sweep) on a synthetic rows x cols
+// fp64 matrix -- entries uniform in [lo, hi] drawn as generateRandomProblem draws A
+// (problem.cu:49-126, seed's third CRT draw) -- with `pivots` random pending pivots: row
+// factors in [-1, 1), pivot rows in [lo, hi], distinct leaving rows (their entries take the
+// divide path of solver.cu:40-43).  The matrix is swept `warmup` + `iters` times in place;
+// the `iters` timed sweeps are bracketed by HIP events on the sweep's stream.  Returns the
+// average microseconds per sweep; *bytes = 16 * rows * cols (each element read and written
+// once, SURVEY.md §8d's 16 (m+1) N figure for this matrix).
+double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi, int pivots, int warmup, int iters,
+                           double *bytes) {
+    if (rows <= 0 || cols <= 1 || pivots < 1 || pivots > SX_KMAX || iters < 1 || rows < pivots) return -1.0;
+    const size_t ld = round_up((size_t)cols, 16);
+    hipStream_t s;
+    SX_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    uint32_t sd[3];
+    sx_crt_seeds(seed, 0, sd);
+    double *T = dalloc<double>((size_t)rows * ld);
+    double *U = dalloc<double>((size_t)SX_KMAX * ld);
+    double *F = dalloc<double>((size_t)rows * SX_KMAX);
+    PivRec *recs = dalloc<PivRec>(SX_KMAX);
+    unsigned long long *PM = dalloc<unsigned long long>(rows);
+    DevState *st = dalloc<DevState>(1);
+    SX_HIP(hipMemsetAsync(T, 0, sizeof(double) * (size_t)rows * ld, s));
+    // column 0 = b (first CRT seed), columns 1.. = A's rows (third), as generateRandomProblem
+    double *b_dev = dalloc<double>(rows);
+    sx_launch_gen_vector(sd[0], 0, rows, lo, hi, b_dev, s);
+    sx_launch_gen_rows(sd[2], cols - 1, rows, 0, rows, lo, hi, T, ld, nullptr, s);
+    SX_HIP(hipMemcpy2DAsync(T, ld * sizeof(double), b_dev, sizeof(double), sizeof(double), rows,
+                            hipMemcpyDeviceToDevice, s));
+    SX_HIP(hipStreamSynchronize(s));
+    (void)hipFree(b_dev);
+    SX_HIP(hipMemsetAsync(U, 0, sizeof(double) * SX_KMAX * ld, s));
+    for (int k = 0; k < pivots; ++k) sx_launch_gen_vector(sd[1] + 7919u * (unsigned)k, 0, cols, lo, hi, U + k * ld, s);
+    sx_launch_gen_vector(sd[1] ^ 0x9e3779b9u, 0, rows * SX_KMAX, -1, 1, F, s);
+    const unsigned B = 1;
+    std::vector<PivRec> rc(SX_KMAX);
+    std::vector<unsigned long long> pm((size_t)rows, 0ull);
+    for (int k = 0; k < SX_KMAX; ++k) {
+        rc[k].r = (int)(((long long)k * rows) / pivots % rows);
+        rc[k].e = k;
+        rc[k].p = 1.0 + (double)(k % 97);
+        if (k < pivots) pm[(size_t)rc[k].r] = ((unsigned long long)B << 32) | (1ull << k);
+    }
+    SX_HIP(hipMemcpyAsync(recs, rc.data(), sizeof(PivRec) * SX_KMAX, hipMemcpyHostToDevice, s));
+    SX_HIP(hipMemcpyAsync(PM, pm.data(), sizeof(unsigned long long) * rows, hipMemcpyHostToDevice, s));
+    DevState init;
+    std::memset(&init, 0, sizeof(init));
+    init.status = SX_NOT_ENDED;
+    init.batch_tag = B;
+    init.batch_count = pivots;
+    SX_HIP(hipMemcpyAsync(st, &init, sizeof(init), hipMemcpyHostToDevice, s));
+    Pending pd;
+    pd.U = U;
+    pd.F = F;
+    pd.recs = recs;
+    pd.PM = PM;
+    pd.batch = B;
+    pd.q = pivots;
+    const bool big = 8.0 * (double)rows * (double)cols > 256.0 * 1024 * 1024;
+    SweepCfg cfg;
+    cfg.batch = pivots;
+    cfg.rows_per_block = g_cfg.update_rows > 0 ? std::min(g_cfg.update_rows, 4) : (pivots > 16 ? 4 : 2);
+    cfg.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : (big ? 1 : 0);
+    long long sweeps = 0;
+    for (int w = 0; w < warmup; ++w, ++sweeps)
+        sx_launch_sweep(T, rows, ld, cols, nullptr, 0, pd, st, (int)(sweeps & 1), cfg, s);
+    hipEvent_t e0, e1;
+    SX_HIP(hipEventCreate(&e0));
+    SX_HIP(hipEventCreate(&e1));
+    SX_HIP(hipEventRecord(e0, s));
+    for (int it = 0; it < iters; ++it, ++sweeps)
+        sx_launch_sweep(T, rows, ld, cols, nullptr, 0, pd, st, (int)(sweeps & 1), cfg, s);
+    SX_HIP(hipEventRecord(e1, s));
+    SX_HIP(hipEventSynchronize(e1));
+    float ms = 0.f;
+    SX_HIP(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    for (void *p : {(void *)T, (void *)U, (void *)F, (void *)recs, (void *)PM, (void *)st}) (void)hipFree(p);
+    (void)hipStreamDestroy(s);
+    if (bytes) *bytes = 16.0 * (double)rows * (double)cols;
+    return 1e3 * (double)ms / (double)iters;
 }
 
 // ---------------------------------------------------------------- parity hooks

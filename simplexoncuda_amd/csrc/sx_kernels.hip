@@ -783,14 +783,15 @@ __device__ __forceinline__ int rec2_a(int k) { return (k >> 1) * SX_GA_STRIDE + 
 __device__ __forceinline__ int rec2_b(int k) { return (k >> 1) * SX_GB_STRIDE + (k & 1); }
 
 __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int rows, size_t ld, Cols c,
-                                               double *__restrict__ d, int *base, DevState *st, double *U, double *F,
-                                               PivRec *recs, unsigned long long *PM, unsigned B, int K, int NA,
-                                               int NB, BatchChan *ch, u64 *ga, u64 *gb, unsigned long long *stamps) {
+                                               double *__restrict__ d, double *__restrict__ d_save, int *base,
+                                               DevState *st, double *U, double *F, PivRec *recs,
+                                               unsigned long long *PM, unsigned B, int K, int NA, int NB,
+                                               BatchChan *ch, u64 *ga, u64 *gb, unsigned long long *stamps) {
     extern __shared__ double s_hist[];  // [K][512]: F history (ratio blocks) / U history (objective blocks)
     __shared__ double s_v[16];
     __shared__ int s_i[16];
     __shared__ double s_p[SX_KMAX];                  // pivots of the batch
-    __shared__ int s_r[SX_KMAX];                     // leaving rows of the batch
+    __shared__ int s_r[SX_KMAX], s_e[SX_KMAX];       // leaving rows / entering variables of the batch
     __shared__ double s_ue[SX_KMAX], s_fr[SX_KMAX];  // U[s][e] (entering column) / F[r][s] (leaving row)
     __shared__ double s_a[SX_TILE], s_b[SX_TILE];    // ratio blocks: entering column, RHS (winner lookup)
     __shared__ unsigned s_g[4 * SX_TILE];            // gathered granules
@@ -813,6 +814,10 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
     int status = SX_NOT_ENDED, cnt = 0, last_r = -1, last_e = -1;
     bool aborted = false;
     if (status0 == SX_NOT_ENDED) {
+        // the objective row as the batch found it, for the host to restore when the batch is
+        // aborted (SX_HANG): d is written only at the end of the batch, after hand-offs that
+        // need every block, so every block has copied its share before anything changes it
+        for (int j = blockIdx.x * blockDim.x + t; j < c.N; j += gridDim.x * blockDim.x) d_save[j] = d[j];
         // ratio block: its row; objective block: its logical column d[1 + ia]
         const int li = blockIdx.x * SX_TILE + t;
         const bool liveA = isA && li < rows;
@@ -925,6 +930,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
             if (t == 0) {
                 s_p[q] = p;
                 s_r[q] = r;
+                s_e[q] = e;
             }
             cnt = q + 1;
             last_r = r;
@@ -945,8 +951,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                         b = fma(f, br, b);
                     }
                 }
-                if (blockIdx.x == 0 && t == 0) {
-                    base[r] = e;  // solver.cu:105 (one writer per launch: this thread)
+                if (blockIdx.x == 0 && t == 0) {  // (base[r] = e, solver.cu:105: at the end of the batch)
                     recs[q].r = r;
                     recs[q].e = e;
                     recs[q].p = p;
@@ -1039,6 +1044,8 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                 __hip_atomic_store(&ch->abort_w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 return;
             }
+            // base[r] = e of every pivot, in order (solver.cu:105), only for a batch that completed
+            for (int s = 0; s < cnt; ++s) base[s_r[s]] = s_e[s];
             st->status = status;
             st->pivots = piv0 + cnt;
             if (cnt > 0) {
@@ -1091,8 +1098,9 @@ __device__ __forceinline__ double ld_sys(const double *p) {
 }
 
 __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, int rows, int row0, int rpr, size_t ld,
-                                                  Cols c, double *__restrict__ d, int *base, DevState *st, double *U,
-                                                  double *F, PivRec *recs, unsigned long long *PM, unsigned B, int K,
+                                                  Cols c, double *__restrict__ d, double *__restrict__ d_save, int *base,
+                                                  DevState *st, double *U, double *F, PivRec *recs,
+                                                  unsigned long long *PM, unsigned B, int K,
                                                   int slots, int W, int rank, int tb0, int tb1, int NBg,
                                                   BatchChan *ch, const u64 *ga, const u64 *gb, const u64 *gdone,
                                                   PeerView pv, unsigned long long timeout) {
@@ -1100,7 +1108,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
     __shared__ double s_v[16];
     __shared__ int s_i[16];
     __shared__ double s_p[SX_KMAX];
-    __shared__ int s_r[SX_KMAX];
+    __shared__ int s_r[SX_KMAX], s_e[SX_KMAX];
     __shared__ double s_ue[SX_KMAX], s_fr[SX_KMAX];
     __shared__ double s_a[SX_TILE], s_b[SX_TILE];
     __shared__ unsigned s_g[4 * SX_TILE];
@@ -1130,6 +1138,10 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
     double dj = liveB ? d[1 + ia] : 0.0;
     double d0 = (!isA && tb == 0 && t == 0) ? d[0] : 0.0;
     if (status0 == SX_NOT_ENDED) {
+        // this rank's whole objective row as the batch found it (restored by the host on
+        // SX_HANG): every rank writes d slices only at the end of the batch, after hand-offs
+        // that need every block of every rank, so this copy is complete before any change
+        for (int j = blockIdx.x * blockDim.x + t; j < c.N; j += gridDim.x * blockDim.x) d_save[j] = d[j];
         double b = liveA ? T[(size_t)li * ld] : 0.0;
         unsigned bits = 0u;
         // the entering column's stored value of this row: loaded as soon as the entering
@@ -1235,6 +1247,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
             if (t == 0) {
                 s_p[q] = p;
                 s_r[q] = r;
+                s_e[q] = e;
             }
             cnt = q + 1;
             last_r = r;
@@ -1255,8 +1268,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
                     }
                 }
                 if (blockIdx.x == 0 && t == 0) {  // every rank keeps the whole basis and the records
-                    base[r] = e;                  // solver.cu:105
-                    recs[q].r = r;
+                    recs[q].r = r;                // (base[r] = e, solver.cu:105: at the end of the batch)
                     recs[q].e = e;
                     recs[q].p = p;
                     U[(size_t)q * ld] = br;
@@ -1349,6 +1361,10 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
     }
     __syncthreads();
     if (!s_flag) return;
+    // every wave of this rank drained its system-scope stores (U, d, granules) before adding
+    // to exit_cnt; a system-scope release here orders them before the done granules
+    if (t == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __syncthreads();
     const unsigned dtag = make_tag(B, 0);
     if (t < W) put_g_sys(pv.gdone[t] + rank, aborted ? 1u : 0u, dtag);
     const bool ok = gather_tagged<decltype(ident), true>(gdone, W, ident, dtag, s_g, &ch->abort_w, &s_ok, timeout);
@@ -1361,6 +1377,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
         __hip_atomic_store(&ch->abort_w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
+    for (int s = 0; s < cnt; ++s) base[s_r[s]] = s_e[s];  // solver.cu:105, in pivot order
     st->status = status;
     st->pivots = piv0 + cnt;
     if (cnt > 0) {
@@ -1431,7 +1448,12 @@ __global__ __launch_bounds__(256) void k_sweep(double *__restrict__ T, int rows,
             const int i = i0 + k;
             if (i >= rows) break;
             // the row's factors: unconditional (wave-uniform, scalar) loads issued together --
-            // F rows hold SX_KMAX allocated doubles; slots >= cnt are loaded but not used
+            // F rows hold SX_KMAX allocated doubles; slots >= cnt are loaded but not used.
+            // Only a full batch (cnt == KT) runs the unguarded chain: a partial one (the last
+            // batch of a phase) takes the per-slot guarded path, about 2x slower per byte
+            // (1668 vs 851 us at config 5 with 20-pivot batches, profiles/r02_sweep_partial_batch.txt).
+            // Padding slots >= cnt with f = -0.0 (fma(-0, +0, y) = y exactly) instead cost every
+            // full sweep 40 % (1218 vs 851 us): 32 scalar selects per row behind spilled masks.
             const double *Fr = F + (size_t)i * SX_KMAX;
             double f[KT];
 #pragma unroll
@@ -1851,12 +1873,12 @@ bool sx_batch_fits(int rows, Cols c, int k) {
     return per_cu[k] > 0 && (long long)(NA + NB) <= (long long)per_cu[k] * cus - 16;
 }
 
-void sx_launch_batch(const double *T, int rows, size_t ld, Cols c, double *d, int *base, DevState *st,
-                     const Pending &pd, int k, BatchChan *chan, unsigned long long *ga, unsigned long long *gb,
-                     unsigned long long *stamps, hipStream_t s) {
+void sx_launch_batch(const double *T, int rows, size_t ld, Cols c, double *d, double *d_save, int *base,
+                     DevState *st, const Pending &pd, int k, BatchChan *chan, unsigned long long *ga,
+                     unsigned long long *gb, unsigned long long *stamps, hipStream_t s) {
     if (!sx_batch_fits(rows, c, k)) SX_FATAL("fused batch grid does not fit the device");
     const int NA = (rows + SX_TILE - 1) / SX_TILE, NB = (c.N - 1 + SX_TILE - 1) / SX_TILE;
-    k_batch<<<NA + NB, SX_TILE, batch_lds(k), s>>>(T, rows, ld, c, d, base, st, pd.U, pd.F, pd.recs, pd.PM,
+    k_batch<<<NA + NB, SX_TILE, batch_lds(k), s>>>(T, rows, ld, c, d, d_save, base, st, pd.U, pd.F, pd.recs, pd.PM,
                                                    pd.batch, k, NA, NB, chan, ga, gb, stamps);
 }
 
@@ -1877,15 +1899,15 @@ bool sx_batch_mr_fits(int slots, int nb_local, int k, int grids) {
     return per_cu[k] > 0 && (long long)grids * (slots + nb_local) <= (long long)per_cu[k] * cus - 16;
 }
 
-void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld, Cols c, double *d, int *base,
-                        DevState *st, const Pending &pd, int k, int slots, int W, int rank, int tb0, int tb1,
+void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld, Cols c, double *d, double *d_save,
+                        int *base, DevState *st, const Pending &pd, int k, int slots, int W, int rank, int tb0, int tb1,
                         BatchChan *chan, const unsigned long long *ga, const unsigned long long *gb,
                         const unsigned long long *gdone, const PeerView &pv, unsigned long long timeout,
                         hipStream_t s) {
     const int NBg = (c.N - 1 + SX_TILE - 1) / SX_TILE;
     if (W < 1 || W > SX_MAXW || W * slots > SX_TILE || NBg > SX_TILE || NBg < 1 || tb0 < 0 || tb1 > NBg || tb0 > tb1)
         SX_FATAL("multi-rank fused batch: bad shape");
-    k_batch_mr<<<slots + (tb1 - tb0), SX_TILE, batch_lds(k), s>>>(T, rows, row0, rpr, ld, c, d, base, st, pd.U, pd.F,
+    k_batch_mr<<<slots + (tb1 - tb0), SX_TILE, batch_lds(k), s>>>(T, rows, row0, rpr, ld, c, d, d_save, base, st, pd.U, pd.F,
                                                                   pd.recs, pd.PM, pd.batch, k, slots, W, rank, tb0,
                                                                   tb1, NBg, chan, ga, gb, gdone, pv, timeout);
 }

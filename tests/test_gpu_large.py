@@ -1,0 +1,74 @@
+"""BASELINE.json configs 4 and 5 at full size on the GPU, against oracle pins.
+
+tests/golden/large_pivots.json (tests/golden/scripts/make_large_fixtures.py, run in the build
+container) holds SHA-256 digests of the CPU oracle's phase-1 state -- logical tableau T
+(m x (1+n+2m) fp64), objective row d and basis -- after 48 phase-1 pivots of:
+  config4            generateRandomProblem(4096, 16384, 425984, 1, 100)
+  config5            generateRandomProblem(8192, 32768, 851968, 1, 100)
+  config5_degenerate generateRandomProblem(8192, 32768, 851968, -100, 100)
+Here the same instance is synthesised in HBM, 48 pivots run (one full 32-pivot batch and a
+partial one), and the digests of the GPU's state must match: on one shard (fused batch), on
+row-block virtual shards through both per-pivot exchanges (the W = 4 split of config 4, the
+W = 8 split of config 5), and through the peer-memory fused batch (W = 2, 3: the virtual
+shards' launches must run at once on one GPU's 4 hardware queues).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import simplexoncuda_amd as sx
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+with open(os.path.join(GOLDEN, "large_pivots.json")) as _f:
+    PINS = json.load(_f)
+
+
+def sha(a):
+    h = hashlib.sha256()
+    mv = memoryview(np.ascontiguousarray(a)).cast("B")
+    step = 1 << 28
+    for k in range(0, len(mv), step):
+        h.update(mv[k:k + step])
+    return h.hexdigest()
+
+
+def run(name, W=1, mode=0, p2p=-1):
+    pin = PINS[name]
+    n, m = pin["n"], pin["m"]
+    sx.set_virtual_ranks(W)
+    sx.set_exchange_mode(mode)
+    sx.set_p2p(p2p)
+    try:
+        sess = sx.Session(generated=(n, m, pin["seed"], pin["lo"], pin["hi"]))
+        tim = sess.pivots(pin["pivots"])
+        T, d, base = sess.tableau(m, pin["width"])
+        sess.close()
+    finally:
+        sx.set_virtual_ranks(1)
+        sx.set_exchange_mode(0)
+        sx.set_p2p(-1)
+    assert tim.pivots == pin["pivots"]
+    assert sha(base) == pin["sha256_base"]
+    assert float(d[0]) == pin["d0"]
+    assert sha(d) == pin["sha256_d"]
+    assert sha(T) == pin["sha256_T"]
+
+
+@pytest.mark.parametrize("W,mode,p2p", [(1, 0, -1), (4, 1, 0), (4, 2, 0), (2, 0, 1), (3, 0, 1)])
+def test_config4_pivots_match_oracle(gpu, W, mode, p2p):
+    run("config4", W, mode, p2p)
+
+
+@pytest.mark.parametrize("W,mode,p2p", [(1, 0, -1), (8, 1, 0), (8, 2, 0), (3, 0, 1)])
+def test_config5_pivots_match_oracle(gpu, W, mode, p2p):
+    run("config5", W, mode, p2p)
+
+
+@pytest.mark.parametrize("W,mode,p2p", [(1, 0, -1), (8, 1, 0), (2, 0, 1)])
+def test_config5_degenerate_variant_pivots_match_oracle(gpu, W, mode, p2p):
+    run("config5_degenerate", W, mode, p2p)

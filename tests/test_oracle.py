@@ -182,3 +182,23 @@ def test_phase1_build_b_negative_quirk():
     assert np.signbit(T[1][3]) and np.signbit(T[1][5])
     assert list(base) == [4, 5]
     assert list(d) == [0, 0, 0, 0, 0, 1, 1]
+
+
+# DEGENERATE (-3) pins: tests/golden/degenerate_cases.json (scripts/make_degenerate_cases.py)
+def test_degenerate_fixtures_reproduced():
+    with open(os.path.join(GOLDEN, "degenerate_cases.json")) as f:
+        cases = json.load(f)
+    for s in cases["small"]:
+        r = oracle.two_phase(np.array(s["A"]), np.array(s["b"]), np.array(s["c"]))
+        assert r["status"] == oracle.DEGENERATE == s["status"]
+        assert list(r["pivots"]) == s["pivots"] and r["base"].tolist() == s["base"]
+    e = cases["embedded"][0]
+    nb, mb, seed = e["big"]
+    s = cases["small"][e["small"]]
+    Ab, bb, cb = oracle.generate(nb, mb, seed, 1, 100)
+    As = np.array(s["A"])
+    A = np.zeros((mb + As.shape[0], nb + As.shape[1]))
+    A[:mb, :nb] = Ab
+    A[mb:, nb:] = As
+    r = oracle.two_phase(A, np.concatenate([bb, s["b"]]), np.concatenate([cb, s["c"]]))
+    assert r["status"] == oracle.DEGENERATE and list(r["pivots"]) == e["pivots"]
