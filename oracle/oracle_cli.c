@@ -48,5 +48,10 @@ int main(int argc, char **argv) {
     int st = orc_two_phase(n, m, A, b, c, cap, x, &opt, base, piv, &p1v);
     double t1 = now();
     printf("%d %lld %lld %.17g %.17g %.3f\n", st, (long long)piv[0], (long long)piv[1], opt, p1v, t1 - t0);
+    free(A);
+    free(b);
+    free(c);
+    free(x);
+    free(base);
     return 0;
 }

@@ -202,3 +202,32 @@ def test_degenerate_fixtures_reproduced():
     A[mb:, nb:] = As
     r = oracle.two_phase(A, np.concatenate([bb, s["b"]]), np.concatenate([cb, s["c"]]))
     assert r["status"] == oracle.DEGENERATE and list(r["pivots"]) == e["pivots"]
+
+
+# SURVEY.md §5 race/sanitizer row: the oracle built with -fsanitize=address,undefined
+# (oracle/Makefile `sanitize`) runs the examples and generated instances cleanly and agrees
+# with the plain build
+def test_oracle_under_sanitizers(tmp_path):
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(os.path.dirname(GOLDEN), "..", "oracle"), "sanitize"],
+                   check=True)
+    exe = os.path.join(os.path.dirname(GOLDEN), "..", "oracle", "oracle_cli_san")
+    with open(os.path.join(GOLDEN, "degenerate_cases.json")) as f:
+        s = json.load(f)["small"][0]
+    deg = tmp_path / "degenerate.txt"  # readProblemFromFile format (problem.cu:20-47)
+    A, b, c = np.array(s["A"]), np.array(s["b"]), np.array(s["c"])
+    lines = [f"{A.shape[1]} {A.shape[0]}", " ".join(repr(float(v)) for v in c)]
+    lines += [" ".join(repr(float(v)) for v in list(A[i]) + [b[i]]) for i in range(A.shape[0])]
+    deg.write_text("\n".join(lines) + "\n")
+    runs = [["file", os.path.join(EX, f)] for f in ("smallProblem.txt", "infeasibleProblem.txt",
+                                                    "unboundedProblem.txt")]
+    runs += [["file", str(deg)], ["gen", "20", "10", "2010"], ["gen", "256", "256", "25856"],
+             ["gen", "37", "600", "5", "-100", "100"]]
+    expect = {"smallProblem.txt": "0 2 2", "infeasibleProblem.txt": "-1 2 0", "unboundedProblem.txt": "-2 2 0",
+              "degenerate.txt": f"-3 {s['pivots'][0]} {s['pivots'][1]}", "25856": "0 459 25"}
+    for args in runs:
+        r = subprocess.run([exe] + args, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0 and "Sanitizer" not in r.stderr, r.stderr[-2000:]
+        key = os.path.basename(args[1]) if args[0] == "file" else args[3]
+        if key in expect:
+            assert r.stdout.startswith(expect[key]), (key, r.stdout)
