@@ -72,6 +72,14 @@ int simplex_p2p_ready(void);
 void simplex_last_phase_seconds(double *out);
 /* the sweep's grid: waves x (blocks resident on the device) blocks (default 1; <= 0 resets) */
 void simplex_set_update_waves(double waves);
+/* fused batches: a hand-off of up to 512 granules is polled by one wave (1, default) or by
+ * every thread of the block with a block vote per poll (0) */
+void simplex_set_gather_wide(int on);
+/* extra doubles appended to every tableau row of new engines (rounded up to 16; default 0) */
+void simplex_set_ld_pad(int doubles);
+/* several shards: keep d and U in uncached memory (1) or plain memory (0, default; uncached
+ * was measured to corrupt results after earlier allocations were freed -- diagnostic only) */
+void simplex_set_uncached_exchange(int on);
 
 /* ---- fault handling and test hooks ---- */
 /* a fused batch whose in-kernel hand-off wait times out (SIMPLEX_HANG, never expected) is

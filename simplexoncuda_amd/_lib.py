@@ -9,7 +9,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsimplex_hip.so")
+LIB_PATH = os.environ.get("SIMPLEX_LIB_PATH") or os.path.join(_HERE, "libsimplex_hip.so")  # (diagnostic override)
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int_p = ctypes.POINTER(ctypes.c_int)
@@ -102,6 +102,9 @@ SIGNATURES = {
     "simplex_set_p2p": (None, [ctypes.c_int]),
     "simplex_p2p_ready": (ctypes.c_int, []),
     "simplex_set_update_waves": (None, [ctypes.c_double]),
+    "simplex_set_gather_wide": (None, [ctypes.c_int]),
+    "simplex_set_ld_pad": (None, [ctypes.c_int]),
+    "simplex_set_uncached_exchange": (None, [ctypes.c_int]),
     "simplex_hang_recoveries": (ctypes.c_longlong, []),
     "simplex_fused_batches": (ctypes.c_longlong, []),
     "simplex_set_hang_inject": (None, [ctypes.c_longlong]),

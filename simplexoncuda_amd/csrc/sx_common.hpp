@@ -173,6 +173,7 @@ void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld,
                         const unsigned long long *gdone, const PeerView &pv, unsigned long long timeout,
                         hipStream_t s);
 void sx_set_update_waves(float w);  // resident-grid multiple of the sweep (default 1)
+void sx_set_gather_wide(int on);    // fused batches: one-wave gathers up to 512 granules (default 1)
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s);
 
 void sx_launch_coef(const double *d, const int *base, int row0, int rows, double *coef, hipStream_t s);

@@ -72,6 +72,8 @@ struct Config {
     bool no_timer = false;         // the multi-GPU self-check: never write TIMER CSVs
     long long inject_hang = -1;    // test hook: abort the n-th fused batch from now (-1 off)
     unsigned first_batch_id = 1;   // test hook: batch id of a new engine's first batch
+    int ld_pad = 0;                // extra doubles per tableau row (multiple of 16; row stride tuning)
+    int uncached_xchg = 0;         // several shards: d and U in uncached memory (diagnostic; see alloc_shard)
     long long hang_recoveries = 0; // fused batches aborted and re-run on the per-pivot path
     long long fused_batches = 0;   // fused batch launches (every shard's counted once)
     // distributed
@@ -236,7 +238,7 @@ class Engine {
         N = N1;
         alias = alias_ && g_cfg.alias && m > 0;
         Ns1 = alias ? N2 : N1;
-        ld = round_up((size_t)Ns1, 16);
+        ld = round_up((size_t)Ns1, 16) + (size_t)g_cfg.ld_pad;
         batch_id = (g_cfg.first_batch_id >= 1 && g_cfg.first_batch_id < SX_BATCH_IDS) ? g_cfg.first_batch_id : 1;
         if (g_cfg.dist && g_cfg.comm) {
             rccl = true;
@@ -409,10 +411,15 @@ class Engine {
     void alloc_shard(Shard &x) {
         const size_t rows_alloc = x.rows > 0 ? (size_t)x.rows : 1;
         x.T = dalloc<double>(rows_alloc * ld);
-        // several shards: d and U are written by other ranks' batches (peer memory over xGMI,
-        // system-scope stores) and read here by plain loads -- uncached, so no L2 of this
-        // device keeps a stale line of them
-        if (xchg) {
+        // d and U: plain device memory.  Other ranks write them over xGMI (system-scope stores)
+        // inside the multi-rank batch; this rank reads them only in later kernels, after the
+        // batch has seen every rank's done granule, across a kernel boundary.  Allocating them
+        // uncached instead (simplex_set_uncached_exchange(1)) was measured WRONG: after earlier
+        // engines had used and freed plain memory, a W = 8 virtual-shard solve diverged from
+        // the oracle in 3 of 3 runs (1126 / 1124 / 1181 phase-1 pivots instead of 1318), and
+        // never with plain memory (tools/_bisect_seq.py) -- dirty L2 lines of a
+        // page's earlier cached use written back over the uncached data is the likely cause.
+        if (xchg && g_cfg.uncached_xchg) {
             SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&x.d), round_up((size_t)N1, 16) * sizeof(double),
                                          hipDeviceMallocUncached));
             SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&x.U), (size_t)SX_KMAX * ld * sizeof(double),
@@ -1178,6 +1185,9 @@ void simplex_last_phase_seconds(double *out) {
     out[1] = g_phase_seconds[1];
 }
 void simplex_set_update_waves(double waves) { sx_set_update_waves((float)waves); }
+void simplex_set_gather_wide(int on) { sx_set_gather_wide(on); }
+void simplex_set_uncached_exchange(int on) { g_cfg.uncached_xchg = on ? 1 : 0; }
+void simplex_set_ld_pad(int doubles) { g_cfg.ld_pad = doubles > 0 ? (int)round_up((size_t)doubles, 16) : 0; }
 void simplex_set_exchange_mode(int mode) { g_cfg.exchange_mode = (mode >= 0 && mode <= 2) ? mode : 0; }
 void simplex_set_timer_dir(const char *dir) { g_cfg.timer_dir = dir ? dir : ""; }
 

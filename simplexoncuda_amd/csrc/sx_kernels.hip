@@ -24,17 +24,43 @@ __device__ __forceinline__ int cmp_eps(double x, double y) {
     return x < y ? -1 : 1;
 }
 
-// warpReduceMin (reduction.cu:10-22) on one 32-lane half of a wave64.
-__device__ __forceinline__ void half_argmin(double &v, int &i) {
-#pragma unroll
-    for (int off = 16; off > 0; off >>= 1) {
-        const double sv = __shfl_down(v, off, 32);
-        const int si = __shfl_down(i, off, 32);
-        if (cmp_eps(sv, v) < 0) {
-            v = sv;
-            i = si;
-        }
+// Lane i takes lane i + OFF's value inside its 16-lane DPP row (row_shl:OFF); a lane whose
+// source is past the row keeps its own value, as a CUDA shuffle past the warp's end does.
+template <int OFF>
+__device__ __forceinline__ int dpp_down(int x) {
+    return __builtin_amdgcn_update_dpp(x, x, 0x100 + OFF, 0xF, 0xF, false);
+}
+template <int OFF>
+__device__ __forceinline__ double dpp_down(double x) {
+    const long long b = __double_as_longlong(x);
+    const int lo = dpp_down<OFF>((int)b), hi = dpp_down<OFF>((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+template <int OFF>
+__device__ __forceinline__ void argmin_step(double &v, int &i, double sv, int si) {
+    if (cmp_eps(sv, v) < 0) {
+        v = sv;
+        i = si;
     }
+}
+
+// warpReduceMin (reduction.cu:10-22) on one 32-lane half of a wave64.  Every caller reads
+// the result of lane 0 of the half, whose inputs at every step come from lanes inside the
+// half (lanes 0..15 take 16..31, then 0..7 take 8..15, ...), so these are exactly the
+// reference's combines.  The offset-16 step crosses DPP rows (a bpermute shuffle); offsets
+// 8, 4, 2, 1 stay inside row 0 and use DPP row shifts (VALU, no LDS round trip).
+__device__ __forceinline__ void half_argmin(double &v, int &i) {
+#ifdef SX_SHFL_ARGMIN  // (diagnostic build: every step a bpermute shuffle)
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) argmin_step<0>(v, i, __shfl_down(v, off, 32), __shfl_down(i, off, 32));
+    return;
+#endif
+    argmin_step<16>(v, i, __shfl_down(v, 16, 32), __shfl_down(i, 16, 32));
+    argmin_step<8>(v, i, dpp_down<8>(v), dpp_down<8>(i));
+    argmin_step<4>(v, i, dpp_down<4>(v), dpp_down<4>(i));
+    argmin_step<2>(v, i, dpp_down<2>(v), dpp_down<2>(i));
+    argmin_step<1>(v, i, dpp_down<1>(v), dpp_down<1>(i));
 }
 
 // blockReduceMin (reduction.cu:24-49) for a 512-thread block (8 waves = 16 halves).
@@ -696,6 +722,9 @@ __device__ __forceinline__ u64 ld_sys(const u64 *p) {
     return __hip_atomic_load(const_cast<u64 *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// granules per lane of the one-wave gather (larger gathers use every thread of the block)
+#define SX_GATHER_PER_LANE 8
+
 // The block reads n <= 4 * blockDim granules, granule k at base[off(k)], each until it
 // carries `tag`, into out[k] (LDS): every thread polls its own granules (k = t, t + 512, ...),
 // all of them in flight together, until the block agrees that all have arrived.  Block-uniform
@@ -703,7 +732,8 @@ __device__ __forceinline__ u64 ld_sys(const u64 *p) {
 // thread of the block must call it.
 template <typename OFF, bool SYS = false>
 __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, unsigned *out, unsigned *abort_w,
-                              int *s_ok, unsigned long long timeout = 20000000ull, unsigned *pay = nullptr) {
+                              int *s_ok, unsigned long long timeout = 20000000ull, unsigned *pay = nullptr,
+                              int wide = 1) {
     // (pay: the payload of every even granule k goes to pay[k / 2] -- records of two granules)
     const int t = threadIdx.x, nt = blockDim.x;
     if (n <= 64) {  // one wave polls, no block barrier per poll
@@ -722,6 +752,49 @@ __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, uns
                     }
                 }
                 if (__ballot(!have) == 0ull) break;
+                if ((it & 63) == 63) {
+                    int stop = ld_sc1(abort_w) != 0u;
+                    if (!stop && __builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+                        __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        stop = 1;
+                    }
+                    if (__builtin_amdgcn_readfirstlane(stop)) {
+                        ok = 0;
+                        break;
+                    }
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (t == 0) *s_ok = ok;
+        }
+        __syncthreads();
+        return *s_ok != 0;
+    }
+    if (wide && n <= 64 * SX_GATHER_PER_LANE) {
+        // one wave polls up to SX_GATHER_PER_LANE granules per lane, all of a round's loads in
+        // flight together, and the block meets once at the end (no barrier per poll)
+        if (t < 64) {
+            unsigned miss = 0u;  // bit c: granule t + 64 c still missing
+#pragma unroll
+            for (int c = 0; c < SX_GATHER_PER_LANE; ++c)
+                if (t + 64 * c < n) miss |= 1u << c;
+            int ok = 1;
+            const u64 t0 = __builtin_amdgcn_s_memrealtime();
+            for (unsigned it = 0;; ++it) {
+                u64 w[SX_GATHER_PER_LANE];
+#pragma unroll
+                for (int c = 0; c < SX_GATHER_PER_LANE; ++c)
+                    if ((miss >> c) & 1u) w[c] = SYS ? ld_sys(base + off(t + 64 * c)) : ld_sc1(base + off(t + 64 * c));
+#pragma unroll
+                for (int c = 0; c < SX_GATHER_PER_LANE; ++c) {
+                    const int k = t + 64 * c;
+                    if (((miss >> c) & 1u) && ((unsigned)(w[c] >> 32) | SX_PAYMASK) == (tag | SX_PAYMASK)) {
+                        miss &= ~(1u << c);
+                        out[k] = (unsigned)w[c];
+                        if (pay && !(k & 1)) pay[k >> 1] = (unsigned)(w[c] >> 32) & SX_PAYMASK;
+                    }
+                }
+                if (__ballot(miss != 0u) == 0ull) break;
                 if ((it & 63) == 63) {
                     int stop = ld_sc1(abort_w) != 0u;
                     if (!stop && __builtin_amdgcn_s_memrealtime() - t0 > timeout) {
@@ -786,7 +859,8 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                                                double *__restrict__ d, double *__restrict__ d_save, int *base,
                                                DevState *st, double *U, double *F, PivRec *recs,
                                                unsigned long long *PM, unsigned B, int K, int NA, int NB,
-                                               BatchChan *ch, u64 *ga, u64 *gb, unsigned long long *stamps) {
+                                               BatchChan *ch, u64 *ga, u64 *gb, unsigned long long *stamps,
+                                               int gw) {
     extern __shared__ double s_hist[];  // [K][512]: F history (ratio blocks) / U history (objective blocks)
     __shared__ double s_v[16];
     __shared__ int s_i[16];
@@ -849,11 +923,26 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                 // ---- ratio tile: current entering column, ratios, tile winner
                 if (blockIdx.x == 0) SX_STAMP(0);
                 a = a_pre;
-                for (int s = 0; s < q; ++s) {
-                    if ((bits >> s) & 1u)
-                        a = a / s_p[s];
-                    else
-                        a = fma(s_hist[s * SX_TILE + t], s_ue[s], a);
+                // pending pivots of the batch, in order; LDS reads batched 8 slots at a time
+                // (slots past q read slot s0 and are not used)
+                for (int s0 = 0; s0 < q; s0 += 8) {
+                    double h[8], ue[8], pp[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int s = s0 + k < q ? s0 + k : s0;
+                        h[k] = s_hist[s * SX_TILE + t];
+                        ue[k] = s_ue[s];
+                        pp[k] = s_p[s];
+                    }
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        if (s0 + k < q) {
+                            if ((bits >> (s0 + k)) & 1u)
+                                a = a / pp[k];
+                            else
+                                a = fma(h[k], ue[k], a);
+                        }
+                    }
                 }
                 double rv = DBL_MAX;
                 int ri = -1, elig = 0;
@@ -888,7 +977,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                 if (blockIdx.x == 0) SX_STAMP(1);
             }
             // ---- selection: every block runs pass 2 over the ratio-tile winners
-            if (!gather_tagged(ga, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay)) {
+            if (!gather_tagged(ga, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay, gw)) {
                 aborted = true;
                 break;
             }
@@ -959,11 +1048,26 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                 }
             } else {
                 // ---- objective tile: current pivot row on this column, d, tile winner
-                for (int s = 0; s < q; ++s) {
-                    if (s_r[s] == r)
-                        u = u / s_p[s];
-                    else
-                        u = fma(s_fr[s], s_hist[s * SX_TILE + t], u);
+                for (int s0 = 0; s0 < q; s0 += 8) {  // (LDS reads batched as in the ratio tiles)
+                    double h[8], fr[8], pp[8];
+                    int rr[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int s = s0 + k < q ? s0 + k : s0;
+                        h[k] = s_hist[s * SX_TILE + t];
+                        fr[k] = s_fr[s];
+                        pp[k] = s_p[s];
+                        rr[k] = s_r[s];
+                    }
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        if (s0 + k < q) {
+                            if (rr[k] == r)
+                                u = u / pp[k];
+                            else
+                                u = fma(fr[k], h[k], u);
+                        }
+                    }
                 }
                 s_hist[q * SX_TILE + t] = u;
                 if (liveB && 1 + ia < c.Ns) U[(size_t)q * ld + mj] = u;
@@ -992,7 +1096,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                 if (tb == 0) SX_STAMP(4);
             }
             // ---- entering variable of pivot q + 1: every block runs pass 2 over the objective tiles
-            if (!gather_tagged(gb, 2 * NB, rec2_b, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay)) {
+            if (!gather_tagged(gb, 2 * NB, rec2_b, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay, gw)) {
                 aborted = true;
                 break;
             }
@@ -1103,7 +1207,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
                                                   unsigned long long *PM, unsigned B, int K,
                                                   int slots, int W, int rank, int tb0, int tb1, int NBg,
                                                   BatchChan *ch, const u64 *ga, const u64 *gb, const u64 *gdone,
-                                                  PeerView pv, unsigned long long timeout) {
+                                                  PeerView pv, unsigned long long timeout, int gw) {
     extern __shared__ double s_hist[];  // [K][512]: F history (ratio tiles) / U history (objective tiles)
     __shared__ double s_v[16];
     __shared__ int s_i[16];
@@ -1160,11 +1264,26 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
             double a = 0.0;
             if (isA) {
                 a = a_pre;
-                for (int s = 0; s < q; ++s) {
-                    if ((bits >> s) & 1u)
-                        a = a / s_p[s];
-                    else
-                        a = fma(s_hist[s * SX_TILE + t], s_ue[s], a);
+                // pending pivots of the batch, in order; LDS reads batched 8 slots at a time
+                // (slots past q read slot s0 and are not used)
+                for (int s0 = 0; s0 < q; s0 += 8) {
+                    double h[8], ue[8], pp[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int s = s0 + k < q ? s0 + k : s0;
+                        h[k] = s_hist[s * SX_TILE + t];
+                        ue[k] = s_ue[s];
+                        pp[k] = s_p[s];
+                    }
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        if (s0 + k < q) {
+                            if ((bits >> (s0 + k)) & 1u)
+                                a = a / pp[k];
+                            else
+                                a = fma(h[k], ue[k], a);
+                        }
+                    }
                 }
                 double rv = DBL_MAX;
                 int ri = -1, elig = 0;
@@ -1202,7 +1321,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
             }
             // ---- selection: pass 2 over every rank's ratio tiles
             if (!gather_tagged<decltype(gather_a), true>(ga, 2 * NAg, gather_a, tag, s_g, &ch->abort_w, &s_ok,
-                                                         timeout, s_pay)) {
+                                                         timeout, s_pay, gw)) {
                 aborted = true;
                 break;
             }
@@ -1274,11 +1393,26 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
                     U[(size_t)q * ld] = br;
                 }
             } else {
-                for (int s = 0; s < q; ++s) {
-                    if (s_r[s] == r)
-                        u = u / s_p[s];
-                    else
-                        u = fma(s_fr[s], s_hist[s * SX_TILE + t], u);
+                for (int s0 = 0; s0 < q; s0 += 8) {  // (LDS reads batched as in the ratio tiles)
+                    double h[8], fr[8], pp[8];
+                    int rr[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int s = s0 + k < q ? s0 + k : s0;
+                        h[k] = s_hist[s * SX_TILE + t];
+                        fr[k] = s_fr[s];
+                        pp[k] = s_p[s];
+                        rr[k] = s_r[s];
+                    }
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        if (s0 + k < q) {
+                            if (rr[k] == r)
+                                u = u / pp[k];
+                            else
+                                u = fma(fr[k], h[k], u);
+                        }
+                    }
                 }
                 s_hist[q * SX_TILE + t] = u;
                 if (liveB && 1 + ia < c.Ns)
@@ -1311,7 +1445,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
             }
             // ---- entering variable of pivot q + 1: pass 2 over every objective tile
             if (!gather_tagged<decltype(gather_b), true>(gb, 2 * NBg, gather_b, tag, s_g, &ch->abort_w, &s_ok,
-                                                         timeout, s_pay)) {
+                                                         timeout, s_pay, gw)) {
                 aborted = true;
                 break;
             }
@@ -1848,6 +1982,11 @@ void sx_launch_sweep(double *T, int rows, size_t ld, int Ns, const int *nact, in
         SX_FATAL("batch larger than SX_KMAX");
 }
 
+// fused batches: gathers of up to 512 granules polled by one wave (1, default) or by every
+// thread with a block vote per poll (0)
+static int g_gather_wide = 1;
+void sx_set_gather_wide(int on) { g_gather_wide = on ? 1 : 0; }
+
 static size_t batch_lds(int k) { return (size_t)k * SX_TILE * sizeof(double); }
 
 size_t sx_batch_granules_a() { return (size_t)SX_TILE * SX_GA_STRIDE; }
@@ -1879,7 +2018,7 @@ void sx_launch_batch(const double *T, int rows, size_t ld, Cols c, double *d, do
     if (!sx_batch_fits(rows, c, k)) SX_FATAL("fused batch grid does not fit the device");
     const int NA = (rows + SX_TILE - 1) / SX_TILE, NB = (c.N - 1 + SX_TILE - 1) / SX_TILE;
     k_batch<<<NA + NB, SX_TILE, batch_lds(k), s>>>(T, rows, ld, c, d, d_save, base, st, pd.U, pd.F, pd.recs, pd.PM,
-                                                   pd.batch, k, NA, NB, chan, ga, gb, stamps);
+                                                   pd.batch, k, NA, NB, chan, ga, gb, stamps, g_gather_wide);
 }
 
 bool sx_batch_mr_fits(int slots, int nb_local, int k, int grids) {
@@ -1909,7 +2048,8 @@ void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld,
         SX_FATAL("multi-rank fused batch: bad shape");
     k_batch_mr<<<slots + (tb1 - tb0), SX_TILE, batch_lds(k), s>>>(T, rows, row0, rpr, ld, c, d, d_save, base, st, pd.U, pd.F,
                                                                   pd.recs, pd.PM, pd.batch, k, slots, W, rank, tb0,
-                                                                  tb1, NBg, chan, ga, gb, gdone, pv, timeout);
+                                                                  tb1, NBg, chan, ga, gb, gdone, pv, timeout,
+                                                                  g_gather_wide);
 }
 
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s) {
