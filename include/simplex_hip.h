@@ -155,6 +155,22 @@ long long simplex_session_launch_log(simplex_session *s, long long *rows, double
 int simplex_session_stamps(simplex_session *s, int k, unsigned long long *out);
 void simplex_session_close(simplex_session *s);
 
+/* ---- multi-process peer-memory test mode (no RCCL; e.g. 2 processes on one GPU) ----
+ * Each process owns rank `rank` of `world` row-block shards (512-aligned blocks, as
+ * simplex_dist_init would make them) of a phase-1 state given in logical columns: T_rows =
+ * this rank's rows (ld_host doubles apart, width 1+n+2m), d and base whole.  The session's
+ * six peer-visible buffers are exported as IPC handles (simplex_ipc_handles_size() bytes);
+ * the caller gathers every rank's handles (rank order) and connects; simplex_session_pivots
+ * then runs fused multi-rank batches whose hand-offs cross the processes through those
+ * mappings.  Returns NULL / < 0 on failure.  Keep every process alive until all have
+ * finished their pivots before closing. */
+int simplex_ipc_handles_size(void);
+simplex_session *simplex_ipc_session_open(int n, int m, int rank, int world, const double *T_rows, long long ld_host,
+                                          const double *d, const int *base, unsigned char *handles_out);
+int simplex_ipc_session_connect(simplex_session *s, const unsigned char *all_handles);
+/* this process's rows of the resident tableau (logical columns), d and base; returns rows */
+long long simplex_session_rows(simplex_session *s, double *T_rows, long long ld_host, double *d, int *base);
+
 /* ---- kernel bench (SURVEY.md §8d config 3') ---- */
 /* the sweep kernel (solver.cu:34-46's update, `pivots` pending pivots per pass) on a synthetic
  * rows x cols fp64 matrix drawn like generateRandomProblem's A (seed, values in [lo, hi]) with

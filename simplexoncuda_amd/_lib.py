@@ -133,6 +133,12 @@ SIGNATURES = {
     "simplex_session_launch_log": (ctypes.c_longlong, [ctypes.c_void_p, c_ll_p, c_double_p, ctypes.c_longlong]),
     "simplex_session_close": (None, [ctypes.c_void_p]),
     "simplex_session_stamps": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_ulonglong)]),
+    "simplex_ipc_handles_size": (ctypes.c_int, []),
+    "simplex_ipc_session_open": (ctypes.c_void_p, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_double_p,
+                                                   ctypes.c_longlong, c_double_p, c_int_p, ctypes.c_char_p]),
+    "simplex_ipc_session_connect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),
+    "simplex_session_rows": (ctypes.c_longlong, [ctypes.c_void_p, c_double_p, ctypes.c_longlong, c_double_p,
+                                                 c_int_p]),
     "simplex_bench_sweep": (ctypes.c_double, [ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_int, ctypes.c_int,
                                               ctypes.c_int, ctypes.c_int, ctypes.c_int, c_double_p]),
     "simplex_dev_argmin": (ctypes.c_longlong, [c_double_p, ctypes.c_longlong, c_double_p]),

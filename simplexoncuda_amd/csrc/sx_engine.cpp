@@ -73,6 +73,7 @@ struct Config {
     long long inject_hang = -1;    // test hook: abort the n-th fused batch from now (-1 off)
     unsigned first_batch_id = 1;   // test hook: batch id of a new engine's first batch
     int ld_pad = 0;                // extra doubles per tableau row (multiple of 16; row stride tuning)
+    int ipc_rank = -1, ipc_world = 0;  // test hook: one shard per process, peers through IPC handles, no RCCL
     int uncached_xchg = 0;         // several shards: d and U in uncached memory (diagnostic; see alloc_shard)
     long long hang_recoveries = 0; // fused batches aborted and re-run on the per-pivot path
     long long fused_batches = 0;   // fused batch launches (every shard's counted once)
@@ -205,7 +206,8 @@ class Engine {
   public:
     int n = 0, m = 0;
     int W = 1;             // total shards (ranks)
-    bool rccl = false;     // true: one shard per process, collectives over RCCL
+    bool rccl = false;     // true: one shard per process (collectives over RCCL unless ipc)
+    bool ipc = false;      // one shard per process, peer buffers through caller-exchanged IPC handles only
     bool xchg = false;     // exchange path: tile allgather + pivot-row allreduce per pivot
     bool rowgather = false;  // exchange path variant: one allgather of tile winners with their rows
     size_t slot_stride = 0;  // doubles per row-gather slot (16-byte header + ld)
@@ -240,7 +242,10 @@ class Engine {
         Ns1 = alias ? N2 : N1;
         ld = round_up((size_t)Ns1, 16) + (size_t)g_cfg.ld_pad;
         batch_id = (g_cfg.first_batch_id >= 1 && g_cfg.first_batch_id < SX_BATCH_IDS) ? g_cfg.first_batch_id : 1;
-        if (g_cfg.dist && g_cfg.comm) {
+        if (g_cfg.ipc_world > 1) {
+            rccl = ipc = true;
+            W = g_cfg.ipc_world;
+        } else if (g_cfg.dist && g_cfg.comm) {
             rccl = true;
             W = g_cfg.world;
         } else if (g_cfg.virtual_ranks > 1) {
@@ -262,7 +267,7 @@ class Engine {
         rowgather = xchg && (g_cfg.exchange_mode == 2 || (g_cfg.exchange_mode == 0 && slot_bytes <= 1048576.0));
         std::vector<int> ranks;
         if (rccl)
-            ranks.push_back(g_cfg.rank);
+            ranks.push_back(ipc ? g_cfg.ipc_rank : g_cfg.rank);
         else
             for (int k = 0; k < W; ++k) ranks.push_back(k);
         for (int k : ranks) {
@@ -295,6 +300,7 @@ class Engine {
 
     void setup_peers() {
         std::memset(&pv, 0, sizeof(pv));
+        if (ipc) return;  // the caller connects the peers (connect_peers)
         if (!xchg || W > SX_MAXW || g_cfg.p2p == 0) return;
         if (rccl && !(g_cfg.p2p == 1 || g_cfg.p2p_ready)) return;
         SX_HIP(hipStreamSynchronize(s));
@@ -319,43 +325,63 @@ class Engine {
             return;
         }
         // one shard per process: exchange IPC handles of the six buffers over RCCL, map the peers'
-        struct Handles {
-            hipIpcMemHandle_t h[6];
-        };
         // (a failure here is not fatal: every rank learns whether all mapped, and they all fall
         // back to the RCCL exchange together)
-        Shard &x = sh[0];
-        Handles mine;
-        std::memset(&mine, 0, sizeof(mine));
-        void *bufs[6] = {x.T, x.ga, x.gb, x.gdone, x.U, x.d};
-        int ok = 1;
-        for (int k = 0; k < 6; ++k) ok &= hipIpcGetMemHandle(&mine.h[k], bufs[k]) == hipSuccess;
-        unsigned char *dev = dalloc<unsigned char>(sizeof(Handles) * W);
-        SX_HIP(hipMemcpy(dev + sizeof(Handles) * g_cfg.rank, &mine, sizeof(Handles), hipMemcpyHostToDevice));
-        SX_NCCL(ncclAllGather(dev + sizeof(Handles) * g_cfg.rank, dev, sizeof(Handles), ncclUint8, g_cfg.comm, s));
-        std::vector<Handles> all(W);
-        SX_HIP(hipMemcpyAsync(all.data(), dev, sizeof(Handles) * W, hipMemcpyDeviceToHost, s));
+        std::vector<unsigned char> all((size_t)W * kHandles);
+        int ok = export_handles(all.data() + (size_t)g_cfg.rank * kHandles);
+        unsigned char *dev = dalloc<unsigned char>(all.size());
+        SX_HIP(hipMemcpy(dev + (size_t)g_cfg.rank * kHandles, all.data() + (size_t)g_cfg.rank * kHandles, kHandles,
+                         hipMemcpyHostToDevice));
+        SX_NCCL(ncclAllGather(dev + (size_t)g_cfg.rank * kHandles, dev, kHandles, ncclUint8, g_cfg.comm, s));
+        SX_HIP(hipMemcpyAsync(all.data(), dev, all.size(), hipMemcpyDeviceToHost, s));
         SX_HIP(hipStreamSynchronize(s));
         (void)hipFree(dev);
-        std::vector<void *> mapped((size_t)W * 6, nullptr);
-        for (int r = 0; r < W && ok; ++r)
-            for (int k = 0; k < 6 && ok; ++k) {
-                if (r == g_cfg.rank) {
-                    mapped[(size_t)r * 6 + k] = bufs[k];
-                } else if (hipIpcOpenMemHandle(&mapped[(size_t)r * 6 + k], all[r].h[k],
-                                               hipIpcMemLazyEnablePeerAccess) == hipSuccess) {
-                    opened.push_back(mapped[(size_t)r * 6 + k]);
-                } else {
-                    ok = 0;
-                }
-            }
-        (void)hipGetLastError();
+        ok = ok && map_peers(all.data(), g_cfg.rank);
         if (!all_ranks(ok)) {
-            for (void *p : opened) (void)hipIpcCloseMemHandle(p);
-            opened.clear();
+            unmap_peers();
             if (g_cfg.verbose) say("peer memory unavailable: per-pivot RCCL exchange");
             return;
         }
+        p2p = true;
+    }
+
+    // IPC handles of this process's six exchanged buffers (T, ga, gb, gdone, U, d)
+    static constexpr size_t kHandles = 6 * sizeof(hipIpcMemHandle_t);
+    int export_handles(unsigned char *out) {
+        const Shard &x = sh[0];
+        void *bufs[6] = {x.T, x.ga, x.gb, x.gdone, x.U, x.d};
+        int ok = 1;
+        for (int k = 0; k < 6; ++k) {
+            hipIpcMemHandle_t h;
+            std::memset(&h, 0, sizeof(h));
+            ok &= hipIpcGetMemHandle(&h, bufs[k]) == hipSuccess;
+            std::memcpy(out + k * sizeof(h), &h, sizeof(h));
+        }
+        (void)hipGetLastError();
+        return ok;
+    }
+
+    // map every other rank's buffers from `all` (W x kHandles bytes) into pv; false if any fails
+    bool map_peers(const unsigned char *all, int me) {
+        const Shard &x = sh[0];
+        void *mine[6] = {x.T, x.ga, x.gb, x.gdone, x.U, x.d};
+        std::vector<void *> mapped((size_t)W * 6, nullptr);
+        bool ok = true;
+        for (int r = 0; r < W && ok; ++r)
+            for (int k = 0; k < 6 && ok; ++k) {
+                if (r == me) {
+                    mapped[(size_t)r * 6 + k] = mine[k];
+                    continue;
+                }
+                hipIpcMemHandle_t h;
+                std::memcpy(&h, all + (size_t)r * kHandles + k * sizeof(h), sizeof(h));
+                if (hipIpcOpenMemHandle(&mapped[(size_t)r * 6 + k], h, hipIpcMemLazyEnablePeerAccess) == hipSuccess)
+                    opened.push_back(mapped[(size_t)r * 6 + k]);
+                else
+                    ok = false;
+            }
+        (void)hipGetLastError();
+        if (!ok) return false;
         for (int r = 0; r < W; ++r) {
             void *const *p = &mapped[(size_t)r * 6];
             pv.T[r] = static_cast<const double *>(p[0]);
@@ -365,7 +391,13 @@ class Engine {
             pv.U[r] = static_cast<double *>(p[4]);
             pv.d[r] = static_cast<double *>(p[5]);
         }
-        p2p = true;
+        return true;
+    }
+
+    void unmap_peers() {
+        for (void *p : opened) (void)hipIpcCloseMemHandle(p);
+        opened.clear();
+        std::memset(&pv, 0, sizeof(pv));
     }
 
     // 1 on every rank iff `ok` on every rank (an RCCL min-allreduce; RCCL ranks only)
@@ -382,8 +414,8 @@ class Engine {
 
     void close_peers() {
         if (opened.empty()) return;
-        for (void *p : opened) (void)hipIpcCloseMemHandle(p);
-        opened.clear();
+        unmap_peers();
+        if (ipc) return;  // (the caller keeps every process alive until all have unmapped)
         // every rank has unmapped before any rank frees what the others mapped
         int *one = dalloc<int>(1);
         SX_NCCL(ncclAllReduce(one, one, 1, ncclInt, ncclSum, g_cfg.comm, s));
@@ -815,7 +847,7 @@ class Engine {
         }
         // peer ranks write into these records: no rank starts its next batch before every rank
         // has cleared its own (an RCCL all-reduce behind the memsets on every rank)
-        if (rccl) all_ranks(1);
+        if (rccl && !ipc) all_ranks(1);
         SX_HIP(hipStreamSynchronize(s));
     }
 
@@ -961,7 +993,7 @@ class Engine {
 
     // rows of the whole tableau (virtual or single shard only), logical columns: for tests
     // and printing (aliased artificial columns are expanded from their slack columns)
-    void download(double *T_host, size_t ld_host, int width, double *d_host) {
+    void download(double *T_host, size_t ld_host, int width, double *d_host, bool local_rows = false) {
         const Cols c = cols(width);
         std::vector<double> tmp;
         std::vector<int> perm;
@@ -978,7 +1010,7 @@ class Engine {
                                     x.rows, hipMemcpyDeviceToHost, s));
             SX_HIP(hipStreamSynchronize(s));
             for (int i = 0; i < x.rows; ++i) {
-                double *dst = T_host + (size_t)(x.row0 + i) * ld_host;
+                double *dst = T_host + (size_t)((local_rows ? 0 : x.row0) + i) * ld_host;
                 const double *src = tmp.data() + (size_t)i * c.Ns;
                 for (int j = 0; j < width; ++j) {
                     const int k = c.map(j);
@@ -992,12 +1024,13 @@ class Engine {
 
     // logical columns in; with aliasing only the stored columns are taken (the caller's
     // artificial columns must equal the slack columns, checked by the callers below)
-    void upload(const double *T_host, size_t ld_host, int width, const double *d_host, const int *base_host) {
+    void upload(const double *T_host, size_t ld_host, int width, const double *d_host, const int *base_host,
+                bool local_rows = false) {
         set_compact(false);  // a caller's tableau: any column may be touched
         const Cols c = cols(width);
         for (auto &x : sh) {
             if (x.rows > 0)
-                SX_HIP(hipMemcpy2DAsync(x.T, ld * sizeof(double), T_host + (size_t)x.row0 * ld_host,
+                SX_HIP(hipMemcpy2DAsync(x.T, ld * sizeof(double), T_host + (size_t)(local_rows ? 0 : x.row0) * ld_host,
                                         ld_host * sizeof(double), c.Ns * sizeof(double), x.rows,
                                         hipMemcpyHostToDevice, s));
             if (d_host) SX_HIP(hipMemcpyAsync(x.d, d_host, sizeof(double) * width, hipMemcpyHostToDevice, s));
@@ -1009,14 +1042,17 @@ class Engine {
 
 // true when a caller's phase-1-width tableau has every artificial column bit-identical to
 // its slack column (so the aliased storage represents it exactly)
-static bool artificial_equals_slack(const double *T, long long m, long long N, long long ld) {
-    const long long n = N - 1 - 2 * m;
-    if (n < 0 || m <= 0) return false;
-    for (long long i = 0; i < m; ++i) {
+static bool artificial_equals_slack(const double *T, long long rows, long long N, long long ld, long long n,
+                                    long long m) {
+    if (n < 0 || m <= 0 || N != 1 + n + 2 * m) return false;
+    for (long long i = 0; i < rows; ++i) {
         const double *row = T + i * ld;
         if (std::memcmp(row + 1 + n, row + 1 + n + m, sizeof(double) * (size_t)m) != 0) return false;
     }
     return true;
+}
+static bool artificial_equals_slack(const double *T, long long m, long long N, long long ld) {
+    return artificial_equals_slack(T, m, N, ld, N - 1 - 2 * m, m);
 }
 
 // tabular_t <-> engine
@@ -1521,6 +1557,54 @@ void simplex_session_close(simplex_session *S) {
     if (!S) return;
     delete S->E;
     delete S;
+}
+
+// ---- multi-process peer-memory test mode (no RCCL): see simplex_hip.h
+int simplex_ipc_handles_size(void) { return (int)Engine::kHandles; }
+
+simplex_session *simplex_ipc_session_open(int n, int m, int rank, int world, const double *T_rows, long long ld_host,
+                                          const double *d, const int *base, unsigned char *handles_out) {
+    if (world < 2 || world > SX_MAXW || rank < 0 || rank >= world) return nullptr;
+    const long long N1 = 1 + (long long)n + 2LL * m;
+    g_cfg.ipc_rank = rank;
+    g_cfg.ipc_world = world;
+    simplex_session *S = new simplex_session;
+    // probe the shard's row range with a throw-away shape first: aliasing needs this rank's rows
+    // to satisfy the artificial == slack invariant (true for any fresh phase-1 state)
+    const int W = world;
+    const int rpr = (int)round_up((size_t)((m + W - 1) / W), SX_TILE);
+    const int row0 = rank * rpr, rows = std::max(0, std::min(rpr, m - row0));
+    // (every rank must store the same columns: a rank without rows follows the invariant)
+    const bool alias = rows == 0 || artificial_equals_slack(T_rows, rows, N1, ld_host, n, m);
+    S->E = new Engine(n, m, alias);
+    g_cfg.ipc_rank = -1;
+    g_cfg.ipc_world = 0;
+    Engine &E = *S->E;
+    E.upload(T_rows, (size_t)ld_host, (int)N1, d, base, /*local_rows=*/true);
+    E.N = E.N1;
+    E.reset_state(-1);
+    E.enqueue_enter_partials();
+    SX_HIP(hipStreamSynchronize(E.s));
+    if (!E.export_handles(handles_out)) {
+        simplex_session_close(S);
+        return nullptr;
+    }
+    return S;
+}
+
+int simplex_ipc_session_connect(simplex_session *S, const unsigned char *all_handles) {
+    Engine &E = *S->E;
+    if (!E.ipc || !E.map_peers(all_handles, E.sh[0].rank)) return -1;
+    E.p2p = true;
+    return E.fused_ok(E.batch_size()) ? 0 : -2;
+}
+
+long long simplex_session_rows(simplex_session *S, double *T_rows, long long ld_host, double *d, int *base) {
+    Engine &E = *S->E;
+    if (ld_host < E.N) return -1;
+    E.download(T_rows, (size_t)ld_host, E.N, d, /*local_rows=*/true);
+    E.read_base(base);
+    return E.sh[0].rows;
 }
 
 // ---------------------------------------------------------------- synthetic sweep bench
