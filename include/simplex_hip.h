@@ -149,9 +149,10 @@ long long simplex_session_total_pivots(simplex_session *s);
  * duration in microseconds; returns the number of sweeps logged (at most cap are copied) */
 long long simplex_session_launch_log(simplex_session *s, long long *rows, double *update_us, long long cap);
 /* diagnostic: one fused batch of k pivots with in-kernel timestamps (100 MHz ticks) at the
- * hand-off points, out[k][8]: 0 ratio block 0 starts the pivot, 1 its tile published,
- * 3 objective block 0 knows the selection, 4 its tile published, 5 ratio block 0 knows the
- * next entering variable; -1 when the fused path is not in use */
+ * hand-off points, out[k][8]: 0 ratio block 0 starts the pivot, 2 its ratios computed, 1 its
+ * tile published, 3 objective block 0 knows the selection, 6 it has the leaving row's details,
+ * 7 its pivot-row values, 4 its tile published, 5 ratio block 0 knows the next entering
+ * variable; -1 when the fused path is not in use */
 int simplex_session_stamps(simplex_session *s, int k, unsigned long long *out);
 void simplex_session_close(simplex_session *s);
 

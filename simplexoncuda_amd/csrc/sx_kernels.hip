@@ -954,6 +954,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                         ri = li;
                     }
                 }
+                if (blockIdx.x == 0) SX_STAMP(2);
                 s_a[t] = a;
                 s_b[t] = b;
                 const int any = __syncthreads_or(elig);
@@ -1048,6 +1049,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                 }
             } else {
                 // ---- objective tile: current pivot row on this column, d, tile winner
+                if (tb == 0) SX_STAMP(6);
                 for (int s0 = 0; s0 < q; s0 += 8) {  // (LDS reads batched as in the ratio tiles)
                     double h[8], fr[8], pp[8];
                     int rr[8];
@@ -1070,6 +1072,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                     }
                 }
                 s_hist[q * SX_TILE + t] = u;
+                if (tb == 0) SX_STAMP(7);
                 if (liveB && 1 + ia < c.Ns) U[(size_t)q * ld + mj] = u;
                 const double fd = -dmin / p;  // updateCostsVector, solver.cu:48-56
                 if (tb == 0 && t == 0) d0 = fma(fd, br, d0);

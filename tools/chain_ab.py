@@ -25,7 +25,8 @@ def stamps_summary(s, k=32, nb=6):
         st = st.astype(np.int64)
         for q in range(k - 1):
             a, nxt = st[q], st[q + 1, 0]
-            rows.append([a[1] - a[0], a[3] - a[1], a[4] - a[3], a[5] - a[4], nxt - a[5], nxt - a[0]])
+            rows.append([a[2] - a[0], a[1] - a[2], a[3] - a[1], a[6] - a[3], a[7] - a[6], a[4] - a[7], a[5] - a[4],
+                         nxt - a[5], nxt - a[0]])
     return np.median(np.array(rows) * 0.01, axis=0)
 
 
@@ -40,7 +41,8 @@ def main():
     (name, vals), = args.items()
     setter = {"gather_wide": lib.simplex_set_gather_wide, "ld_pad": lib.simplex_set_ld_pad}[name]
     reset = {"gather_wide": 1, "ld_pad": 0}[name]
-    print("stamps: ratio tile | -> selection | objective tile | -> entering | entering history | pivot (us)")
+    print("stamps (us): ratio compute | ratio argmin+publish | -> selection seen | pass2 + row details |"
+          " row compute | obj argmin+publish | -> entering seen | entering history | pivot")
     for r in range(rounds):
         for cfg in configs:
             n, m, seed = bench.CONFIGS[cfg]
