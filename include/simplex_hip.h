@@ -75,6 +75,9 @@ void simplex_set_update_waves(double waves);
 /* fused batches: a hand-off of up to 512 granules is polled by one wave (1, default) or by
  * every thread of the block with a block vote per poll (0) */
 void simplex_set_gather_wide(int on);
+/* one shard: the fused batch's tile records are written in n copies (1..8) and each block polls
+ * copy blockIdx % n, spreading the pollers of a large grid (default 1) */
+void simplex_set_record_replicas(int n);
 /* extra doubles appended to every tableau row of new engines (rounded up to 16; default 0) */
 void simplex_set_ld_pad(int doubles);
 /* several shards: keep d and U in uncached memory (1) or plain memory (0, default; uncached

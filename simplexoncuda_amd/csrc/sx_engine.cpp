@@ -87,6 +87,19 @@ struct Config {
 Config g_cfg;
 std::mutex g_mu;
 
+// The granule records of the RCCL ranks' peer-memory batch are polled inside a launch while
+// other GPUs write them, so they are uncached.  Uncached and cached allocations must not
+// trade pages within a process: after virtual-shard runs had allocated and freed uncached
+// records, later single-GPU batches diverged from the oracle (tests/test_gpu_parity.py run
+// in order).  So the uncached records are allocated once per process (after an
+// L2 write-back, so no dirty line of the pages' earlier cached use lands on them later) and
+// never freed; everything else, virtual shards included, uses plain device memory.
+struct UncachedRecords {
+    unsigned long long *ga = nullptr, *gb = nullptr, *gdone = nullptr;
+    bool busy = false;
+};
+UncachedRecords g_urec;
+
 void say(const char *s) {
     if (g_cfg.verbose) {
         printf("%s\n", s);
@@ -489,19 +502,30 @@ class Engine {
         x.base = dalloc<int>(m);
         x.enter_parts = dalloc<TilePart>(SX_TILE);
         x.chan = dalloc<BatchChan>(1);
-        if (xchg) {
-            // polled by other ranks' writers: uncached (no stale line in any L2)
+        if (rccl && !ipc && !g_urec.busy) {
+            // polled while other GPUs write them: the process's uncached records (g_urec)
+            if (!g_urec.ga) {
+                sx_launch_l2_writeback(s);
+                SX_HIP(hipStreamSynchronize(s));
+                SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&g_urec.ga), sx_batch_granules_a() * 8,
+                                             hipDeviceMallocUncached));
+                SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&g_urec.gb), sx_batch_granules_b() * 8,
+                                             hipDeviceMallocUncached));
+                SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&g_urec.gdone), SX_MAXW * 8,
+                                             hipDeviceMallocUncached));
+            }
+            g_urec.busy = true;
             x.uncached = true;
-            SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&x.ga), sx_batch_granules_a() * 8,
-                                         hipDeviceMallocUncached));
-            SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&x.gb), sx_batch_granules_b() * 8,
-                                         hipDeviceMallocUncached));
-            SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&x.gdone), SX_MAXW * 8, hipDeviceMallocUncached));
-            SX_HIP(hipMemsetAsync(x.gdone, 0, SX_MAXW * 8, s));
+            x.ga = g_urec.ga;
+            x.gb = g_urec.gb;
+            x.gdone = g_urec.gdone;
         } else {
+            // one device (virtual shards, processes sharing a GPU): plain memory, sc1 hand-offs
             x.ga = dalloc<unsigned long long>(sx_batch_granules_a());
             x.gb = dalloc<unsigned long long>(sx_batch_granules_b());
+            if (xchg) x.gdone = dalloc<unsigned long long>(SX_MAXW);
         }
+        if (x.gdone) SX_HIP(hipMemsetAsync(x.gdone, 0, SX_MAXW * 8, s));
         SX_HIP(hipMemsetAsync(x.chan, 0, sizeof(BatchChan), s));
         SX_HIP(hipMemsetAsync(x.ga, 0, sx_batch_granules_a() * sizeof(unsigned long long), s));
         SX_HIP(hipMemsetAsync(x.gb, 0, sx_batch_granules_b() * sizeof(unsigned long long), s));
@@ -524,6 +548,10 @@ class Engine {
     }
 
     void free_shard(Shard &x) {
+        if (x.uncached) {  // the process's uncached records stay allocated (g_urec)
+            x.ga = x.gb = x.gdone = nullptr;
+            g_urec.busy = false;
+        }
         for (void *p : {(void *)x.T, (void *)x.d, (void *)x.d_save, (void *)x.colE, (void *)x.prow, (void *)x.prow_send,
                         (void *)x.slot_send, (void *)x.slot_all, (void *)x.U, (void *)x.F, (void *)x.recs, (void *)x.PM,
                         (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
@@ -1222,6 +1250,7 @@ void simplex_last_phase_seconds(double *out) {
 }
 void simplex_set_update_waves(double waves) { sx_set_update_waves((float)waves); }
 void simplex_set_gather_wide(int on) { sx_set_gather_wide(on); }
+void simplex_set_record_replicas(int n) { sx_set_record_replicas(n); }
 void simplex_set_uncached_exchange(int on) { g_cfg.uncached_xchg = on ? 1 : 0; }
 void simplex_set_ld_pad(int doubles) { g_cfg.ld_pad = doubles > 0 ? (int)round_up((size_t)doubles, 16) : 0; }
 void simplex_set_exchange_mode(int mode) { g_cfg.exchange_mode = (mode >= 0 && mode <= 2) ? mode : 0; }

@@ -703,11 +703,6 @@ __device__ __forceinline__ unsigned make_tag(unsigned B, int q) {
 __device__ __forceinline__ void put_g(u64 *g, unsigned data, unsigned tag) {
     __hip_atomic_store(g, ((u64)tag << 32) | data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void put_gd(u64 *g, double v, unsigned tag) {  // a double: 2 granules
-    const u64 b = (u64)__double_as_longlong(v);
-    put_g(g, (unsigned)b, tag);
-    put_g(g + 1, (unsigned)(b >> 32), tag);
-}
 __device__ __forceinline__ double gd(unsigned lo, unsigned hi) {
     return __longlong_as_double((long long)(((u64)hi << 32) | lo));
 }
@@ -853,6 +848,10 @@ __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, uns
 #define SX_GA_STRIDE (8 + 2 * SX_KMAX)  // ratio tile: v(2, payload: idx, elig) pad(2) a(2) b(2) | F[r][s] (2 per slot)
 #define SX_GB_STRIDE (4 + 2 * SX_KMAX)  // objective tile: v(2, payload: idx) pad(2) | U[s][e] (2 per slot)
 __device__ __forceinline__ int rec2_a(int k) { return (k >> 1) * SX_GA_STRIDE + (k & 1); }
+// granules of one replica of all tile records (k_batch keeps up to SX_GREP replicas)
+#define SX_GREP 8
+__host__ __device__ __forceinline__ size_t sx_ga_size() { return (size_t)SX_TILE * SX_GA_STRIDE; }
+__host__ __device__ __forceinline__ size_t sx_gb_size() { return (size_t)SX_TILE * SX_GB_STRIDE; }
 __device__ __forceinline__ int rec2_b(int k) { return (k >> 1) * SX_GB_STRIDE + (k & 1); }
 
 __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int rows, size_t ld, Cols c,
@@ -860,7 +859,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                                                DevState *st, double *U, double *F, PivRec *recs,
                                                unsigned long long *PM, unsigned B, int K, int NA, int NB,
                                                BatchChan *ch, u64 *ga, u64 *gb, unsigned long long *stamps,
-                                               int gw) {
+                                               int gw, int nrep) {
     extern __shared__ double s_hist[];  // [K][512]: F history (ratio blocks) / U history (objective blocks)
     __shared__ double s_v[16];
     __shared__ int s_i[16];
@@ -874,6 +873,11 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
     __shared__ double s_wv;
     const int t = threadIdx.x;
     const bool isA = (int)blockIdx.x < NA;
+    // the tile records are written in nrep replicas; a block polls replica blockIdx % nrep, so
+    // the ~200 pollers of a large grid spread over nrep copies of each line (speed only: every
+    // replica carries the same granules)
+    const u64 *gam = ga + (size_t)(blockIdx.x % nrep) * sx_ga_size();
+    const u64 *gbm = gb + (size_t)(blockIdx.x % nrep) * sx_gb_size();
     // stamps (diagnostic, normally null): s_memrealtime (100 MHz) at hand-off points of ratio
     // block 0 and objective block 0, [q][8]
 #define SX_STAMP(k)                                                                           \
@@ -963,22 +967,26 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                     s_win = ri >= 0 ? ri - (int)blockIdx.x * SX_TILE : 0;
                     s_wv = rv;
                 }
+                if (t == 0) s_flag = ri >= 0 ? (int)(ri - (int)blockIdx.x * SX_TILE) : (int)SX_NOIDX;
                 __syncthreads();
-                u64 *g = ga + (size_t)blockIdx.x * SX_GA_STRIDE;
                 const int wl = s_win;
-                if (t == 0) {
-                    const unsigned pl = (ri >= 0 ? (unsigned)(ri - (int)blockIdx.x * SX_TILE) : SX_NOIDX) |
-                                        ((unsigned)any << 10);
-                    put_gd(g, s_wv, tag | pl);
-                    put_gd(g + 4, s_a[wl], tag);
-                    put_gd(g + 6, s_b[wl], tag);
-                } else if (t - 1 < q) {
-                    put_gd(g + 8 + 2 * (t - 1), s_hist[(t - 1) * SX_TILE + wl], tag);  // F[winner][s]
+                {  // the record: v (payload: index, "any" bit), pad, a, b, then F[winner][s] for s < q
+                    const unsigned pl = (unsigned)s_flag | ((unsigned)any << 10);
+                    const int nG = 8 + 2 * q;
+                    for (int idx = t; idx < nrep * nG; idx += SX_TILE) {
+                        const int r = idx / nG, k = idx - r * nG;
+                        if (k == 2 || k == 3) continue;
+                        const double val = k < 2 ? s_wv : k < 6 ? s_a[wl] : k < 8 ? s_b[wl]
+                                                                           : s_hist[((k - 8) >> 1) * SX_TILE + wl];
+                        const unsigned long long bits64 = (unsigned long long)__double_as_longlong(val);
+                        put_g(ga + (size_t)r * sx_ga_size() + (size_t)blockIdx.x * SX_GA_STRIDE + k,
+                              (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64, k < 2 ? (tag | pl) : tag);
+                    }
                 }
                 if (blockIdx.x == 0) SX_STAMP(1);
             }
             // ---- selection: every block runs pass 2 over the ratio-tile winners
-            if (!gather_tagged(ga, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay, gw)) {
+            if (!gather_tagged(gam, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay, gw)) {
                 aborted = true;
                 break;
             }
@@ -1010,7 +1018,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
             // the objective blocks' pivot-row load does not wait for the winner's details
             double u = liveB ? T[(size_t)r * ld + mj] : 0.0;
             const int wt = r / SX_TILE;
-            if (!gather_tagged(ga + (size_t)wt * SX_GA_STRIDE + 4, 4 + 2 * q, [](int k) { return k; }, tag, s_g,
+            if (!gather_tagged(gam + (size_t)wt * SX_GA_STRIDE + 4, 4 + 2 * q, [](int k) { return k; }, tag, s_g,
                                &ch->abort_w, &s_ok)) {
                 aborted = true;
                 break;
@@ -1092,14 +1100,22 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                     s_flag = i;
                 }
                 __syncthreads();
-                u64 *g = gb + (size_t)tb * SX_GB_STRIDE;
-                if (t == 0) put_gd(g, s_wv, tag | (s_flag >= 0 ? (unsigned)(s_flag - tb * SX_TILE) : SX_NOIDX)); else if (t - 1 <= q) {
-                    put_gd(g + 4 + 2 * (t - 1), s_hist[(t - 1) * SX_TILE + s_win], tag);  // U[s][winner]
+                {  // the record: v (payload: index), pad, then U[s][winner] for s <= q
+                    const unsigned pl = s_flag >= 0 ? (unsigned)(s_flag - tb * SX_TILE) : SX_NOIDX;
+                    const int nG = 4 + 2 * (q + 1);
+                    for (int idx = t; idx < nrep * nG; idx += SX_TILE) {
+                        const int r = idx / nG, k = idx - r * nG;
+                        if (k == 2 || k == 3) continue;
+                        const double val = k < 2 ? s_wv : s_hist[((k - 4) >> 1) * SX_TILE + s_win];
+                        const unsigned long long bits64 = (unsigned long long)__double_as_longlong(val);
+                        put_g(gb + (size_t)r * sx_gb_size() + (size_t)tb * SX_GB_STRIDE + k,
+                              (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64, k < 2 ? (tag | pl) : tag);
+                    }
                 }
                 if (tb == 0) SX_STAMP(4);
             }
             // ---- entering variable of pivot q + 1: every block runs pass 2 over the objective tiles
-            if (!gather_tagged(gb, 2 * NB, rec2_b, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay, gw)) {
+            if (!gather_tagged(gbm, 2 * NB, rec2_b, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay, gw)) {
                 aborted = true;
                 break;
             }
@@ -1125,7 +1141,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
             if (isA && blockIdx.x == 0) SX_STAMP(5);
             // the ratio blocks need the pending pivot rows' entries in the new entering column
             if (isA && q + 1 < K && e >= 0 && cmp_eps(dmin, 0.0) < 0) {
-                if (!gather_tagged(gb + (size_t)(e / SX_TILE) * SX_GB_STRIDE + 4, 2 * (q + 1), [](int k) { return k; },
+                if (!gather_tagged(gbm + (size_t)(e / SX_TILE) * SX_GB_STRIDE + 4, 2 * (q + 1), [](int k) { return k; },
                                    tag, s_g, &ch->abort_w, &s_ok)) {
                     aborted = true;
                     break;
@@ -1190,11 +1206,6 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
 // arrays are uncached allocations.  The same arithmetic, trees and order as k_batch.
 __device__ __forceinline__ void put_g_sys(u64 *g, unsigned data, unsigned tag) {
     __hip_atomic_store(g, ((u64)tag << 32) | data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void put_gd_sys(u64 *g, double v, unsigned tag) {
-    const u64 b = (u64)__double_as_longlong(v);
-    put_g_sys(g, (unsigned)b, tag);
-    put_g_sys(g + 1, (unsigned)(b >> 32), tag);
 }
 __device__ __forceinline__ void st_sys(double *p, double v) {
     __hip_atomic_store(reinterpret_cast<u64 *>(p), (u64)__double_as_longlong(v), __ATOMIC_RELAXED,
@@ -1309,16 +1320,18 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
                 }
                 __syncthreads();
                 const int wl = s_win;
-                for (int k = 0; k < W; ++k) {
-                    u64 *g = pv.ga[k] + (size_t)gt * SX_GA_STRIDE;
-                    if (t == 0) {
-                        const unsigned pl = (s_flag >= 0 ? (unsigned)(s_flag - gt * SX_TILE) : SX_NOIDX) |
-                                            ((unsigned)any << 10);
-                        put_gd_sys(g, s_wv, tag | pl);
-                        put_gd_sys(g + 4, s_a[wl], tag);
-                        put_gd_sys(g + 6, s_b[wl], tag);
-                    } else if (t - 1 < q) {
-                        put_gd_sys(g + 8 + 2 * (t - 1), s_hist[(t - 1) * SX_TILE + wl], tag);
+                {  // the record (v, pad, a, b, F[winner][s < q]) into every rank's copy, one granule per thread
+                    const unsigned pl = (s_flag >= 0 ? (unsigned)(s_flag - gt * SX_TILE) : SX_NOIDX) |
+                                        ((unsigned)any << 10);
+                    const int nG = 8 + 2 * q;
+                    for (int idx = t; idx < W * nG; idx += SX_TILE) {
+                        const int rk = idx / nG, k = idx - rk * nG;
+                        if (k == 2 || k == 3) continue;
+                        const double val = k < 2 ? s_wv : k < 6 ? s_a[wl] : k < 8 ? s_b[wl]
+                                                                           : s_hist[((k - 8) >> 1) * SX_TILE + wl];
+                        const unsigned long long bits64 = (unsigned long long)__double_as_longlong(val);
+                        put_g_sys(pv.ga[rk] + (size_t)gt * SX_GA_STRIDE + k,
+                                  (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64, k < 2 ? (tag | pl) : tag);
                     }
                 }
             }
@@ -1438,11 +1451,16 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
                     s_flag = i;
                 }
                 __syncthreads();
-                for (int k = 0; k < W; ++k) {
-                    u64 *g = pv.gb[k] + (size_t)tb * SX_GB_STRIDE;
-                    if (t == 0)
-                        put_gd_sys(g, s_wv, tag | (s_flag >= 0 ? (unsigned)(s_flag - tb * SX_TILE) : SX_NOIDX)); else if (t - 1 <= q) {
-                        put_gd_sys(g + 4 + 2 * (t - 1), s_hist[(t - 1) * SX_TILE + s_win], tag);
+                {  // the record (v, pad, U[s <= q][winner]) into every rank's copy, one granule per thread
+                    const unsigned pl = s_flag >= 0 ? (unsigned)(s_flag - tb * SX_TILE) : SX_NOIDX;
+                    const int nG = 4 + 2 * (q + 1);
+                    for (int idx = t; idx < W * nG; idx += SX_TILE) {
+                        const int rk = idx / nG, k = idx - rk * nG;
+                        if (k == 2 || k == 3) continue;
+                        const double val = k < 2 ? s_wv : s_hist[((k - 4) >> 1) * SX_TILE + s_win];
+                        const unsigned long long bits64 = (unsigned long long)__double_as_longlong(val);
+                        put_g_sys(pv.gb[rk] + (size_t)tb * SX_GB_STRIDE + k,
+                                  (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64, k < 2 ? (tag | pl) : tag);
                     }
                 }
             }
@@ -1989,11 +2007,13 @@ void sx_launch_sweep(double *T, int rows, size_t ld, int Ns, const int *nact, in
 // thread with a block vote per poll (0)
 static int g_gather_wide = 1;
 void sx_set_gather_wide(int on) { g_gather_wide = on ? 1 : 0; }
+static int g_record_replicas = 1;
+void sx_set_record_replicas(int n) { g_record_replicas = n < 1 ? 1 : n > SX_GREP ? SX_GREP : n; }
 
 static size_t batch_lds(int k) { return (size_t)k * SX_TILE * sizeof(double); }
 
-size_t sx_batch_granules_a() { return (size_t)SX_TILE * SX_GA_STRIDE; }
-size_t sx_batch_granules_b() { return (size_t)SX_TILE * SX_GB_STRIDE; }
+size_t sx_batch_granules_a() { return sx_ga_size() * SX_GREP; }
+size_t sx_batch_granules_b() { return sx_gb_size() * SX_GREP; }
 
 bool sx_batch_fits(int rows, Cols c, int k) {
     if (k < 1 || k > SX_KMAX || rows <= 0) return false;
@@ -2021,7 +2041,8 @@ void sx_launch_batch(const double *T, int rows, size_t ld, Cols c, double *d, do
     if (!sx_batch_fits(rows, c, k)) SX_FATAL("fused batch grid does not fit the device");
     const int NA = (rows + SX_TILE - 1) / SX_TILE, NB = (c.N - 1 + SX_TILE - 1) / SX_TILE;
     k_batch<<<NA + NB, SX_TILE, batch_lds(k), s>>>(T, rows, ld, c, d, d_save, base, st, pd.U, pd.F, pd.recs, pd.PM,
-                                                   pd.batch, k, NA, NB, chan, ga, gb, stamps, g_gather_wide);
+                                                   pd.batch, k, NA, NB, chan, ga, gb, stamps, g_gather_wide,
+                                                   g_record_replicas);
 }
 
 bool sx_batch_mr_fits(int slots, int nb_local, int k, int grids) {
@@ -2054,6 +2075,13 @@ void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld,
                                                                   tb1, NBg, chan, ga, gb, gdone, pv, timeout,
                                                                   g_gather_wide);
 }
+
+// every XCD's L2 writes back its dirty lines (blocks are dealt over all XCDs; each block's
+// first wave issues an agent-scope release: buffer_wbl2)
+__global__ void k_l2_writeback() {
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+}
+void sx_launch_l2_writeback(hipStream_t s) { k_l2_writeback<<<4096, 64, 0, s>>>(); }
 
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s) {
     int g = (N + 255) / 256;

@@ -3,7 +3,8 @@ W untimed + K timed phase-1 pivots; per pivot: wall time, sweep time (HIP events
 (the chain: the fused batch + slack exchanges), plus the in-kernel stamp breakdown of one batch.
 
 usage: python tools/chain_ab.py <setting>=<v1>,<v2> [config=config5,config3] [rounds=2]
-  settings: gather_wide (simplex_set_gather_wide), ld_pad (simplex_set_ld_pad)"""
+  settings: gather_wide (simplex_set_gather_wide), ld_pad (simplex_set_ld_pad),
+            replicas (simplex_set_record_replicas)"""
 import os
 import sys
 
@@ -39,8 +40,9 @@ def main():
     configs = args.pop("config", "config5,config3").split(",")
     rounds = int(args.pop("rounds", "2"))
     (name, vals), = args.items()
-    setter = {"gather_wide": lib.simplex_set_gather_wide, "ld_pad": lib.simplex_set_ld_pad}[name]
-    reset = {"gather_wide": 1, "ld_pad": 0}[name]
+    setter = {"gather_wide": lib.simplex_set_gather_wide, "ld_pad": lib.simplex_set_ld_pad,
+              "replicas": lib.simplex_set_record_replicas}[name]
+    reset = {"gather_wide": 1, "ld_pad": 0, "replicas": 1}[name]
     print("stamps (us): ratio compute | ratio argmin+publish | -> selection seen | pass2 + row details |"
           " row compute | obj argmin+publish | -> entering seen | entering history | pivot")
     for r in range(rounds):
