@@ -733,16 +733,14 @@ class Engine {
 
     // ---------------------------------------------------------------- one pivot
     SweepCfg sweep_cfg(int batch) const {
-        // Measured in the real pivot loop (tools/sweep_update.py on MI355X, config 3):
-        // write-through (sc1) stores pay once the shard exceeds the 256 MB Infinity Cache;
-        // 4 rows per step at 32 pivots per sweep (138 us), 2 rows at 16 (127 us).
-        double bytes = 0.0;
-        for (auto &x : sh) bytes = std::max(bytes, 8.0 * (double)x.rows * (double)cols(N).Ns);
-        const bool big = bytes > 256.0 * 1024 * 1024;
+        // Measured on MI355X: 4 rows per step at 32 pivots per sweep (config 3: 138 us), 2 rows
+        // at 16 (127 us); write-through (sc1) stores faster at every size from 32 MiB to
+        // 512 MiB (tools/sweep_bench_ab.py, profiles/r02_sweep_sc1_sizes.txt: 4096 x 8192
+        // 98 vs 110 us, 1024 x 4096 17.8 vs 22 us), so they are on by default.
         SweepCfg c;
         c.batch = batch;
         c.rows_per_block = g_cfg.update_rows > 0 ? std::min(g_cfg.update_rows, 4) : (batch > 16 ? 4 : 2);
-        c.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : (big ? 1 : 0);
+        c.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : 1;
         // peer ranks read leaving rows straight from this tableau (system-scope loads over
         // xGMI): its stores must write through to memory, not stay dirty in an L2 of this device
         if (p2p && rccl) c.sc1 = 1;
@@ -1695,11 +1693,10 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     pd.PM = PM;
     pd.batch = B;
     pd.q = pivots;
-    const bool big = 8.0 * (double)rows * (double)cols > 256.0 * 1024 * 1024;
     SweepCfg cfg;
     cfg.batch = pivots;
     cfg.rows_per_block = g_cfg.update_rows > 0 ? std::min(g_cfg.update_rows, 4) : (pivots > 16 ? 4 : 2);
-    cfg.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : (big ? 1 : 0);
+    cfg.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : 1;  // (as sweep_cfg: write-through at every size)
     long long sweeps = 0;
     for (int w = 0; w < warmup; ++w, ++sweeps)
         sx_launch_sweep(T, rows, ld, cols, nullptr, 0, pd, st, (int)(sweeps & 1), cfg, s);
