@@ -78,6 +78,10 @@ void simplex_set_gather_wide(int on);
 /* one shard: the fused batch's tile records are written in n copies (1..8) and each block polls
  * copy blockIdx % n, spreading the pollers of a large grid (default 1) */
 void simplex_set_record_replicas(int n);
+/* full-batch sweeps staged through LDS by LDS-DMA with d stages per wave (rows per step as
+ * simplex_set_update_rows: 4 rows with d = 2 or 3, 2 rows with d = 4, 1 row with d = 4; 0 = the
+ * register sweep, default; measured no faster) */
+void simplex_set_sweep_stages(int d);
 /* extra doubles appended to every tableau row of new engines (rounded up to 16; default 0) */
 void simplex_set_ld_pad(int doubles);
 /* several shards: keep d and U in uncached memory (1) or plain memory (0, default; uncached

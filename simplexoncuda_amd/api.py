@@ -339,6 +339,11 @@ def set_update_waves(w):
     _lib.load().simplex_set_update_waves(float(w))
 
 
+def set_sweep_stages(d):
+    """Full-batch sweeps staged through LDS by LDS-DMA, d stages per wave (0: register sweep)."""
+    _lib.load().simplex_set_sweep_stages(int(d))
+
+
 def set_verbose(on):
     _lib.load().simplex_set_verbose(1 if on else 0)
 

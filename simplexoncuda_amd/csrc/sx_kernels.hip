@@ -1651,6 +1651,150 @@ __global__ __launch_bounds__(256) void k_sweep(double *__restrict__ T, int rows,
     }
 }
 
+// One row of the sweep (the arithmetic of k_sweep above, shared by the staged variant).
+template <int KT>
+__device__ __forceinline__ double2 sweep_row(double2 y, const double2 (&u)[KT], const double *__restrict__ F,
+                                             const PivRec *__restrict__ recs, const unsigned long long *__restrict__ PM,
+                                             int i, unsigned B, unsigned mask, int cnt) {
+    const double *Fr = F + (size_t)i * SX_KMAX;
+    double f[KT];
+#pragma unroll
+    for (int s = 0; s < KT; ++s) f[s] = Fr[s];
+    const unsigned bits = pend_bits(PM, i, B, mask);
+    if (bits == 0u && cnt == KT) {
+#pragma unroll
+        for (int s = 0; s < KT; ++s) {
+            y.x = fma(f[s], u[s].x, y.x);
+            y.y = fma(f[s], u[s].y, y.y);
+        }
+    } else if (bits == 0u) {
+#pragma unroll
+        for (int s = 0; s < KT; ++s) {
+            if (s < cnt) {
+                y.x = fma(f[s], u[s].x, y.x);
+                y.y = fma(f[s], u[s].y, y.y);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < KT; ++s) {
+            if (s < cnt) {
+                if ((bits >> s) & 1u) {
+                    const double p = recs[s].p;
+                    y.x = y.x / p;
+                    y.y = y.y / p;
+                } else {
+                    y.x = fma(f[s], u[s].x, y.x);
+                    y.y = fma(f[s], u[s].y, y.y);
+                }
+            }
+        }
+    }
+    return y;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// The same sweep with the tableau reads staged through LDS by LDS-DMA (global_load_lds_dwordx4,
+// no VGPR destination): each wave keeps D - 1 row groups of its own 1 KB column slice in
+// flight ahead of the one it updates, where k_sweep holds one group in registers.  A wave
+// reads back only what it loaded itself, so no block barrier is needed: a counted
+// `s_waitcnt vmcnt` retires a stage (the DMA is inline asm, invisible to the compiler's own
+// counting; every iteration issues exactly RB loads -- past its last group it re-reads that
+// group -- and RB stores, so the counts are exact).  Same operations, same order as k_sweep.
+template <int KT, int RB, bool SC1, int D>
+__global__ __launch_bounds__(256) void k_sweep_lds(double *__restrict__ T, int rows, size_t ld, int Ns,
+                                                   const int *__restrict__ nact, int s0,
+                                                   const double *__restrict__ F, const double *__restrict__ U,
+                                                   const PivRec *__restrict__ recs,
+                                                   const unsigned long long *__restrict__ PM,
+                                                   const DevState *__restrict__ st, unsigned B, int rev) {
+    __shared__ double2 stage[D][RB][256];
+    const int cnt = st->batch_tag == B ? st->batch_count : 0;
+    if (cnt <= 0) return;
+    if (nact && s0 + *nact < Ns) Ns = s0 + *nact;
+    const int cb = (Ns + 511) / 512;
+    const int lin = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    const int G = (int)(gridDim.x * gridDim.y) / cb;
+    const int tile = lin % cb, gy = lin / cb;
+    if (gy >= G) return;
+    const int bx = rev ? cb - 1 - tile : tile;
+    const int j = (bx * 256 + (int)threadIdx.x) * 2;
+    if (j >= Ns) return;  // (whole lanes leave; a wave's DMA runs on the lanes left)
+    const int ng = (rows + RB - 1) / RB;
+    const int nmy = gy < ng ? (ng - gy + G - 1) / G : 0;
+    if (nmy == 0) return;
+    const unsigned mask = slot_mask(cnt);
+    const int w = (int)threadIdx.x >> 6;
+    double2 u[KT];
+#pragma unroll
+    for (int s = 0; s < KT; ++s)
+        u[s] = s < cnt ? *reinterpret_cast<const double2 *>(U + (size_t)s * ld + j) : make_double2(0.0, 0.0);
+    // the stage buffers of this wave (LDS byte addresses, wave-uniform)
+    const unsigned lds0 = (unsigned)(uintptr_t)&stage[0][0][w * 64];
+    auto first_row = [&](int it) {  // first row of this block's it-th group (past the last: the last)
+        const int g = gy + (it < nmy ? it : nmy - 1) * G;
+        return (rev ? ng - 1 - g : g) * RB;
+    };
+    auto issue = [&](int it) {
+        const int i0 = first_row(it);
+        const unsigned sb = lds0 + (unsigned)((it % D) * RB * 256 * 16);
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+            const int i = i0 + k < rows ? i0 + k : rows - 1;
+            const double *src = T + (size_t)i * ld + j;
+            unsigned keep;
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
+                         "s_mov_b32 m0, %0"
+                         : "=&s"(keep)
+                         : "v"(src), "s"(__builtin_amdgcn_readfirstlane(sb + (unsigned)(k * 256 * 16)))
+                         : "memory");
+        }
+    };
+#pragma unroll
+    for (int it = 0; it < D - 1; ++it) issue(it);
+    const int oob = (int)(ld * 8);
+    for (int it = 0; it < nmy; ++it) {
+        issue(it + D - 1);
+        // ops issued after stage it's loads: steady state 2 RB (D - 1); the first D - 1
+        // iterations RB (D - 1 + it)
+        if (it >= D - 1) {
+            wait_vm<2 * RB * (D - 1)>();
+        } else if (it == 0) {
+            wait_vm<RB * (D - 1)>();
+        } else if (it == 1) {
+            wait_vm<RB * D>();
+        } else if (it == 2) {
+            wait_vm<RB * (D + 1)>();
+        } else if (it == 3) {
+            wait_vm<RB * (D + 2)>();
+        } else {
+            wait_vm<RB * (D - 1)>();  // (D > 5: conservative)
+        }
+        const int i0 = first_row(it);
+        const int sl = it % D;
+        double2 x[RB];
+#pragma unroll
+        for (int k = 0; k < RB; ++k) x[k] = stage[sl][k][threadIdx.x];
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+            const int i = i0 + k;
+            const bool live = i < rows;
+            const double2 y = sweep_row<KT>(x[k], u, F, recs, PM, live ? i : i0, B, mask, cnt);
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(T + (size_t)(live ? i : i0) * ld, 0, oob, 0x00020000);
+            // (a row past the end: the store goes out of range and is dropped -- one store per
+            // row slot always, so the counts above hold)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, live ? j * 8 : oob, 0,
+                                                   SC1 ? 16 : 0);
+        }
+    }
+    wait_vm<0>();  // (the DMA of the trailing re-reads lands before the block's LDS is released)
+}
+
 // Slack compaction (sx_common.hpp Cols), between a batch's selections and its
 // sweep.  The first time row r leaves the basis, its slack column -- still the unit vector e_r
 // as built, never swept -- is exchanged with the slack column at the first untouched stored
@@ -1985,10 +2129,41 @@ void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, in
     k_activate<<<1, 256, 0, s>>>(perm, iperm, act, nact, m, T, rows, row0, ld, s0, pd.U, pd.recs, st, pd.batch);
 }
 
+// the LDS-staged sweep (k_sweep_lds): stages per wave, 0 = the register sweep
+static int g_sweep_stages = 0;
+void sx_set_sweep_stages(int d) { g_sweep_stages = d < 0 ? 0 : d; }
+
+template <int RB, int D>
+static void launch_sweep_lds_t(double *T, int rows, size_t ld, int Ns, const int *nact, int s0, const Pending &pd,
+                               const DevState *st, int rev, hipStream_t s) {
+    const int cb = (Ns + 511) / 512;
+    dim3 grid(cb, row_slots(sweep_capacity(k_sweep_lds<SX_KMAX, RB, true, D>), cb, rows, RB));
+    k_sweep_lds<SX_KMAX, RB, true, D><<<grid, 256, 0, s>>>(T, rows, ld, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st,
+                                                           pd.batch, rev);
+}
+
+static bool launch_sweep_lds(int rb, int d, double *T, int rows, size_t ld, int Ns, const int *nact, int s0,
+                             const Pending &pd, const DevState *st, int rev, hipStream_t s) {
+#define SX_LDS_CASE(R, DD)                                                      \
+    if (rb == R && d == DD) {                                                   \
+        launch_sweep_lds_t<R, DD>(T, rows, ld, Ns, nact, s0, pd, st, rev, s); \
+        return true;                                                            \
+    }
+    SX_LDS_CASE(4, 2)
+    SX_LDS_CASE(4, 3)
+    SX_LDS_CASE(2, 4)
+    SX_LDS_CASE(1, 4)
+#undef SX_LDS_CASE
+    return false;
+}
+
 void sx_launch_sweep(double *T, int rows, size_t ld, int Ns, const int *nact, int s0, const Pending &pd,
                      const DevState *st, int rev, SweepCfg cfg, hipStream_t s) {
     if (rows <= 0) return;
     const int k = cfg.batch;  // pivots the sweep may have to apply (register slots)
+    if (g_sweep_stages > 0 && k > 16 && k <= SX_KMAX && cfg.sc1 &&
+        launch_sweep_lds(cfg.rows_per_block, g_sweep_stages, T, rows, ld, Ns, nact, s0, pd, st, rev, s))
+        return;
     if (k <= 1)
         launch_sweep_k<1>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, nact, s0, pd, st, rev, s);
     else if (k <= 4)

@@ -208,7 +208,8 @@ def _pivots_with(cfg, T, d, base, k):
     Tg, dg, bg = T.copy(), d.copy(), base.copy()
     setters = {"batch": (sx.set_batch, 0), "rb": (sx.set_update_rows, 0), "sc1": (sx.set_store_sc1, -1),
                "fused": (sx.set_fused, -1), "p2p": (sx.set_p2p, -1),
-               "waves": (sx.set_update_waves, 0), "W": (sx.set_virtual_ranks, 1)}
+               "waves": (sx.set_update_waves, 0), "W": (sx.set_virtual_ranks, 1),
+               "stages": (sx.set_sweep_stages, 0)}
     try:
         for key, val in cfg.items():
             setters[key][0](val)
@@ -282,6 +283,19 @@ def test_sweep_grid_bit_exact(gpu, sc1, waves):
     T, d, base = _phase1_state(210, 1700, 3)
     Tg, dg, bg, st, done = _pivots_with({"sc1": sc1, "waves": waves, "batch": 16}, T, d, base, 90)
     oracle.solve(T, d, base, max_pivots=90)
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+@pytest.mark.parametrize("rb,stages", [(4, 2), (4, 3), (2, 4), (1, 4)])
+@pytest.mark.parametrize("waves", [1e-4, 1])
+def test_sweep_lds_staged_bit_exact(gpu, rb, stages, waves):
+    """the LDS-DMA staged sweep (k_sweep_lds): every built stage depth and row step, one block
+    per column tile (long row walks: every pipeline stage reused) and the resident grid; full
+    batches of 32 and a partial last batch (register sweep)"""
+    T, d, base = _phase1_state(210, 1700, 3)
+    Tg, dg, bg, st, done = _pivots_with({"stages": stages, "rb": rb, "waves": waves, "batch": 32}, T, d, base, 70)
+    oracle.solve(T, d, base, max_pivots=70)
+    assert done == 70
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 

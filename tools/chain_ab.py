@@ -4,7 +4,9 @@ W untimed + K timed phase-1 pivots; per pivot: wall time, sweep time (HIP events
 
 usage: python tools/chain_ab.py <setting>=<v1>,<v2> [config=config5,config3] [rounds=2]
   settings: gather_wide (simplex_set_gather_wide), ld_pad (simplex_set_ld_pad),
-            replicas (simplex_set_record_replicas)"""
+            replicas (simplex_set_record_replicas),
+            sweep (rows per step:LDS stages, simplex_set_update_rows + simplex_set_sweep_stages;
+                   e.g. sweep=4:0,4:3,1:8 -- stages 0 = the register sweep)"""
 import os
 import sys
 
@@ -40,16 +42,21 @@ def main():
     configs = args.pop("config", "config5,config3").split(",")
     rounds = int(args.pop("rounds", "2"))
     (name, vals), = args.items()
+    def set_sweep(v):
+        rb, d = (int(x) for x in str(v).split(":"))
+        lib.simplex_set_update_rows(rb)
+        lib.simplex_set_sweep_stages(d)
+
     setter = {"gather_wide": lib.simplex_set_gather_wide, "ld_pad": lib.simplex_set_ld_pad,
-              "replicas": lib.simplex_set_record_replicas}[name]
-    reset = {"gather_wide": 1, "ld_pad": 0, "replicas": 1}[name]
+              "replicas": lib.simplex_set_record_replicas, "sweep": set_sweep}[name]
+    reset = {"gather_wide": 1, "ld_pad": 0, "replicas": 1, "sweep": "0:0"}[name]
     print("stamps (us): ratio compute | ratio argmin+publish | -> selection seen | pass2 + row details |"
           " row compute | obj argmin+publish | -> entering seen | entering history | pivot")
     for r in range(rounds):
         for cfg in configs:
             n, m, seed = bench.CONFIGS[cfg]
             for v in vals.split(","):
-                setter(int(v))
+                setter(v if name == "sweep" else int(v))
                 s = sx.Session(generated=(n, m, seed, 1, 100))
                 s.pivots(64)
                 tim = s.pivots(PIVOTS[cfg], time_updates=1)
