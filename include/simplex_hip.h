@@ -82,6 +82,9 @@ void simplex_set_record_replicas(int n);
  * simplex_set_update_rows: 4 rows with d = 2 or 3, 2 rows with d = 4, 1 row with d = 4; 0 = the
  * register sweep, default; measured no faster) */
 void simplex_set_sweep_stages(int d);
+/* fused batches: pause between two polls of a hand-off, s_sleep 0/1/2/4/8/16 for k = 0..5
+ * (default 1; diagnostic) */
+void simplex_set_poll_sleep(int k);
 /* extra doubles appended to every tableau row of new engines (rounded up to 16; default 0) */
 void simplex_set_ld_pad(int doubles);
 /* several shards: keep d and U in uncached memory (1) or plain memory (0, default; uncached

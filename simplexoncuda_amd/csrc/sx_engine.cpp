@@ -1250,6 +1250,7 @@ void simplex_set_update_waves(double waves) { sx_set_update_waves((float)waves);
 void simplex_set_gather_wide(int on) { sx_set_gather_wide(on); }
 void simplex_set_record_replicas(int n) { sx_set_record_replicas(n); }
 void simplex_set_sweep_stages(int d) { sx_set_sweep_stages(d); }
+void simplex_set_poll_sleep(int k) { sx_set_poll_sleep(k); }
 void simplex_set_uncached_exchange(int on) { g_cfg.uncached_xchg = on ? 1 : 0; }
 void simplex_set_ld_pad(int doubles) { g_cfg.ld_pad = doubles > 0 ? (int)round_up((size_t)doubles, 16) : 0; }
 void simplex_set_exchange_mode(int mode) { g_cfg.exchange_mode = (mode >= 0 && mode <= 2) ? mode : 0; }
@@ -1647,7 +1648,7 @@ long long simplex_session_rows(simplex_session *S, double *T_rows, long long ld_
 double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi, int pivots, int warmup, int iters,
                            double *bytes) {
     if (rows <= 0 || cols <= 1 || pivots < 1 || pivots > SX_KMAX || iters < 1 || rows < pivots) return -1.0;
-    const size_t ld = round_up((size_t)cols, 16);
+    const size_t ld = round_up((size_t)cols, 16) + (size_t)g_cfg.ld_pad;  // (ld_pad: sparse-row layouts)
     hipStream_t s;
     SX_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     uint32_t sd[3];

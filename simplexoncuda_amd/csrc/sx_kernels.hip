@@ -720,6 +720,19 @@ __device__ __forceinline__ u64 ld_sys(const u64 *p) {
 // granules per lane of the one-wave gather (larger gathers use every thread of the block)
 #define SX_GATHER_PER_LANE 8
 
+// pause between two polls of a hand-off (s_sleep units of 64 clocks; diagnostic knob, default 1)
+__constant__ int c_poll_sleep = 1;
+__device__ __forceinline__ void poll_pause() {
+    switch (c_poll_sleep) {
+    case 0: break;
+    case 1: __builtin_amdgcn_s_sleep(1); break;
+    case 2: __builtin_amdgcn_s_sleep(2); break;
+    case 3: __builtin_amdgcn_s_sleep(4); break;
+    case 4: __builtin_amdgcn_s_sleep(8); break;
+    default: __builtin_amdgcn_s_sleep(16); break;
+    }
+}
+
 // The block reads n <= 4 * blockDim granules, granule k at base[off(k)], each until it
 // carries `tag`, into out[k] (LDS): every thread polls its own granules (k = t, t + 512, ...),
 // all of them in flight together, until the block agrees that all have arrived.  Block-uniform
@@ -758,7 +771,7 @@ __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, uns
                         break;
                     }
                 }
-                __builtin_amdgcn_s_sleep(1);
+                poll_pause();
             }
             if (t == 0) *s_ok = ok;
         }
@@ -801,7 +814,7 @@ __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, uns
                         break;
                     }
                 }
-                __builtin_amdgcn_s_sleep(1);
+                poll_pause();
             }
             if (t == 0) *s_ok = ok;
         }
@@ -839,7 +852,7 @@ __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, uns
             __syncthreads();
             if (!*s_ok) return false;
         }
-        __builtin_amdgcn_s_sleep(1);
+        poll_pause();
     }
     return true;  // the vote's barrier made every thread's LDS writes visible
 }
@@ -2182,6 +2195,10 @@ void sx_launch_sweep(double *T, int rows, size_t ld, int Ns, const int *nact, in
 // thread with a block vote per poll (0)
 static int g_gather_wide = 1;
 void sx_set_gather_wide(int on) { g_gather_wide = on ? 1 : 0; }
+void sx_set_poll_sleep(int k) {
+    const int v = k < 0 ? 1 : k;
+    SX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_poll_sleep), &v, sizeof(int)));
+}
 static int g_record_replicas = 1;
 void sx_set_record_replicas(int n) { g_record_replicas = n < 1 ? 1 : n > SX_GREP ? SX_GREP : n; }
 

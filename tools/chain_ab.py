@@ -48,8 +48,9 @@ def main():
         lib.simplex_set_sweep_stages(d)
 
     setter = {"gather_wide": lib.simplex_set_gather_wide, "ld_pad": lib.simplex_set_ld_pad,
-              "replicas": lib.simplex_set_record_replicas, "sweep": set_sweep}[name]
-    reset = {"gather_wide": 1, "ld_pad": 0, "replicas": 1, "sweep": "0:0"}[name]
+              "replicas": lib.simplex_set_record_replicas, "sweep": set_sweep,
+              "sleep": lib.simplex_set_poll_sleep}[name]
+    reset = {"gather_wide": 1, "ld_pad": 0, "replicas": 1, "sweep": "0:0", "sleep": 1}[name]
     print("stamps (us): ratio compute | ratio argmin+publish | -> selection seen | pass2 + row details |"
           " row compute | obj argmin+publish | -> entering seen | entering history | pivot")
     for r in range(rounds):
