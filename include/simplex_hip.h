@@ -85,6 +85,10 @@ void simplex_set_sweep_stages(int d);
 /* fused batches: pause between two polls of a hand-off, s_sleep 0/1/2/4/8/16 for k = 0..5
  * (default 1; diagnostic) */
 void simplex_set_poll_sleep(int k);
+/* new engines' tableau layout: plain row-major rows (0), the two-region layout when aliasing and
+ * m > 4096 (1, default), or region A forced to hold `mode` slack positions (>= 2,
+ * test hook) */
+void simplex_set_regions(int mode);
 /* extra doubles appended to every tableau row of new engines (rounded up to 16; default 0) */
 void simplex_set_ld_pad(int doubles);
 /* several shards: keep d and U in uncached memory (1) or plain memory (0, default; uncached

@@ -339,6 +339,12 @@ def set_update_waves(w):
     _lib.load().simplex_set_update_waves(float(w))
 
 
+def set_regions(mode):
+    """New engines' tableau layout: 0 plain rows, 1 auto two-region layout (default), >= 2 region A
+    forced to that many slack positions (test hook)."""
+    _lib.load().simplex_set_regions(int(mode))
+
+
 def set_sweep_stages(d):
     """Full-batch sweeps staged through LDS by LDS-DMA, d stages per wave (0: register sweep)."""
     _lib.load().simplex_set_sweep_stages(int(d))

@@ -129,6 +129,21 @@ struct Cols {
     }
 };
 
+// Tableau storage in HBM: two row-major regions.  Region A holds stored
+// columns [0, jB) of every row at stride ldA; region B, starting offB doubles later, holds
+// stored columns [jB, Ns) at stride ldB.  With slack compaction the swept columns
+// [0, 1 + n + nact) lie in region A while nact fits, so the sweep streams dense rows (a row of
+// A is only a little wider than what is swept) instead of a prefix of every full-width row;
+// without a region B (jB = Ns, the default for small m and for callers' tableaux) this is the
+// plain row-major layout.  jB is a multiple of 512, so no 512-column tile straddles the two.
+struct TLay {
+    size_t ldA = 0, ldB = 0, offB = 0;
+    int jB = 0x7fffffff;
+    __host__ __device__ __forceinline__ size_t idx(long long i, int j) const {
+        return j < jB ? (size_t)i * ldA + (size_t)j : offB + (size_t)i * ldB + (size_t)(j - jB);
+    }
+};
+
 // ---- kernel launchers (sx_kernels.hip) ----
 struct SweepCfg {
     int batch;           // pivots per sweep (1..SX_KMAX): register slots of the sweep
@@ -138,36 +153,36 @@ struct SweepCfg {
 
 int sx_enter_blocks(int L);
 void sx_launch_enter(const double *d, int L, TilePart *parts, DevState *st, hipStream_t s);
-void sx_launch_ratio_select(const double *T, int rows, int row0, size_t ld, TilePart *tiles_local, double *colE,
+void sx_launch_ratio_select(const double *T, int rows, int row0, size_t ld, TLay tl, TilePart *tiles_local, double *colE,
                             DevState *st, int *base, bool select, double *slots, size_t slot_stride, Cols c,
                             const Pending &pd, hipStream_t s);
 void sx_launch_select_gathered(const double *slots, size_t slot_stride, int B2, int *base, DevState *st,
                                const Pending &pd, hipStream_t s);
-void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, Cols c, const TilePart *tiles_all, int B2,
+void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, TLay tl, Cols c, const TilePart *tiles_all, int B2,
                           double *prow_out, int *base, DevState *st, const Pending &pd, hipStream_t s);
-void sx_launch_pivot_row(const double *T, int rows, int row0, size_t ld, Cols c, double *d, const double *prow_buf,
+void sx_launch_pivot_row(const double *T, int rows, int row0, size_t ld, TLay tl, Cols c, double *d, const double *prow_buf,
                          size_t prow_stride, const double *colE, DevState *st, const Pending &pd,
                          TilePart *enter_parts, hipStream_t s);
 // nact (device, or null): sweep only the columns [0, s0 + *nact) (slack compaction)
-void sx_launch_sweep(double *T, int rows, size_t ld, int Ns, const int *nact, int s0, const Pending &pd,
+void sx_launch_sweep(double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0, const Pending &pd,
                      const DevState *st, int rev, SweepCfg cfg, hipStream_t s);
 // slack compaction, after a batch's selections and before its sweep: move the slack column
 // of every row that left the basis for the first time into the swept block
 void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, int m, double *T, int rows, int row0,
-                        size_t ld, int s0, const Pending &pd, const DevState *st, hipStream_t s);
+                        size_t ld, TLay tl, int s0, const Pending &pd, const DevState *st, hipStream_t s);
 // fused batch of up to k pivots on one shard (ratio tiles + objective tiles in one resident
 // grid); returns false (nothing launched) when the grid cannot be resident at once
 bool sx_batch_fits(int rows, Cols c, int k);
 // d_save: the objective row as the batch found it (restored by the host after SX_HANG); the
 // basis is written only by a batch that completed
-void sx_launch_batch(const double *T, int rows, size_t ld, Cols c, double *d, double *d_save, int *base,
+void sx_launch_batch(const double *T, int rows, size_t ld, TLay tl, Cols c, double *d, double *d_save, int *base,
                      DevState *st, const Pending &pd, int k, BatchChan *chan, unsigned long long *ga,
                      unsigned long long *gb, unsigned long long *stamps, hipStream_t s);
 size_t sx_batch_granules_a();
 size_t sx_batch_granules_b();
 // the multi-rank fused batch: `grids` co-resident launches of this shape must fit the device
 bool sx_batch_mr_fits(int slots, int nb_local, int k, int grids);
-void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld, Cols c, double *d, double *d_save,
+void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld, TLay tl, Cols c, double *d, double *d_save,
                         int *base, DevState *st, const Pending &pd, int k, int slots, int W, int rank, int tb0, int tb1,
                         BatchChan *chan, const unsigned long long *ga, const unsigned long long *gb,
                         const unsigned long long *gdone, const PeerView &pv, unsigned long long timeout,
@@ -175,17 +190,17 @@ void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld,
 void sx_set_update_waves(float w);  // resident-grid multiple of the sweep (default 1)
 void sx_set_gather_wide(int on);
 void sx_set_record_replicas(int n);  // fused batch (one shard): tile records written in n <= 8 copies
-void sx_set_sweep_stages(int d);
-void sx_set_poll_sleep(int k);  // hand-off polls pause s_sleep 0/1/2/4/8/16 for k = 0..5 (default 1)     // LDS-staged sweep with d stages per wave (0: register sweep)
+void sx_set_sweep_stages(int d);    // LDS-staged sweep with d stages per wave (0: register sweep)
+void sx_set_poll_sleep(int k);      // hand-off polls pause s_sleep 0/1/2/4/8/16 for k = 0..5 (default 1)
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s);
 void sx_launch_l2_writeback(hipStream_t s);  // every XCD's L2 writes back its dirty lines
 
 void sx_launch_coef(const double *d, const int *base, int row0, int rows, double *coef, hipStream_t s);
-void sx_launch_gemv_partials(const double *T, int rows, size_t ld, int Ns, const double *coef, double *partials,
+void sx_launch_gemv_partials(const double *T, int rows, TLay tl, int Ns, const double *coef, double *partials,
                              hipStream_t s);
 void sx_launch_gemv_apply(double *d, Cols c, const double *partials, int nblk, hipStream_t s);
 
-void sx_launch_build_rows(double *T, int rows, int row0, size_t ld, int n, int m, int Ns, const double *A_local,
+void sx_launch_build_rows(double *T, int rows, int row0, TLay tl, int n, int m, int Ns, const double *A_local,
                           const double *b_full, hipStream_t s);
 void sx_launch_init_vectors(double *d, int N1, int n, int m, int *base, hipStream_t s);
 void sx_launch_phase2_costs(double *d, int n, int m, const double *c, hipStream_t s);

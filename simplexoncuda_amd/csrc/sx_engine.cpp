@@ -64,6 +64,8 @@ struct Config {
     int exchange_mode = 0;   // 0 auto, 1 tile allgather + row allreduce, 2 row-gather
     int alias = 1;           // store phase-1 artificial columns as their slack columns
     int compact = 1;         // sweep only the slack columns pivots have touched (when exact)
+    int regions = 1;         // two-region tableau layout (TLay): 0 off, 1 auto (aliasing, m > 4096),
+                             // >= 2: region A holds that many slack positions (test hook)
     int fused = -1;          // whole batches in one resident launch: -1 auto (one shard), 0 off
     int p2p = -1;            // several shards: fused batches exchanging over peer memory: -1 auto, 0 off, 1 force
     bool p2p_ready = false;  // RCCL ranks: the peer-memory path passed the start-up self-check
@@ -228,7 +230,8 @@ class Engine {
     bool alias = false;    // phase-1 artificial columns stored as their slack columns (sx_common.hpp Cols)
     bool compact = false;  // untouched slack columns kept past the swept block (sx_common.hpp Cols)
     int Ns1 = 0;           // stored columns in phase 1
-    size_t ld = 0;         // row stride in doubles
+    size_t ld = 0;         // full stored row width in doubles (U's row stride; T's without region B)
+    TLay tl;               // T's storage regions (sx_common.hpp)
     int rpr = 0;           // rows per rank (multiple of 512)
     int slots = 0;         // argmin tiles / GEMV blocks per rank
     int device = 0;
@@ -275,6 +278,23 @@ class Engine {
         if (rpr == 0) rpr = SX_TILE;
         slots = rpr / SX_TILE;
         if ((long long)W * slots > SX_TILE) SX_FATAL("too many constraint tiles for the exact argmin tree");
+        // Storage regions (sx_common.hpp TLay): with aliasing -- the precondition
+        // of slack compaction -- region A holds the structural columns and the first capA stored
+        // slack positions, region B the other slack positions, so the swept prefix of a row is
+        // most of a row of A (dense streaming: 32768 x 9216 swept 5.7 TB/s with dense rows, 5.3
+        // with rows 4.4x wider than the swept part, profiles/r02_sweep_row_stride.txt)
+        tl.ldA = ld;
+        tl.jB = Ns1;
+        if (alias && g_cfg.regions) {
+            const int capA = g_cfg.regions >= 2 ? g_cfg.regions : std::max(4096, (m + 7) / 8);
+            const int jB = (int)round_up((size_t)(1 + n + capA), SX_TILE);
+            if (jB < Ns1) {
+                tl.jB = jB;
+                tl.ldA = (size_t)jB + (size_t)g_cfg.ld_pad;
+                tl.ldB = round_up((size_t)(Ns1 - jB), 16) + (size_t)g_cfg.ld_pad;
+                tl.offB = (size_t)rpr * tl.ldA;  // every shard allocates rpr rows (peers index alike)
+            }
+        }
         // one allgather of (tile winner, row) beats two collectives while the rows are small
         const double slot_bytes = 8.0 * (double)slots * (double)slot_stride;
         rowgather = xchg && (g_cfg.exchange_mode == 2 || (g_cfg.exchange_mode == 0 && slot_bytes <= 1048576.0));
@@ -453,9 +473,14 @@ class Engine {
         (void)hipStreamDestroy(s);
     }
 
+    // doubles of a shard's tableau allocation
+    size_t t_doubles(size_t rows_alloc) const {
+        return tl.jB < Ns1 ? tl.offB + (size_t)rpr * tl.ldB : rows_alloc * ld;
+    }
+
     void alloc_shard(Shard &x) {
         const size_t rows_alloc = x.rows > 0 ? (size_t)x.rows : 1;
-        x.T = dalloc<double>(rows_alloc * ld);
+        x.T = dalloc<double>(t_doubles(rows_alloc));
         // d and U: plain device memory.  Other ranks write them over xGMI (system-scope stores)
         // inside the multi-rank batch; this rank reads them only in later kernels, after the
         // batch has seen every rank's done granule, across a kernel boundary.  Allocating them
@@ -532,7 +557,7 @@ class Engine {
         x.tiles_local = dalloc<TilePart>(slots);
         if (xchg) x.tiles_all = dalloc<TilePart>((size_t)W * slots);
         x.st = dalloc<DevState>(1);
-        SX_HIP(hipMemsetAsync(x.T, 0, rows_alloc * ld * sizeof(double), s));
+        SX_HIP(hipMemsetAsync(x.T, 0, t_doubles(rows_alloc) * sizeof(double), s));
         SX_HIP(hipMemsetAsync(x.d, 0, round_up((size_t)N1, 16) * sizeof(double), s));
         SX_HIP(hipMemsetAsync(x.prow, 0, ld * sizeof(double), s));
         // padding tile entries must read (DBL_MAX, -1, not eligible)
@@ -574,7 +599,7 @@ class Engine {
                 SX_HIP(hipMemcpy2DAsync(A_local, sizeof(double) * x.rows, P->constraintsMatrix + x.row0,
                                         sizeof(double) * m, sizeof(double) * x.rows, n, hipMemcpyHostToDevice, s));
             }
-            sx_launch_build_rows(x.T, x.rows, x.row0, ld, n, m, Ns1, A_local, b_dev, s);
+            sx_launch_build_rows(x.T, x.rows, x.row0, tl, n, m, Ns1, A_local, b_dev, s);
             sx_launch_init_vectors(x.d, N1, n, m, x.base, s);
             SX_HIP(hipStreamSynchronize(s));
             if (A_local) (void)hipFree(A_local);
@@ -600,8 +625,8 @@ class Engine {
         if (!c_dev) c_dev = dalloc<double>(n);
         sx_launch_gen_vector(sd[1], 0, n, lo, hi, c_dev, s);
         for (auto &x : sh) {
-            sx_launch_gen_rows(sd[2], n, m, x.row0, x.rows, lo, hi, x.T, ld, nullptr, s);
-            sx_launch_build_rows(x.T, x.rows, x.row0, ld, n, m, Ns1, nullptr, b_dev, s);
+            sx_launch_gen_rows(sd[2], n, m, x.row0, x.rows, lo, hi, x.T, tl.ldA, nullptr, s);  // (region A)
+            sx_launch_build_rows(x.T, x.rows, x.row0, tl, n, m, Ns1, nullptr, b_dev, s);
             sx_launch_init_vectors(x.d, N1, n, m, x.base, s);
         }
         SX_HIP(hipStreamSynchronize(s));
@@ -666,7 +691,7 @@ class Engine {
             if (xchg && !x.gemv_all) x.gemv_all = dalloc<double>((size_t)W * slots * Ns1);
             SX_HIP(hipMemsetAsync(x.gemv_local, 0, part * sizeof(double), s));
             sx_launch_coef(x.d, x.base, x.row0, x.rows, x.coef, s);
-            sx_launch_gemv_partials(x.T, x.rows, ld, c.Ns, x.coef, x.gemv_local, s);
+            sx_launch_gemv_partials(x.T, x.rows, tl, c.Ns, x.coef, x.gemv_local, s);
         }
         if (xchg) allgather_doubles(&Shard::gemv_local, &Shard::gemv_all, part);
         const int nblk = (m + SX_TILE - 1) / SX_TILE;
@@ -774,7 +799,7 @@ class Engine {
     // row, the objective row and the next entering variable.  The tableau is not touched.
     void enqueue_pivot() {
         for (auto &x : sh)
-            sx_launch_ratio_select(x.T, x.rows, x.row0, ld, x.tiles_local, x.colE, x.st, x.base, !xchg,
+            sx_launch_ratio_select(x.T, x.rows, x.row0, ld, tl, x.tiles_local, x.colE, x.st, x.base, !xchg,
                                    rowgather ? x.slot_send : nullptr, slot_stride, cols(N, x), pending(x), s);
         if (rowgather) {
             allgather_slots();
@@ -782,13 +807,13 @@ class Engine {
         } else if (xchg) {
             allgather_tiles();
             for (auto &x : sh)
-                sx_launch_select_row(x.T, x.rows, x.row0, ld, cols(N, x), x.tiles_all, W * slots, x.prow_send, x.base, x.st,
+                sx_launch_select_row(x.T, x.rows, x.row0, ld, tl, cols(N, x), x.tiles_all, W * slots, x.prow_send, x.base, x.st,
                                      pending(x), s);
             allreduce_prow();
         }
         for (auto &x : sh) {
             const double *pb = rowgather ? x.slot_all : (xchg ? x.prow : nullptr);
-            sx_launch_pivot_row(x.T, x.rows, x.row0, ld, cols(N, x), x.d, pb, rowgather ? slot_stride : 0, x.colE, x.st,
+            sx_launch_pivot_row(x.T, x.rows, x.row0, ld, tl, cols(N, x), x.d, pb, rowgather ? slot_stride : 0, x.colE, x.st,
                                 pending(x), x.enter_parts, s);
         }
         ++q_host;
@@ -811,7 +836,7 @@ class Engine {
             for (auto &x : sh) SX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&x.chan->abort_w), 1u, 1, s));
         if (!xchg) {
             Shard &x = sh[0];
-            sx_launch_batch(x.T, x.rows, ld, cols(N, x), x.d, x.d_save, x.base, x.st, pending(x), k, x.chan, x.ga, x.gb,
+            sx_launch_batch(x.T, x.rows, ld, tl, cols(N, x), x.d, x.d_save, x.base, x.st, pending(x), k, x.chan, x.ga, x.gb,
                             stamps, s);
         } else {
             // every rank's batch runs at once (virtual shards: one stream each, forked from and
@@ -827,7 +852,7 @@ class Engine {
                     SX_HIP(hipStreamWaitEvent(xs, ev_fork, 0));
                 }
                 const int tb0 = (int)((long long)x.rank * NBg / W), tb1 = (int)((long long)(x.rank + 1) * NBg / W);
-                sx_launch_batch_mr(x.T, x.rows, x.row0, rpr, ld, cols(N, x), x.d, x.d_save, x.base, x.st, pending(x), k,
+                sx_launch_batch_mr(x.T, x.rows, x.row0, rpr, ld, tl, cols(N, x), x.d, x.d_save, x.base, x.st, pending(x), k,
                                    slots, W,
                                    x.rank, tb0, tb1, x.chan, x.ga, x.gb, x.gdone, pv, timeout, xs);
                 if (!rccl) SX_HIP(hipEventRecord(ev_join[i], xs));
@@ -848,11 +873,11 @@ class Engine {
         // sweeps alone
         if (compact)
             for (auto &x : sh)
-                sx_launch_activate(x.perm, x.iperm, x.act, x.nact, m, x.T, x.rows, x.row0, ld, 1 + n, pending(x), x.st,
+                sx_launch_activate(x.perm, x.iperm, x.act, x.nact, m, x.T, x.rows, x.row0, ld, tl, 1 + n, pending(x), x.st,
                                    s);
         if (ev0) SX_HIP(hipEventRecord(ev0, s));
         for (auto &x : sh)
-            sx_launch_sweep(x.T, x.rows, ld, cols(N).Ns, compact ? x.nact : nullptr, 1 + n, pending(x), x.st, rev, cfg,
+            sx_launch_sweep(x.T, x.rows, ld, tl, cols(N).Ns, compact ? x.nact : nullptr, 1 + n, pending(x), x.st, rev, cfg,
                             s);
         if (ev1) SX_HIP(hipEventRecord(ev1, s));
         ++sweeps;
@@ -1007,7 +1032,7 @@ class Engine {
     // RHS column of all rows (for the solution, getSolution twoPhaseMethod.cu:116-128)
     void read_rhs(std::vector<double> &out) {
         out.assign(m, 0.0);
-        for (auto &x : sh) sx_launch_gather_rhs(x.T, x.rows, ld, x.rhs_local, s);
+        for (auto &x : sh) sx_launch_gather_rhs(x.T, x.rows, tl.ldA, x.rhs_local, s);  // (column 0: region A)
         if (xchg) {
             allgather_doubles(&Shard::rhs_local, &Shard::rhs_all, rpr);
             SX_HIP(hipMemcpyAsync(out.data(), sh[0].rhs_all, sizeof(double) * m, hipMemcpyDeviceToHost, s));
@@ -1032,8 +1057,12 @@ class Engine {
         for (auto &x : sh) {
             if (x.rows <= 0) continue;
             tmp.assign((size_t)x.rows * c.Ns, 0.0);
-            SX_HIP(hipMemcpy2DAsync(tmp.data(), c.Ns * sizeof(double), x.T, ld * sizeof(double), c.Ns * sizeof(double),
-                                    x.rows, hipMemcpyDeviceToHost, s));
+            const int wa = std::min(c.Ns, tl.jB);  // region A's columns, then region B's
+            SX_HIP(hipMemcpy2DAsync(tmp.data(), c.Ns * sizeof(double), x.T, tl.ldA * sizeof(double),
+                                    wa * sizeof(double), x.rows, hipMemcpyDeviceToHost, s));
+            if (wa < c.Ns)
+                SX_HIP(hipMemcpy2DAsync(tmp.data() + wa, c.Ns * sizeof(double), x.T + tl.offB, tl.ldB * sizeof(double),
+                                        (c.Ns - wa) * sizeof(double), x.rows, hipMemcpyDeviceToHost, s));
             SX_HIP(hipStreamSynchronize(s));
             for (int i = 0; i < x.rows; ++i) {
                 double *dst = T_host + (size_t)((local_rows ? 0 : x.row0) + i) * ld_host;
@@ -1055,10 +1084,15 @@ class Engine {
         set_compact(false);  // a caller's tableau: any column may be touched
         const Cols c = cols(width);
         for (auto &x : sh) {
-            if (x.rows > 0)
-                SX_HIP(hipMemcpy2DAsync(x.T, ld * sizeof(double), T_host + (size_t)(local_rows ? 0 : x.row0) * ld_host,
-                                        ld_host * sizeof(double), c.Ns * sizeof(double), x.rows,
-                                        hipMemcpyHostToDevice, s));
+            if (x.rows > 0) {
+                const double *src = T_host + (size_t)(local_rows ? 0 : x.row0) * ld_host;
+                const int wa = std::min(c.Ns, tl.jB);  // region A's columns, then region B's
+                SX_HIP(hipMemcpy2DAsync(x.T, tl.ldA * sizeof(double), src, ld_host * sizeof(double),
+                                        wa * sizeof(double), x.rows, hipMemcpyHostToDevice, s));
+                if (wa < c.Ns)
+                    SX_HIP(hipMemcpy2DAsync(x.T + tl.offB, tl.ldB * sizeof(double), src + wa, ld_host * sizeof(double),
+                                            (c.Ns - wa) * sizeof(double), x.rows, hipMemcpyHostToDevice, s));
+            }
             if (d_host) SX_HIP(hipMemcpyAsync(x.d, d_host, sizeof(double) * width, hipMemcpyHostToDevice, s));
             if (base_host) SX_HIP(hipMemcpyAsync(x.base, base_host, sizeof(int) * m, hipMemcpyHostToDevice, s));
         }
@@ -1238,6 +1272,7 @@ void simplex_set_device(int device) {
 void simplex_set_virtual_ranks(int world) { g_cfg.virtual_ranks = world > 1 ? world : 1; }
 void simplex_set_force_exchange(int on) { g_cfg.force_exchange = on ? 1 : 0; }
 void simplex_set_alias(int on) { g_cfg.alias = on ? 1 : 0; }
+void simplex_set_regions(int mode) { g_cfg.regions = mode < 0 ? 1 : mode; }
 void simplex_set_compact(int on) { g_cfg.compact = on ? 1 : 0; }
 void simplex_set_fused(int mode) { g_cfg.fused = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_p2p(int mode) { g_cfg.p2p = mode < 0 ? -1 : (mode ? 1 : 0); }
@@ -1695,19 +1730,22 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     pd.PM = PM;
     pd.batch = B;
     pd.q = pivots;
+    TLay btl;  // one region: rows of ld doubles
+    btl.ldA = ld;
+    btl.jB = cols;
     SweepCfg cfg;
     cfg.batch = pivots;
     cfg.rows_per_block = g_cfg.update_rows > 0 ? std::min(g_cfg.update_rows, 4) : (pivots > 16 ? 4 : 2);
     cfg.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : 1;  // (as sweep_cfg: write-through at every size)
     long long sweeps = 0;
     for (int w = 0; w < warmup; ++w, ++sweeps)
-        sx_launch_sweep(T, rows, ld, cols, nullptr, 0, pd, st, (int)(sweeps & 1), cfg, s);
+        sx_launch_sweep(T, rows, ld, btl, cols, nullptr, 0, pd, st, (int)(sweeps & 1), cfg, s);
     hipEvent_t e0, e1;
     SX_HIP(hipEventCreate(&e0));
     SX_HIP(hipEventCreate(&e1));
     SX_HIP(hipEventRecord(e0, s));
     for (int it = 0; it < iters; ++it, ++sweeps)
-        sx_launch_sweep(T, rows, ld, cols, nullptr, 0, pd, st, (int)(sweeps & 1), cfg, s);
+        sx_launch_sweep(T, rows, ld, btl, cols, nullptr, 0, pd, st, (int)(sweeps & 1), cfg, s);
     SX_HIP(hipEventRecord(e1, s));
     SX_HIP(hipEventSynchronize(e1));
     float ms = 0.f;

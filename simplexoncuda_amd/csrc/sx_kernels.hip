@@ -255,12 +255,12 @@ __device__ __forceinline__ unsigned stage_row(const double *__restrict__ F, cons
 
 // current values of row rl, columns [0, Ns), written to out (stride over the block; Ns
 // columns in pairs j, j + blockDim)
-__device__ __forceinline__ void cur_row(const double *__restrict__ src, int Ns, int q, unsigned bits,
+__device__ __forceinline__ void cur_row(const double *__restrict__ T, TLay tl, long long rl, int Ns, int q, unsigned bits,
                                         const double *sf, const double *sp, const double *__restrict__ U, size_t ld,
                                         double *out, int first, int stride) {
     for (int j = first; j < Ns; j += 2 * stride) {
         const int jb = j + stride < Ns ? j + stride : j;
-        double xa = src[j], xb = src[jb];
+        double xa = T[tl.idx(rl, j)], xb = T[tl.idx(rl, jb)];
         cur_pair(xa, xb, j, jb, q, bits, sf, sp, U, ld);
         out[j] = xa;
         if (j + stride < Ns) out[jb] = xb;
@@ -280,7 +280,7 @@ __device__ __forceinline__ void cur_row(const double *__restrict__ src, int Ns, 
 // (minElement(knownTerms, rowPivot), solver.cu:104), declares UNBOUNDED (:96-102) or records
 // the pivot: base[r] = e (:105).  With several shards the tile winners are allgathered
 // first and k_select_row / k_select_gathered do that step.
-__global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__ T, int rows, int row0, size_t ld,
+__global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__ T, int rows, int row0, size_t ld, TLay tl,
                                                       TilePart *tiles_local, double *colE, DevState *st, int *base,
                                                       int select, double *slots, size_t slot_stride, Cols c,
                                                       const double *__restrict__ F, const double *__restrict__ U,
@@ -322,9 +322,8 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
     double b = 0.0, a = 0.0;
     unsigned bits = 0u;
     if (li < rows) {
-        const double *row = T + (size_t)li * ld;
-        b = row[0];
-        a = row[ce];
+        b = T[tl.idx(li, 0)];
+        a = T[tl.idx(li, ce)];
         if (q > 0) bits = pend_bits(PM, li, B, mask);
     }
     __syncthreads();
@@ -383,7 +382,7 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
         if (s_ri < 0) return;
         const int wl = s_ri - row0;
         const unsigned wbits = stage_row(F, recs, PM, wl, B, q, s_f, s_p);
-        cur_row(T + (size_t)wl * ld, c.Ns, q, wbits, s_f, s_p, U, ld, slot + 2, threadIdx.x, SX_TILE);
+        cur_row(T, tl, wl, c.Ns, q, wbits, s_f, s_p, U, ld, slot + 2, threadIdx.x, SX_TILE);
         return;
     }
     __shared__ int s_last;
@@ -436,7 +435,7 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
 // current pivot row (the reference's copyColumn, solver.cu:24-32, is a contiguous row
 // here).  Only the owner contributes the row; the others contribute -0.0, the exact
 // additive identity, so the sum-allreduce reproduces the owner's row bit for bit.
-__global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T, int rows, int row0, size_t ld,
+__global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T, int rows, int row0, size_t ld, TLay tl,
                                                     int Ns, const TilePart *__restrict__ tiles_all, int B2,
                                                     double *prow_out, int *base, DevState *st,
                                                     const double *__restrict__ F, const double *__restrict__ U,
@@ -468,7 +467,7 @@ __global__ __launch_bounds__(512) void k_select_row(const double *__restrict__ T
     if (own) {
         __shared__ double s_f[SX_KMAX], s_p[SX_KMAX];
         const unsigned bits = stage_row(F, recs, PM, rl, B, q, s_f, s_p);
-        cur_row(T + (size_t)rl * ld, Ns, q, bits, s_f, s_p, U, ld, prow_out, blockIdx.x * blockDim.x + threadIdx.x,
+        cur_row(T, tl, rl, Ns, q, bits, s_f, s_p, U, ld, prow_out, blockIdx.x * blockDim.x + threadIdx.x,
                 gridDim.x * blockDim.x);
     } else {
         for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < Ns; j += gridDim.x * blockDim.x) prow_out[j] = -0.0;
@@ -540,7 +539,7 @@ __global__ __launch_bounds__(512) void k_select_gathered(const double *__restric
 // Blocks [0, B1) are the objective-row tiles (512 logical columns each, 2 per thread);
 // the rest compute the factor column.  Writes to recs[q] / PM[r] race with nothing: readers
 // in this launch only look at slots < q.
-__global__ __launch_bounds__(256) void k_pivot_row(const double *__restrict__ T, int rows, int row0, size_t ld, Cols c,
+__global__ __launch_bounds__(256) void k_pivot_row(const double *__restrict__ T, int rows, int row0, size_t ld, TLay tl, Cols c,
                                                    double *__restrict__ d, const double *__restrict__ prow_buf,
                                                    size_t prow_stride, const double *__restrict__ colE, DevState *st,
                                                    double *U, double *F, PivRec *recs, unsigned long long *PM,
@@ -550,7 +549,7 @@ __global__ __launch_bounds__(256) void k_pivot_row(const double *__restrict__ T,
     const int rl = r - row0;
     const double *prow =
         prow_buf ? (prow_stride ? prow_buf + (size_t)(r / SX_TILE) * prow_stride + 2 : prow_buf) : nullptr;
-    const double *trow = T + (size_t)(prow ? 0 : rl) * ld;
+    const long long trl = prow ? 0 : rl;  // (the stored row is read only when the row is local)
     __shared__ double s_f[SX_KMAX], s_p[SX_KMAX];
     const unsigned bits = prow ? 0u : stage_row(F, recs, PM, rl, B, q, s_f, s_p);
     // current values of the pivot row at the entering column (the pivot), column 0 and this
@@ -560,7 +559,7 @@ __global__ __launch_bounds__(256) void k_pivot_row(const double *__restrict__ T,
     const int col[4] = {c.map(1 + e), 0, c.map(1 + (ia < L ? ia : 0)), c.map(1 + (ib < L ? ib : 0))};
     double x[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) x[k] = prow ? prow[col[k]] : trow[col[k]];
+    for (int k = 0; k < 4; ++k) x[k] = prow ? prow[col[k]] : T[tl.idx(trl, col[k])];
     if (!prow) cur_cols<4>(x, col, q, bits, s_f, s_p, U, ld);
     const double p = x[0], u0 = x[1], ua = x[2], ub = x[3];
     if ((int)blockIdx.x >= B1) {
@@ -867,7 +866,7 @@ __host__ __device__ __forceinline__ size_t sx_ga_size() { return (size_t)SX_TILE
 __host__ __device__ __forceinline__ size_t sx_gb_size() { return (size_t)SX_TILE * SX_GB_STRIDE; }
 __device__ __forceinline__ int rec2_b(int k) { return (k >> 1) * SX_GB_STRIDE + (k & 1); }
 
-__global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int rows, size_t ld, Cols c,
+__global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int rows, size_t ld, TLay tl, Cols c,
                                                double *__restrict__ d, double *__restrict__ d_save, int *base,
                                                DevState *st, double *U, double *F, PivRec *recs,
                                                unsigned long long *PM, unsigned B, int K, int NA, int NB,
@@ -917,13 +916,13 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
         const int ia = tb * SX_TILE + t;
         const bool liveB = !isA && ia < L;
         const int mj = c.map(1 + (liveB ? ia : 0));
-        double b = liveA ? T[(size_t)li * ld] : 0.0;  // current RHS of the row
+        double b = liveA ? T[tl.idx(li, 0)] : 0.0;  // current RHS of the row
         unsigned bits = 0u;                            // slots where this row left the basis
         double dj = liveB ? d[1 + ia] : 0.0;
         double d0 = (!isA && tb == 0 && t == 0) ? d[0] : 0.0;
         // the entering column's stored value of this row: loaded as soon as the entering
         // variable is known, so the load overlaps the wait for its pending history
-        double a_pre = liveA ? T[(size_t)li * ld + c.map(1 + (e >= 0 ? e : 0))] : 0.0;
+        double a_pre = liveA ? T[tl.idx(li, c.map(1 + (e >= 0 ? e : 0)))] : 0.0;
         for (int q = 0; q < K; ++q) {
             const unsigned tag = make_tag(B, q);
             // ---- does the phase end here?  (the same decision in every block)
@@ -1029,7 +1028,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                 break;
             }
             // the objective blocks' pivot-row load does not wait for the winner's details
-            double u = liveB ? T[(size_t)r * ld + mj] : 0.0;
+            double u = liveB ? T[tl.idx(r, mj)] : 0.0;
             const int wt = r / SX_TILE;
             if (!gather_tagged(gam + (size_t)wt * SX_GA_STRIDE + 4, 4 + 2 * q, [](int k) { return k; }, tag, s_g,
                                &ch->abort_w, &s_ok)) {
@@ -1150,7 +1149,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
             __syncthreads();
             e = s_win;
             dmin = s_wv;
-            if (liveA) a_pre = T[(size_t)li * ld + c.map(1 + (e >= 0 ? e : 0))];
+            if (liveA) a_pre = T[tl.idx(li, c.map(1 + (e >= 0 ? e : 0)))];
             if (isA && blockIdx.x == 0) SX_STAMP(5);
             // the ratio blocks need the pending pivot rows' entries in the new entering column
             if (isA && q + 1 < K && e >= 0 && cmp_eps(dmin, 0.0) < 0) {
@@ -1228,7 +1227,7 @@ __device__ __forceinline__ double ld_sys(const double *p) {
     return __longlong_as_double((long long)ld_sys(reinterpret_cast<const u64 *>(p)));
 }
 
-__global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, int rows, int row0, int rpr, size_t ld,
+__global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, int rows, int row0, int rpr, size_t ld, TLay tl,
                                                   Cols c, double *__restrict__ d, double *__restrict__ d_save, int *base,
                                                   DevState *st, double *U, double *F, PivRec *recs,
                                                   unsigned long long *PM, unsigned B, int K,
@@ -1273,11 +1272,11 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
         // SX_HANG): every rank writes d slices only at the end of the batch, after hand-offs
         // that need every block of every rank, so this copy is complete before any change
         for (int j = blockIdx.x * blockDim.x + t; j < c.N; j += gridDim.x * blockDim.x) d_save[j] = d[j];
-        double b = liveA ? T[(size_t)li * ld] : 0.0;
+        double b = liveA ? T[tl.idx(li, 0)] : 0.0;
         unsigned bits = 0u;
         // the entering column's stored value of this row: loaded as soon as the entering
         // variable is known, so the load overlaps the wait for its pending history
-        double a_pre = liveA ? T[(size_t)li * ld + c.map(1 + (e >= 0 ? e : 0))] : 0.0;
+        double a_pre = liveA ? T[tl.idx(li, c.map(1 + (e >= 0 ? e : 0)))] : 0.0;
         for (int q = 0; q < K; ++q) {
             const unsigned tag = make_tag(B, q);
             if (cap >= 0 && piv0 + q >= cap) {
@@ -1382,7 +1381,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
             const int owner = r / rpr;
             double u = 0.0;
             if (liveB) {
-                const double *src = pv.T[owner] + (size_t)(r - owner * rpr) * ld + mj;
+                const double *src = pv.T[owner] + tl.idx(r - owner * rpr, mj);  // (every rank: the same layout)
                 u = owner == rank ? *src : ld_sys(src);
             }
             if (!gather_tagged<decltype(ident), true>(ga + (size_t)(r / SX_TILE) * SX_GA_STRIDE + 4, 4 + 2 * q, ident,
@@ -1501,7 +1500,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
             __syncthreads();
             e = s_win;
             dmin = s_wv;
-            if (liveA) a_pre = T[(size_t)li * ld + c.map(1 + (e >= 0 ? e : 0))];
+            if (liveA) a_pre = T[tl.idx(li, c.map(1 + (e >= 0 ? e : 0)))];
             if (isA && q + 1 < K && e >= 0 && cmp_eps(dmin, 0.0) < 0) {
                 if (!gather_tagged<decltype(ident), true>(gb + (size_t)(e / SX_TILE) * SX_GB_STRIDE + 4, 2 * (q + 1),
                                                           ident, tag, s_g, &ch->abort_w, &s_ok, timeout)) {
@@ -1572,7 +1571,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 template <int KT, int RB, bool SC1>
-__global__ __launch_bounds__(256) void k_sweep(double *__restrict__ T, int rows, size_t ld, int Ns,
+__global__ __launch_bounds__(256) void k_sweep(double *__restrict__ T, int rows, size_t ld, TLay tl, int Ns,
                                                const int *__restrict__ nact, int s0,
                                                const double *__restrict__ F, const double *__restrict__ U,
                                                const PivRec *__restrict__ recs,
@@ -1591,13 +1590,18 @@ __global__ __launch_bounds__(256) void k_sweep(double *__restrict__ T, int rows,
     const int bx = rev ? cb - 1 - tile : tile;
     const int j = (bx * 256 + (int)threadIdx.x) * 2;
     if (j >= Ns) return;  // the thread of an odd last column moves (j, j+1): j+1 < ld is padding
+    // this tile's storage region (jB is a multiple of 512: a tile lies in one region)
+    const bool inB = bx * 512 >= tl.jB;
+    double *const Tr = inB ? T + tl.offB : T;
+    const size_t ldr = inB ? tl.ldB : tl.ldA;
+    const int jr = inB ? j - tl.jB : j;
     const unsigned mask = slot_mask(cnt);
     double2 u[KT];
 #pragma unroll
     for (int s = 0; s < KT; ++s)
         u[s] = s < cnt ? *reinterpret_cast<const double2 *>(U + (size_t)s * ld + j) : make_double2(0.0, 0.0);
     const int ng = (rows + RB - 1) / RB;
-    const int oob = (int)(ld * 8);
+    const int oob = (int)(ldr * 8);
     for (int g = gy; g < ng; g += G) {
         const int i0 = (rev ? ng - 1 - g : g) * RB;
         double2 x[RB];
@@ -1607,8 +1611,8 @@ __global__ __launch_bounds__(256) void k_sweep(double *__restrict__ T, int rows,
         for (int k = 0; k < RB; ++k) {
             const int i = i0 + k < rows ? i0 + k : i0;
             const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(T + (size_t)i * ld, 0, oob, 0x00020000);
-            x[k] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, i0 + k < rows ? j * 8 : oob,
+                __builtin_amdgcn_make_buffer_rsrc(Tr + (size_t)i * ldr, 0, oob, 0x00020000);
+            x[k] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, i0 + k < rows ? jr * 8 : oob,
                                                                                       0, 2));
         }
 #pragma unroll
@@ -1658,8 +1662,8 @@ __global__ __launch_bounds__(256) void k_sweep(double *__restrict__ T, int rows,
                 }
             }
             const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(T + (size_t)i * ld, 0, oob, 0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, j * 8, 0, SC1 ? 16 : 0);
+                __builtin_amdgcn_make_buffer_rsrc(Tr + (size_t)i * ldr, 0, oob, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, jr * 8, 0, SC1 ? 16 : 0);
         }
     }
 }
@@ -1719,7 +1723,7 @@ __device__ __forceinline__ void wait_vm() {
 // counting; every iteration issues exactly RB loads -- past its last group it re-reads that
 // group -- and RB stores, so the counts are exact).  Same operations, same order as k_sweep.
 template <int KT, int RB, bool SC1, int D>
-__global__ __launch_bounds__(256) void k_sweep_lds(double *__restrict__ T, int rows, size_t ld, int Ns,
+__global__ __launch_bounds__(256) void k_sweep_lds(double *__restrict__ T, int rows, size_t ld, TLay tl, int Ns,
                                                    const int *__restrict__ nact, int s0,
                                                    const double *__restrict__ F, const double *__restrict__ U,
                                                    const PivRec *__restrict__ recs,
@@ -1737,6 +1741,11 @@ __global__ __launch_bounds__(256) void k_sweep_lds(double *__restrict__ T, int r
     const int bx = rev ? cb - 1 - tile : tile;
     const int j = (bx * 256 + (int)threadIdx.x) * 2;
     if (j >= Ns) return;  // (whole lanes leave; a wave's DMA runs on the lanes left)
+    // this tile's storage region (jB is a multiple of 512: a tile lies in one region)
+    const bool inB = bx * 512 >= tl.jB;
+    double *const Tr = inB ? T + tl.offB : T;
+    const size_t ldr = inB ? tl.ldB : tl.ldA;
+    const int jr = inB ? j - tl.jB : j;
     const int ng = (rows + RB - 1) / RB;
     const int nmy = gy < ng ? (ng - gy + G - 1) / G : 0;
     if (nmy == 0) return;
@@ -1758,7 +1767,7 @@ __global__ __launch_bounds__(256) void k_sweep_lds(double *__restrict__ T, int r
 #pragma unroll
         for (int k = 0; k < RB; ++k) {
             const int i = i0 + k < rows ? i0 + k : rows - 1;
-            const double *src = T + (size_t)i * ld + j;
+            const double *src = Tr + (size_t)i * ldr + jr;
             unsigned keep;
             asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
                          "s_mov_b32 m0, %0"
@@ -1769,7 +1778,7 @@ __global__ __launch_bounds__(256) void k_sweep_lds(double *__restrict__ T, int r
     };
 #pragma unroll
     for (int it = 0; it < D - 1; ++it) issue(it);
-    const int oob = (int)(ld * 8);
+    const int oob = (int)(ldr * 8);
     for (int it = 0; it < nmy; ++it) {
         issue(it + D - 1);
         // ops issued after stage it's loads: steady state 2 RB (D - 1); the first D - 1
@@ -1798,10 +1807,10 @@ __global__ __launch_bounds__(256) void k_sweep_lds(double *__restrict__ T, int r
             const bool live = i < rows;
             const double2 y = sweep_row<KT>(x[k], u, F, recs, PM, live ? i : i0, B, mask, cnt);
             const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(T + (size_t)(live ? i : i0) * ld, 0, oob, 0x00020000);
+                __builtin_amdgcn_make_buffer_rsrc(Tr + (size_t)(live ? i : i0) * ldr, 0, oob, 0x00020000);
             // (a row past the end: the store goes out of range and is dropped -- one store per
             // row slot always, so the counts above hold)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, live ? j * 8 : oob, 0,
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, live ? jr * 8 : oob, 0,
                                                    SC1 ? 16 : 0);
         }
     }
@@ -1819,8 +1828,8 @@ __global__ __launch_bounds__(256) void k_sweep_lds(double *__restrict__ T, int r
 // shard's rows only) and to perm / iperm / act / nact.  The shards run it alike.
 __global__ __launch_bounds__(256) void k_activate(int *__restrict__ perm, int *__restrict__ iperm,
                                                   unsigned char *__restrict__ act, int *__restrict__ nact_p, int m,
-                                                  double *__restrict__ T, int rows, int row0, size_t ld, int s0,
-                                                  double *__restrict__ U, const PivRec *__restrict__ recs,
+                                                  double *__restrict__ T, int rows, int row0, size_t ld, TLay tl,
+                                                  int s0, double *__restrict__ U, const PivRec *__restrict__ recs,
                                                   const DevState *__restrict__ st, unsigned B) {
     const int cnt = st->batch_tag == B ? st->batch_count : 0;
     if (cnt <= 0) return;
@@ -1909,8 +1918,8 @@ __global__ __launch_bounds__(256) void k_activate(int *__restrict__ perm, int *_
     if (t < nl) {
         const int x = s_pl[t], o = s_ol[t], c = s_cl[t];
         if (o != c) {
-            if (o >= row0 && o < row0 + rows) T[(size_t)(o - row0) * ld + s0 + x] = 0.0;
-            if (c >= row0 && c < row0 + rows) T[(size_t)(c - row0) * ld + s0 + x] = 1.0;
+            if (o >= row0 && o < row0 + rows) T[tl.idx(o - row0, s0 + x)] = 0.0;
+            if (c >= row0 && c < row0 + rows) T[tl.idx(c - row0, s0 + x)] = 1.0;
         }
         iperm[x] = c;
         perm[c] = x;
@@ -1940,14 +1949,15 @@ __global__ void k_coef(const double *d, const int *base, int row0, int rows, dou
     if (i < rows) coef[i] = d[1 + base[row0 + i]];
 }
 
-__global__ __launch_bounds__(256) void k_gemv_partials(const double *__restrict__ T, int rows, size_t ld, int N,
+__global__ __launch_bounds__(256) void k_gemv_partials(const double *__restrict__ T, int rows, TLay tl, int N,
                                                        const double *__restrict__ coef, double *partials) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     const int k = blockIdx.y;
     if (j >= N) return;
     const int i1 = (k + 1) * SX_TILE < rows ? (k + 1) * SX_TILE : rows;
     double s = 0.0;
-    const double *col = T + j;
+    const double *col = T + tl.idx(0, j);  // column j: stride ldA in region A, ldB in region B
+    const size_t ld = j < tl.jB ? tl.ldA : tl.ldB;
     int i = k * SX_TILE;
     for (; i + 4 <= i1; i += 4) {
         const double t0 = col[(size_t)i * ld], t1 = col[(size_t)(i + 1) * ld];
@@ -1991,22 +2001,22 @@ __global__ __launch_bounds__(256) void k_fill_structural(double *T, int rows, si
 
 // RHS, slack/artificial identities, and the b<0 quirk: a row with compare(b_i) < 0 is
 // negated across ALL its entries, slack and artificial included.
-__global__ void k_fill_rows(double *T, int rows, int row0, size_t ld, int n, int m, int Ns, const double *b_full) {
+__global__ void k_fill_rows(double *T, int rows, int row0, TLay tl, int n, int m, int Ns, const double *b_full) {
     const int i = blockIdx.y;
     if (i >= rows) return;
     const int gi = row0 + i;
     const double bi = b_full[gi];
     const bool neg = cmp_eps(bi, 0.0) < 0;
-    double *row = T + (size_t)i * ld;
     for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < Ns; j += gridDim.x * blockDim.x) {
+        double &el = T[tl.idx(i, j)];
         double x;
         if (j == 0)
             x = bi;
         else if (j <= n)
-            x = row[j];
+            x = el;
         else
             x = (j == 1 + n + gi || j == 1 + n + m + gi) ? 1.0 : 0.0;
-        row[j] = neg ? -x : x;
+        el = neg ? -x : x;
     }
 }
 
@@ -2048,14 +2058,14 @@ void sx_launch_enter(const double *d, int L, TilePart *parts, DevState *st, hipS
     k_enter_finish<<<1, SX_TILE, 0, s>>>(parts, g, st);
 }
 
-void sx_launch_ratio_select(const double *T, int rows, int row0, size_t ld, TilePart *tiles_local, double *colE,
+void sx_launch_ratio_select(const double *T, int rows, int row0, size_t ld, TLay tl, TilePart *tiles_local, double *colE,
                             DevState *st, int *base, bool select, double *slots, size_t slot_stride, Cols c,
                             const Pending &pd, hipStream_t s) {
     int g = (rows + SX_TILE - 1) / SX_TILE;
     if (g < 1) g = 1;  // a shard without rows still decides optimality for its own state
     if (select && g > SX_TILE) SX_FATAL("too many ratio tiles for the 512-thread pass 2");
     if (pd.q < 0 || pd.q >= SX_KMAX) SX_FATAL("pending slot out of range");
-    k_ratio_select<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, tiles_local, colE, st, base, select ? 1 : 0, slots,
+    k_ratio_select<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, tl, tiles_local, colE, st, base, select ? 1 : 0, slots,
                                          slot_stride, c, pd.F, pd.U, pd.recs, pd.PM, pd.batch, pd.q);
 }
 
@@ -2065,25 +2075,25 @@ void sx_launch_select_gathered(const double *slots, size_t slot_stride, int B2, 
     k_select_gathered<<<1, SX_TILE, 0, s>>>(slots, slot_stride, B2, base, st, pd.batch, pd.q);
 }
 
-void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, Cols c, const TilePart *tiles_all, int B2,
+void sx_launch_select_row(const double *T, int rows, int row0, size_t ld, TLay tl, Cols c, const TilePart *tiles_all, int B2,
                           double *prow_out, int *base, DevState *st, const Pending &pd, hipStream_t s) {
     if (B2 > SX_TILE) SX_FATAL("too many ratio tiles for the 512-thread pass 2");
     const int N = c.Ns;
     int g = (N + 4 * SX_TILE - 1) / (4 * SX_TILE);
     if (g < 1) g = 1;
     if (g > 64) g = 64;
-    k_select_row<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, N, tiles_all, B2, prow_out, base, st, pd.F, pd.U, pd.recs,
+    k_select_row<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, tl, N, tiles_all, B2, prow_out, base, st, pd.F, pd.U, pd.recs,
                                        pd.PM, pd.batch, pd.q);
 }
 
-void sx_launch_pivot_row(const double *T, int rows, int row0, size_t ld, Cols c, double *d, const double *prow_buf,
+void sx_launch_pivot_row(const double *T, int rows, int row0, size_t ld, TLay tl, Cols c, double *d, const double *prow_buf,
                          size_t prow_stride, const double *colE, DevState *st, const Pending &pd,
                          TilePart *enter_parts, hipStream_t s) {
     const int B1 = (c.N - 1 + SX_TILE - 1) / SX_TILE;
     if (B1 > 256) SX_FATAL("entering vector too long for the pivot-row kernel's pass 2");
     if (B1 < 1) SX_FATAL("empty objective row");
     const int fb = rows > 0 ? (rows + 255) / 256 : 0;
-    k_pivot_row<<<B1 + fb, 256, 0, s>>>(T, rows, row0, ld, c, d, prow_buf, prow_stride, colE, st, pd.U, pd.F, pd.recs,
+    k_pivot_row<<<B1 + fb, 256, 0, s>>>(T, rows, row0, ld, tl, c, d, prow_buf, prow_stride, colE, st, pd.U, pd.F, pd.recs,
                                         pd.PM, enter_parts, pd.batch, pd.q, B1);
 }
 
@@ -2116,30 +2126,30 @@ static int row_slots(int capacity, int col_blocks, int rows, int rb) {
 }
 
 template <int KT, int RB, bool SC1>
-static void launch_sweep_t(double *T, int rows, size_t ld, int Ns, const int *nact, int s0, const Pending &pd,
+static void launch_sweep_t(double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0, const Pending &pd,
                            const DevState *st, int rev, hipStream_t s) {
     const int cb = (Ns + 511) / 512;
     dim3 grid(cb, row_slots(sweep_capacity(k_sweep<KT, RB, SC1>), cb, rows, RB));
-    k_sweep<KT, RB, SC1><<<grid, 256, 0, s>>>(T, rows, ld, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st, pd.batch,
+    k_sweep<KT, RB, SC1><<<grid, 256, 0, s>>>(T, rows, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st, pd.batch,
                                               rev);
 }
 
 template <int KT>
-static void launch_sweep_k(int rb, bool sc1, double *T, int rows, size_t ld, int Ns, const int *nact, int s0,
+static void launch_sweep_k(int rb, bool sc1, double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0,
                            const Pending &pd, const DevState *st, int rev, hipStream_t s) {
     switch (rb) {
-    case 1: sc1 ? launch_sweep_t<KT, 1, true>(T, rows, ld, Ns, nact, s0, pd, st, rev, s)
-                : launch_sweep_t<KT, 1, false>(T, rows, ld, Ns, nact, s0, pd, st, rev, s); break;
-    case 2: sc1 ? launch_sweep_t<KT, 2, true>(T, rows, ld, Ns, nact, s0, pd, st, rev, s)
-                : launch_sweep_t<KT, 2, false>(T, rows, ld, Ns, nact, s0, pd, st, rev, s); break;
-    default: sc1 ? launch_sweep_t<KT, 4, true>(T, rows, ld, Ns, nact, s0, pd, st, rev, s)
-                 : launch_sweep_t<KT, 4, false>(T, rows, ld, Ns, nact, s0, pd, st, rev, s); break;
+    case 1: sc1 ? launch_sweep_t<KT, 1, true>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s)
+                : launch_sweep_t<KT, 1, false>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s); break;
+    case 2: sc1 ? launch_sweep_t<KT, 2, true>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s)
+                : launch_sweep_t<KT, 2, false>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s); break;
+    default: sc1 ? launch_sweep_t<KT, 4, true>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s)
+                 : launch_sweep_t<KT, 4, false>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s); break;
     }
 }
 
 void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, int m, double *T, int rows, int row0,
-                        size_t ld, int s0, const Pending &pd, const DevState *st, hipStream_t s) {
-    k_activate<<<1, 256, 0, s>>>(perm, iperm, act, nact, m, T, rows, row0, ld, s0, pd.U, pd.recs, st, pd.batch);
+                        size_t ld, TLay tl, int s0, const Pending &pd, const DevState *st, hipStream_t s) {
+    k_activate<<<1, 256, 0, s>>>(perm, iperm, act, nact, m, T, rows, row0, ld, tl, s0, pd.U, pd.recs, st, pd.batch);
 }
 
 // the LDS-staged sweep (k_sweep_lds): stages per wave, 0 = the register sweep
@@ -2147,19 +2157,19 @@ static int g_sweep_stages = 0;
 void sx_set_sweep_stages(int d) { g_sweep_stages = d < 0 ? 0 : d; }
 
 template <int RB, int D>
-static void launch_sweep_lds_t(double *T, int rows, size_t ld, int Ns, const int *nact, int s0, const Pending &pd,
+static void launch_sweep_lds_t(double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0, const Pending &pd,
                                const DevState *st, int rev, hipStream_t s) {
     const int cb = (Ns + 511) / 512;
     dim3 grid(cb, row_slots(sweep_capacity(k_sweep_lds<SX_KMAX, RB, true, D>), cb, rows, RB));
-    k_sweep_lds<SX_KMAX, RB, true, D><<<grid, 256, 0, s>>>(T, rows, ld, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st,
+    k_sweep_lds<SX_KMAX, RB, true, D><<<grid, 256, 0, s>>>(T, rows, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st,
                                                            pd.batch, rev);
 }
 
-static bool launch_sweep_lds(int rb, int d, double *T, int rows, size_t ld, int Ns, const int *nact, int s0,
+static bool launch_sweep_lds(int rb, int d, double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0,
                              const Pending &pd, const DevState *st, int rev, hipStream_t s) {
 #define SX_LDS_CASE(R, DD)                                                      \
     if (rb == R && d == DD) {                                                   \
-        launch_sweep_lds_t<R, DD>(T, rows, ld, Ns, nact, s0, pd, st, rev, s); \
+        launch_sweep_lds_t<R, DD>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s); \
         return true;                                                            \
     }
     SX_LDS_CASE(4, 2)
@@ -2170,23 +2180,23 @@ static bool launch_sweep_lds(int rb, int d, double *T, int rows, size_t ld, int 
     return false;
 }
 
-void sx_launch_sweep(double *T, int rows, size_t ld, int Ns, const int *nact, int s0, const Pending &pd,
+void sx_launch_sweep(double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0, const Pending &pd,
                      const DevState *st, int rev, SweepCfg cfg, hipStream_t s) {
     if (rows <= 0) return;
     const int k = cfg.batch;  // pivots the sweep may have to apply (register slots)
     if (g_sweep_stages > 0 && k > 16 && k <= SX_KMAX && cfg.sc1 &&
-        launch_sweep_lds(cfg.rows_per_block, g_sweep_stages, T, rows, ld, Ns, nact, s0, pd, st, rev, s))
+        launch_sweep_lds(cfg.rows_per_block, g_sweep_stages, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s))
         return;
     if (k <= 1)
-        launch_sweep_k<1>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, nact, s0, pd, st, rev, s);
+        launch_sweep_k<1>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else if (k <= 4)
-        launch_sweep_k<4>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, nact, s0, pd, st, rev, s);
+        launch_sweep_k<4>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else if (k <= 8)
-        launch_sweep_k<8>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, nact, s0, pd, st, rev, s);
+        launch_sweep_k<8>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else if (k <= 16)
-        launch_sweep_k<16>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, nact, s0, pd, st, rev, s);
+        launch_sweep_k<16>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else if (k <= SX_KMAX)
-        launch_sweep_k<SX_KMAX>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, Ns, nact, s0, pd, st, rev, s);
+        launch_sweep_k<SX_KMAX>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else
         SX_FATAL("batch larger than SX_KMAX");
 }
@@ -2227,12 +2237,12 @@ bool sx_batch_fits(int rows, Cols c, int k) {
     return per_cu[k] > 0 && (long long)(NA + NB) <= (long long)per_cu[k] * cus - 16;
 }
 
-void sx_launch_batch(const double *T, int rows, size_t ld, Cols c, double *d, double *d_save, int *base,
+void sx_launch_batch(const double *T, int rows, size_t ld, TLay tl, Cols c, double *d, double *d_save, int *base,
                      DevState *st, const Pending &pd, int k, BatchChan *chan, unsigned long long *ga,
                      unsigned long long *gb, unsigned long long *stamps, hipStream_t s) {
     if (!sx_batch_fits(rows, c, k)) SX_FATAL("fused batch grid does not fit the device");
     const int NA = (rows + SX_TILE - 1) / SX_TILE, NB = (c.N - 1 + SX_TILE - 1) / SX_TILE;
-    k_batch<<<NA + NB, SX_TILE, batch_lds(k), s>>>(T, rows, ld, c, d, d_save, base, st, pd.U, pd.F, pd.recs, pd.PM,
+    k_batch<<<NA + NB, SX_TILE, batch_lds(k), s>>>(T, rows, ld, tl, c, d, d_save, base, st, pd.U, pd.F, pd.recs, pd.PM,
                                                    pd.batch, k, NA, NB, chan, ga, gb, stamps, g_gather_wide,
                                                    g_record_replicas);
 }
@@ -2254,7 +2264,7 @@ bool sx_batch_mr_fits(int slots, int nb_local, int k, int grids) {
     return per_cu[k] > 0 && (long long)grids * (slots + nb_local) <= (long long)per_cu[k] * cus - 16;
 }
 
-void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld, Cols c, double *d, double *d_save,
+void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld, TLay tl, Cols c, double *d, double *d_save,
                         int *base, DevState *st, const Pending &pd, int k, int slots, int W, int rank, int tb0, int tb1,
                         BatchChan *chan, const unsigned long long *ga, const unsigned long long *gb,
                         const unsigned long long *gdone, const PeerView &pv, unsigned long long timeout,
@@ -2262,7 +2272,7 @@ void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld,
     const int NBg = (c.N - 1 + SX_TILE - 1) / SX_TILE;
     if (W < 1 || W > SX_MAXW || W * slots > SX_TILE || NBg > SX_TILE || NBg < 1 || tb0 < 0 || tb1 > NBg || tb0 > tb1)
         SX_FATAL("multi-rank fused batch: bad shape");
-    k_batch_mr<<<slots + (tb1 - tb0), SX_TILE, batch_lds(k), s>>>(T, rows, row0, rpr, ld, c, d, d_save, base, st, pd.U, pd.F,
+    k_batch_mr<<<slots + (tb1 - tb0), SX_TILE, batch_lds(k), s>>>(T, rows, row0, rpr, ld, tl, c, d, d_save, base, st, pd.U, pd.F,
                                                                   pd.recs, pd.PM, pd.batch, k, slots, W, rank, tb0,
                                                                   tb1, NBg, chan, ga, gb, gdone, pv, timeout,
                                                                   g_gather_wide);
@@ -2286,29 +2296,29 @@ void sx_launch_coef(const double *d, const int *base, int row0, int rows, double
     k_coef<<<(rows + 255) / 256, 256, 0, s>>>(d, base, row0, rows, coef);
 }
 
-void sx_launch_gemv_partials(const double *T, int rows, size_t ld, int N, const double *coef, double *partials,
+void sx_launch_gemv_partials(const double *T, int rows, TLay tl, int N, const double *coef, double *partials,
                              hipStream_t s) {
     const int nblk = (rows + SX_TILE - 1) / SX_TILE;
     if (nblk == 0) return;
     dim3 grid((N + 255) / 256, nblk);
-    k_gemv_partials<<<grid, 256, 0, s>>>(T, rows, ld, N, coef, partials);
+    k_gemv_partials<<<grid, 256, 0, s>>>(T, rows, tl, N, coef, partials);
 }
 
 void sx_launch_gemv_apply(double *d, Cols c, const double *partials, int nblk, hipStream_t s) {
     k_gemv_apply<<<(c.N + 255) / 256, 256, 0, s>>>(d, c, partials, nblk);
 }
 
-void sx_launch_build_rows(double *T, int rows, int row0, size_t ld, int n, int m, int Ns, const double *A_local,
+void sx_launch_build_rows(double *T, int rows, int row0, TLay tl, int n, int m, int Ns, const double *A_local,
                           const double *b_full, hipStream_t s) {
     if (rows <= 0) return;
     dim3 tb(32, 8);
     dim3 tg((rows + 31) / 32, (n + 31) / 32);
     // A_local == nullptr: the structural columns are already in T (device generator)
-    if (n > 0 && A_local != nullptr) k_fill_structural<<<tg, tb, 0, s>>>(T, rows, ld, n, A_local);
+    if (n > 0 && A_local != nullptr) k_fill_structural<<<tg, tb, 0, s>>>(T, rows, tl.ldA, n, A_local);  // (columns 1..n: region A)
     int gx = (Ns + 255) / 256;
     if (gx > 64) gx = 64;
     dim3 rg(gx, rows);
-    k_fill_rows<<<rg, 256, 0, s>>>(T, rows, row0, ld, n, m, Ns, b_full);
+    k_fill_rows<<<rg, 256, 0, s>>>(T, rows, row0, tl, n, m, Ns, b_full);
 }
 
 void sx_launch_init_vectors(double *d, int N1, int n, int m, int *base, hipStream_t s) {

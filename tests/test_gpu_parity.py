@@ -473,6 +473,59 @@ def test_slack_compaction_tableau_bit_exact(gpu, n, m, k, fused, W, p2p, compact
         assert active == m
 
 
+@pytest.mark.parametrize("cap", [16, 300])
+@pytest.mark.parametrize("n,m,k,fused,W,p2p", [
+    (300, 1100, 200, -1, 1, -1),   # fused batches
+    (300, 1100, 200, 0, 1, -1),    # per-pivot launches
+    (64, 700, 400, -1, 1, -1),     # rows leave again; the swept block grows past region A
+    (200, 1500, 150, -1, 2, 0),    # two shards, RCCL-style exchange
+    (200, 1500, 150, -1, 2, 1),    # two shards, fused batches over peer memory
+])
+def test_two_region_layout_bit_exact(gpu, n, m, k, fused, W, p2p, cap):
+    """the two-region tableau layout (region A: structural columns + the first `cap` stored
+    slack positions, region B: the rest) with a small region A, so activations, leaving-row and
+    entering-column reads and sweeps all cross into region B: every logical entry bit-identical
+    to the oracle's"""
+    p = sx.generateRandomProblem(n, m, n * 100 + m, 1, 100)
+    try:
+        sx.set_regions(cap)
+        sx.set_fused(fused)
+        sx.set_p2p(p2p)
+        sx.set_virtual_ranks(W)
+        s = sx.Session(problem=p)
+        t = s.pivots(k)
+        Tg, dg, bg = s.tableau(m, 1 + n + 2 * m)
+        active = s.active_slacks()
+        s.close()
+    finally:
+        sx.set_virtual_ranks(1)
+        sx.set_p2p(-1)
+        sx.set_fused(-1)
+        sx.set_regions(1)
+    T, d, base, done = _oracle_after(p, k)
+    assert t.pivots == done
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+    assert 0 < active <= done
+
+
+@pytest.mark.parametrize("W,p2p", [(1, -1), (2, 1), (3, 0)])
+@pytest.mark.parametrize("n,m,seed,lo,hi", [(300, 1100, 41100, 1, 100), (64, 128, 6528, 1, 100),
+                                            (129, 1513, 77, -100, 100)])
+def test_two_region_two_phase(gpu, n, m, seed, lo, hi, W, p2p):
+    """whole two-phase solves (GEMV, phase switch, solution) on the two-region layout with a
+    region A of 16 slack positions, on 1-3 shards"""
+    p = sx.generateRandomProblem(n, m, seed, lo, hi)
+    try:
+        sx.set_regions(16)
+        sx.set_virtual_ranks(W)
+        sx.set_p2p(p2p)
+        _check_two_phase(p)
+    finally:
+        sx.set_p2p(-1)
+        sx.set_virtual_ranks(1)
+        sx.set_regions(1)
+
+
 def test_slack_compaction_off_for_negated_rows(gpu):
     """a b < 0 row is negated at build (its -0.0 entries could flip a zero's sign in an
     untouched column): no compaction, still bit-exact"""

@@ -4,7 +4,8 @@ W untimed + K timed phase-1 pivots; per pivot: wall time, sweep time (HIP events
 
 usage: python tools/chain_ab.py <setting>=<v1>,<v2> [config=config5,config3] [rounds=2]
   settings: gather_wide (simplex_set_gather_wide), ld_pad (simplex_set_ld_pad),
-            replicas (simplex_set_record_replicas),
+            replicas (simplex_set_record_replicas), sleep (simplex_set_poll_sleep),
+            regions (simplex_set_regions: 0 plain rows, 1 two-region layout),
             sweep (rows per step:LDS stages, simplex_set_update_rows + simplex_set_sweep_stages;
                    e.g. sweep=4:0,4:3,1:8 -- stages 0 = the register sweep)"""
 import os
@@ -49,8 +50,8 @@ def main():
 
     setter = {"gather_wide": lib.simplex_set_gather_wide, "ld_pad": lib.simplex_set_ld_pad,
               "replicas": lib.simplex_set_record_replicas, "sweep": set_sweep,
-              "sleep": lib.simplex_set_poll_sleep}[name]
-    reset = {"gather_wide": 1, "ld_pad": 0, "replicas": 1, "sweep": "0:0", "sleep": 1}[name]
+              "sleep": lib.simplex_set_poll_sleep, "regions": lib.simplex_set_regions}[name]
+    reset = {"gather_wide": 1, "ld_pad": 0, "replicas": 1, "sweep": "0:0", "sleep": 1, "regions": 1}[name]
     print("stamps (us): ratio compute | ratio argmin+publish | -> selection seen | pass2 + row details |"
           " row compute | obj argmin+publish | -> entering seen | entering history | pivot")
     for r in range(rounds):
