@@ -63,7 +63,8 @@ void simplex_set_fused(int mode);
 /* several shards: run each batch as ONE launch per rank whose ranks hand off through peer
  * memory (xGMI; virtual shards: the same device) instead of per-pivot RCCL calls; -1 auto
  * (default: RCCL ranks when the start-up self-check in simplex_dist_init passed), 0 off,
- * 1 force (virtual shards: only with 1, and W <= 3, so all W launches can run at once) */
+ * 1 force (virtual shards: only with 1; all ranks' batches as one launch, or with
+ * simplex_set_mr_single_launch(0) one launch per rank for W <= 3) */
 void simplex_set_p2p(int mode);
 /* 1 when the peer-memory fused path passed simplex_dist_init's self-check on every rank */
 int simplex_p2p_ready(void);
@@ -89,6 +90,9 @@ void simplex_set_poll_sleep(int k);
  * m > 4096 (1, default), or region A forced to hold `mode` slack positions (>= 2,
  * test hook) */
 void simplex_set_regions(int mode);
+/* virtual shards with the peer-memory batch: every rank's batch in one launch (1, default) or one
+ * launch per rank on its own stream (0; needs as many hardware queues running at once) */
+void simplex_set_mr_single_launch(int on);
 /* extra doubles appended to every tableau row of new engines (rounded up to 16; default 0) */
 void simplex_set_ld_pad(int doubles);
 /* several shards: keep d and U in uncached memory (1) or plain memory (0, default; uncached

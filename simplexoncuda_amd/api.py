@@ -345,6 +345,12 @@ def set_regions(mode):
     _lib.load().simplex_set_regions(int(mode))
 
 
+def set_mr_single_launch(on):
+    """Virtual shards with the peer-memory batch: all ranks' batches in one launch (default) or one
+    launch per rank on its own stream."""
+    _lib.load().simplex_set_mr_single_launch(1 if on else 0)
+
+
 def set_sweep_stages(d):
     """Full-batch sweeps staged through LDS by LDS-DMA, d stages per wave (0: register sweep)."""
     _lib.load().simplex_set_sweep_stages(int(d))

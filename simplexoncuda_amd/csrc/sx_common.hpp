@@ -187,6 +187,20 @@ void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld,
                         BatchChan *chan, const unsigned long long *ga, const unsigned long long *gb,
                         const unsigned long long *gdone, const PeerView &pv, unsigned long long timeout,
                         hipStream_t s);
+// all W virtual ranks' batches (ranks on one GPU) as one launch
+struct MrLaunchRank {
+    const double *T;
+    int rows, row0, rank, tb0, tb1;
+    const int *perm;
+    double *d, *d_save;
+    int *base;
+    DevState *st;
+    Pending pd;
+    BatchChan *chan;
+    const unsigned long long *ga, *gb, *gdone;
+};
+void sx_launch_batch_mr_multi(const MrLaunchRank *ranks, int W, int rpr, size_t ld, TLay tl, Cols c, unsigned B, int k,
+                              int slots, const PeerView &pv, unsigned long long timeout, hipStream_t s);
 void sx_set_update_waves(float w);  // resident-grid multiple of the sweep (default 1)
 void sx_set_gather_wide(int on);
 void sx_set_record_replicas(int n);  // fused batch (one shard): tile records written in n <= 8 copies

@@ -64,6 +64,7 @@ struct Config {
     int exchange_mode = 0;   // 0 auto, 1 tile allgather + row allreduce, 2 row-gather
     int alias = 1;           // store phase-1 artificial columns as their slack columns
     int compact = 1;         // sweep only the slack columns pivots have touched (when exact)
+    int mr_single_launch = 1;  // virtual shards: all ranks' fused batches as one launch (0: one per stream)
     int regions = 1;         // two-region tableau layout (TLay): 0 off, 1 auto (aliasing, m > 4096),
                              // >= 2: region A holds that many slack positions (test hook)
     int fused = -1;          // whole batches in one resident launch: -1 auto (one shard), 0 off
@@ -337,9 +338,10 @@ class Engine {
         if (!xchg || W > SX_MAXW || g_cfg.p2p == 0) return;
         if (rccl && !(g_cfg.p2p == 1 || g_cfg.p2p_ready)) return;
         SX_HIP(hipStreamSynchronize(s));
-        // virtual shards need their W launches to run at once on one device: only when asked for
-        // (a test hook), and for W <= 3 (the engine stream + W streams on 4 hardware queues)
-        if (!rccl && (g_cfg.p2p != 1 || W > 3)) return;
+        // virtual shards: only when asked for (a test hook); their batches run as one launch
+        // (mr_single_launch), or as W launches on W streams for W <= 3 (the engine stream + W
+        // streams on 4 hardware queues)
+        if (!rccl && (g_cfg.p2p != 1 || (W > 3 && !g_cfg.mr_single_launch))) return;
         if (!rccl) {  // virtual shards: every shard's buffers on this device; one stream per shard
             for (auto &x : sh) {
                 pv.T[x.rank] = x.T;
@@ -838,6 +840,33 @@ class Engine {
             Shard &x = sh[0];
             sx_launch_batch(x.T, x.rows, ld, tl, cols(N, x), x.d, x.d_save, x.base, x.st, pending(x), k, x.chan, x.ga, x.gb,
                             stamps, s);
+        } else if (!rccl && g_cfg.mr_single_launch) {
+            // virtual shards (one GPU): every rank's batch in ONE launch, so all ranks' blocks
+            // are resident together whenever the grid fits; they hand off through each other's
+            // buffers exactly as RCCL ranks do through peer memory
+            const int NBg = (N - 1 + SX_TILE - 1) / SX_TILE;
+            std::vector<MrLaunchRank> rk(sh.size());
+            for (size_t i = 0; i < sh.size(); ++i) {
+                Shard &x = sh[i];
+                MrLaunchRank &q = rk[i];
+                q.T = x.T;
+                q.rows = x.rows;
+                q.row0 = x.row0;
+                q.rank = x.rank;
+                q.tb0 = (int)((long long)x.rank * NBg / W);
+                q.tb1 = (int)((long long)(x.rank + 1) * NBg / W);
+                q.perm = compact ? x.perm : nullptr;
+                q.d = x.d;
+                q.d_save = x.d_save;
+                q.base = x.base;
+                q.st = x.st;
+                q.pd = pending(x);
+                q.chan = x.chan;
+                q.ga = x.ga;
+                q.gb = x.gb;
+                q.gdone = x.gdone;
+            }
+            sx_launch_batch_mr_multi(rk.data(), W, rpr, ld, tl, cols(N), rk[0].pd.batch, k, slots, pv, 100000000ull, s);
         } else {
             // every rank's batch runs at once (virtual shards: one stream each, forked from and
             // joined back into the engine stream); the ranks hand off through peer memory
@@ -1273,6 +1302,7 @@ void simplex_set_virtual_ranks(int world) { g_cfg.virtual_ranks = world > 1 ? wo
 void simplex_set_force_exchange(int on) { g_cfg.force_exchange = on ? 1 : 0; }
 void simplex_set_alias(int on) { g_cfg.alias = on ? 1 : 0; }
 void simplex_set_regions(int mode) { g_cfg.regions = mode < 0 ? 1 : mode; }
+void simplex_set_mr_single_launch(int on) { g_cfg.mr_single_launch = on ? 1 : 0; }
 void simplex_set_compact(int on) { g_cfg.compact = on ? 1 : 0; }
 void simplex_set_fused(int mode) { g_cfg.fused = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_p2p(int mode) { g_cfg.p2p = mode < 0 ? -1 : (mode ? 1 : 0); }

@@ -732,89 +732,127 @@ __device__ __forceinline__ void poll_pause() {
     }
 }
 
+// Wave 0 of the block (threads 0..63) polls n <= 64 * SX_GATHER_PER_LANE granules, granule k
+// at base[off(k)], each until it carries `tag`, into out[k] (LDS), all of a round's loads in
+// flight together, no block barrier per poll.  (pay: the payload of every even granule k goes
+// to pay[k / 2] -- records of two granules.)  Wave-uniform result: false when the batch was
+// aborted (or this wait timed out, which aborts it).  Only wave 0 may call it.
+template <typename OFF, bool SYS = false>
+__device__ int poll_wave(const u64 *base, int n, OFF off, unsigned tag, unsigned *out, unsigned *abort_w,
+                         unsigned long long timeout, unsigned *pay) {
+    const int t = threadIdx.x;
+    const u64 t0 = __builtin_amdgcn_s_memrealtime();
+    if (n <= 64) {
+        bool have = t >= n;
+        for (unsigned it = 0;; ++it) {
+            if (!have) {
+                const u64 w = SYS ? ld_sys(base + off(t)) : ld_sc1(base + off(t));
+                if (((unsigned)(w >> 32) | SX_PAYMASK) == (tag | SX_PAYMASK)) {
+                    have = true;
+                    out[t] = (unsigned)w;
+                    if (pay && !(t & 1)) pay[t >> 1] = (unsigned)(w >> 32) & SX_PAYMASK;
+                }
+            }
+            if (__ballot(!have) == 0ull) return 1;
+            if ((it & 63) == 63) {
+                int stop = ld_sc1(abort_w) != 0u;
+                if (!stop && __builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+                    __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    stop = 1;
+                }
+                if (__builtin_amdgcn_readfirstlane(stop)) return 0;
+            }
+            poll_pause();
+        }
+    }
+    unsigned miss = 0u;  // bit c: granule t + 64 c still missing
+#pragma unroll
+    for (int c = 0; c < SX_GATHER_PER_LANE; ++c)
+        if (t + 64 * c < n) miss |= 1u << c;
+    for (unsigned it = 0;; ++it) {
+        u64 w[SX_GATHER_PER_LANE];
+#pragma unroll
+        for (int c = 0; c < SX_GATHER_PER_LANE; ++c)
+            if ((miss >> c) & 1u) w[c] = SYS ? ld_sys(base + off(t + 64 * c)) : ld_sc1(base + off(t + 64 * c));
+#pragma unroll
+        for (int c = 0; c < SX_GATHER_PER_LANE; ++c) {
+            const int k = t + 64 * c;
+            if (((miss >> c) & 1u) && ((unsigned)(w[c] >> 32) | SX_PAYMASK) == (tag | SX_PAYMASK)) {
+                miss &= ~(1u << c);
+                out[k] = (unsigned)w[c];
+                if (pay && !(k & 1)) pay[k >> 1] = (unsigned)(w[c] >> 32) & SX_PAYMASK;
+            }
+        }
+        if (__ballot(miss != 0u) == 0ull) return 1;
+        if ((it & 63) == 63) {
+            int stop = ld_sc1(abort_w) != 0u;
+            if (!stop && __builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+                __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                stop = 1;
+            }
+            if (__builtin_amdgcn_readfirstlane(stop)) return 0;
+        }
+        poll_pause();
+    }
+}
+
+// Pass 2 of the reference's argmin (deviceReduceKernel<false><<<1,1024>>>, reduction.cu:239-241)
+// over nt <= 256 two-granule tile records already gathered into s_g / s_pay, run by wave 0
+// alone: part p (tile p's winner) sits on lane p % 64 of round p / 64, so round r's two halves
+// are the reference warps 2r and 2r + 1 (half_argmin); their winners go through LDS to lanes
+// 0..2R-1, padded with (DBL_MAX, -1) to the reference's 32 warps, and one more half_argmin
+// combines them -- the combines of block_argmin512 on the same parts.  Result in lane 0;
+// any_elig (wave-uniform): some record carries the "entry >= eps" payload bit (ratio tiles).
+__device__ __forceinline__ void wave_pass2(const unsigned *s_g, const unsigned *s_pay, int nt, double *s_v,
+                                           int *s_i, double &v_out, int &i_out, int &any_elig) {
+    const int lane = threadIdx.x;
+    const int R = (nt + 63) >> 6;
+    unsigned te = 0u;
+    for (int r = 0; r < R; ++r) {
+        const int p = r * 64 + lane;
+        double v = DBL_MAX;
+        int i = -1;
+        if (p < nt) {
+            const double cv = gd(s_g[2 * p], s_g[2 * p + 1]);
+            const unsigned pl = s_pay[p];
+            te |= (pl >> 10) & 1u;
+            if (cmp_eps(cv, v) < 0) {
+                v = cv;
+                i = (pl & SX_NOIDX) == SX_NOIDX ? -1 : p * SX_TILE + (int)(pl & SX_NOIDX);
+            }
+        }
+        half_argmin(v, i);
+        if ((lane & 31) == 0) {
+            s_v[2 * r + (lane >> 5)] = v;
+            s_i[2 * r + (lane >> 5)] = i;
+        }
+    }
+    double v = DBL_MAX;
+    int i = -1;
+    if (lane < 2 * R) {
+        v = s_v[lane];
+        i = s_i[lane];
+    }
+    half_argmin(v, i);
+    any_elig = __ballot(te != 0u) != 0ull;
+    v_out = v;
+    i_out = i;
+}
+
 // The block reads n <= 4 * blockDim granules, granule k at base[off(k)], each until it
-// carries `tag`, into out[k] (LDS): every thread polls its own granules (k = t, t + 512, ...),
-// all of them in flight together, until the block agrees that all have arrived.  Block-uniform
+// carries `tag`, into out[k] (LDS): up to 64 * SX_GATHER_PER_LANE granules one wave polls
+// (poll_wave); larger gathers: every thread polls its own granules (k = t, t + 512, ...), all
+// of them in flight together, until the block agrees that all have arrived.  Block-uniform
 // result: false when the batch was aborted (or this wait timed out, which aborts it).  Every
 // thread of the block must call it.
 template <typename OFF, bool SYS = false>
 __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, unsigned *out, unsigned *abort_w,
                               int *s_ok, unsigned long long timeout = 20000000ull, unsigned *pay = nullptr,
                               int wide = 1) {
-    // (pay: the payload of every even granule k goes to pay[k / 2] -- records of two granules)
     const int t = threadIdx.x, nt = blockDim.x;
-    if (n <= 64) {  // one wave polls, no block barrier per poll
+    if (n <= 64 || (wide && n <= 64 * SX_GATHER_PER_LANE)) {
         if (t < 64) {
-            const bool exists = t < n;
-            bool have = !exists;
-            int ok = 1;
-            const u64 t0 = __builtin_amdgcn_s_memrealtime();
-            for (unsigned it = 0;; ++it) {
-                if (!have) {
-                    const u64 w = SYS ? ld_sys(base + off(t)) : ld_sc1(base + off(t));
-                    if (((unsigned)(w >> 32) | SX_PAYMASK) == (tag | SX_PAYMASK)) {
-                        have = true;
-                        out[t] = (unsigned)w;
-                        if (pay && !(t & 1)) pay[t >> 1] = (unsigned)(w >> 32) & SX_PAYMASK;
-                    }
-                }
-                if (__ballot(!have) == 0ull) break;
-                if ((it & 63) == 63) {
-                    int stop = ld_sc1(abort_w) != 0u;
-                    if (!stop && __builtin_amdgcn_s_memrealtime() - t0 > timeout) {
-                        __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        stop = 1;
-                    }
-                    if (__builtin_amdgcn_readfirstlane(stop)) {
-                        ok = 0;
-                        break;
-                    }
-                }
-                poll_pause();
-            }
-            if (t == 0) *s_ok = ok;
-        }
-        __syncthreads();
-        return *s_ok != 0;
-    }
-    if (wide && n <= 64 * SX_GATHER_PER_LANE) {
-        // one wave polls up to SX_GATHER_PER_LANE granules per lane, all of a round's loads in
-        // flight together, and the block meets once at the end (no barrier per poll)
-        if (t < 64) {
-            unsigned miss = 0u;  // bit c: granule t + 64 c still missing
-#pragma unroll
-            for (int c = 0; c < SX_GATHER_PER_LANE; ++c)
-                if (t + 64 * c < n) miss |= 1u << c;
-            int ok = 1;
-            const u64 t0 = __builtin_amdgcn_s_memrealtime();
-            for (unsigned it = 0;; ++it) {
-                u64 w[SX_GATHER_PER_LANE];
-#pragma unroll
-                for (int c = 0; c < SX_GATHER_PER_LANE; ++c)
-                    if ((miss >> c) & 1u) w[c] = SYS ? ld_sys(base + off(t + 64 * c)) : ld_sc1(base + off(t + 64 * c));
-#pragma unroll
-                for (int c = 0; c < SX_GATHER_PER_LANE; ++c) {
-                    const int k = t + 64 * c;
-                    if (((miss >> c) & 1u) && ((unsigned)(w[c] >> 32) | SX_PAYMASK) == (tag | SX_PAYMASK)) {
-                        miss &= ~(1u << c);
-                        out[k] = (unsigned)w[c];
-                        if (pay && !(k & 1)) pay[k >> 1] = (unsigned)(w[c] >> 32) & SX_PAYMASK;
-                    }
-                }
-                if (__ballot(miss != 0u) == 0ull) break;
-                if ((it & 63) == 63) {
-                    int stop = ld_sc1(abort_w) != 0u;
-                    if (!stop && __builtin_amdgcn_s_memrealtime() - t0 > timeout) {
-                        __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        stop = 1;
-                    }
-                    if (__builtin_amdgcn_readfirstlane(stop)) {
-                        ok = 0;
-                        break;
-                    }
-                }
-                poll_pause();
-            }
+            const int ok = poll_wave<OFF, SYS>(base, n, off, tag, out, abort_w, timeout, pay);
             if (t == 0) *s_ok = ok;
         }
         __syncthreads();
@@ -881,8 +919,12 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
     __shared__ double s_a[SX_TILE], s_b[SX_TILE];    // ratio blocks: entering column, RHS (winner lookup)
     __shared__ unsigned s_g[4 * SX_TILE];            // gathered granules
     __shared__ unsigned s_pay[SX_TILE];              // their payloads (two-granule records)
-    __shared__ int s_ok, s_flag, s_win;
-    __shared__ double s_wv;
+    __shared__ int s_ok;
+    // per-step results written by wave 0 before the step's one barrier (each step its own
+    // words, so no wave still reading an earlier step's result can see them change)
+    __shared__ int s_sel_ok, s_sel_r, s_sel_any, s_det_ok, s_ent_ok, s_ent_e, s_ue_ok;
+    __shared__ double s_ent_v, s_br;
+    __shared__ int s_welig[SX_TILE / 64];
     const int t = threadIdx.x;
     const bool isA = (int)blockIdx.x < NA;
     // the tile records are written in nrep replicas; a block polls replica blockIdx % nrep, so
@@ -973,23 +1015,38 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                 if (blockIdx.x == 0) SX_STAMP(2);
                 s_a[t] = a;
                 s_b[t] = b;
-                const int any = __syncthreads_or(elig);
-                block_argmin512(rv, ri, s_v, s_i);
-                if (t == 0) {
-                    s_win = ri >= 0 ? ri - (int)blockIdx.x * SX_TILE : 0;
-                    s_wv = rv;
+                // pass 1 (reduction.cu:51-80): every half-wave its tree, one block barrier, then
+                // wave 0 combines the 16 half winners (block_argmin512's second step) and
+                // publishes the record alone
+                half_argmin(rv, ri);
+                const int anyw = __ballot(elig) != 0ull;
+                if ((t & 31) == 0) {
+                    s_v[t >> 5] = rv;
+                    s_i[t >> 5] = ri;
                 }
-                if (t == 0) s_flag = ri >= 0 ? (int)(ri - (int)blockIdx.x * SX_TILE) : (int)SX_NOIDX;
+                if ((t & 63) == 0) s_welig[t >> 6] = anyw;
                 __syncthreads();
-                const int wl = s_win;
-                {  // the record: v (payload: index, "any" bit), pad, a, b, then F[winner][s] for s < q
-                    const unsigned pl = (unsigned)s_flag | ((unsigned)any << 10);
+                if (t < 64) {
+                    double v = t < 16 ? s_v[t] : DBL_MAX;
+                    int i = t < 16 ? s_i[t] : -1;
+                    half_argmin(v, i);
+                    int any = 0;
+#pragma unroll
+                    for (int w = 0; w < SX_TILE / 64; ++w) any |= s_welig[w];
+                    const int wi = __builtin_amdgcn_readfirstlane(i);
+                    const long long vb = __double_as_longlong(v);
+                    const double wv = __longlong_as_double(
+                        ((long long)__builtin_amdgcn_readfirstlane((int)(vb >> 32)) << 32) |
+                        (long long)(unsigned)__builtin_amdgcn_readfirstlane((int)vb));
+                    const int wl = wi >= 0 ? wi - (int)blockIdx.x * SX_TILE : 0;
+                    // the record: v (payload: index, "any" bit), pad, a, b, then F[winner][s] for s < q
+                    const unsigned pl = (wi >= 0 ? (unsigned)wl : SX_NOIDX) | ((unsigned)any << 10);
                     const int nG = 8 + 2 * q;
-                    for (int idx = t; idx < nrep * nG; idx += SX_TILE) {
+                    for (int idx = t; idx < nrep * nG; idx += 64) {
                         const int r = idx / nG, k = idx - r * nG;
                         if (k == 2 || k == 3) continue;
-                        const double val = k < 2 ? s_wv : k < 6 ? s_a[wl] : k < 8 ? s_b[wl]
-                                                                           : s_hist[((k - 8) >> 1) * SX_TILE + wl];
+                        const double val = k < 2 ? wv : k < 6 ? s_a[wl] : k < 8 ? s_b[wl]
+                                                                        : s_hist[((k - 8) >> 1) * SX_TILE + wl];
                         const unsigned long long bits64 = (unsigned long long)__double_as_longlong(val);
                         put_g(ga + (size_t)r * sx_ga_size() + (size_t)blockIdx.x * SX_GA_STRIDE + k,
                               (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64, k < 2 ? (tag | pl) : tag);
@@ -997,28 +1054,51 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                 }
                 if (blockIdx.x == 0) SX_STAMP(1);
             }
-            // ---- selection: every block runs pass 2 over the ratio-tile winners
-            if (!gather_tagged(gam, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay, gw)) {
-                aborted = true;
-                break;
+            // ---- selection: every block runs pass 2 over the ratio-tile winners.  Wave 0 polls
+            // the records and runs the tree in registers (wave_pass2); one block barrier.
+            int r, anyall;
+            if (gw && 2 * NA <= 64 * SX_GATHER_PER_LANE) {
+                if (t < 64) {
+                    const int ok = poll_wave(gam, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
+                    double tv = DBL_MAX;
+                    int ti = -1, any = 0;
+                    if (ok) wave_pass2(s_g, s_pay, NA, s_v, s_i, tv, ti, any);
+                    if (t == 0) {
+                        s_sel_ok = ok;
+                        s_sel_r = ti;
+                        s_sel_any = any;
+                    }
+                }
+                __syncthreads();
+                if (!s_sel_ok) {
+                    aborted = true;
+                    break;
+                }
+                r = s_sel_r;
+                anyall = s_sel_any;
+            } else {
+                if (!gather_tagged(gam, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay, gw)) {
+                    aborted = true;
+                    break;
+                }
+                double tv = DBL_MAX;
+                int ti = -1, te = 0;
+                if (t < NA) {
+                    const double cv = gd(s_g[2 * t], s_g[2 * t + 1]);
+                    const unsigned pl = s_pay[t];
+                    te = (int)((pl >> 10) & 1u);
+                    if (cmp_eps(cv, tv) < 0) {
+                        tv = cv;
+                        ti = (pl & SX_NOIDX) == SX_NOIDX ? -1 : t * SX_TILE + (int)(pl & SX_NOIDX);
+                    }
+                }
+                anyall = __syncthreads_or(SX_ELIG(te));
+                block_argmin512(tv, ti, s_v, s_i);
+                if (t == 0) s_sel_r = ti;
+                __syncthreads();
+                r = s_sel_r;
             }
             if (!isA && tb == 0) SX_STAMP(3);
-            double tv = DBL_MAX;
-            int ti = -1, te = 0;
-            if (t < NA) {
-                const double cv = gd(s_g[2 * t], s_g[2 * t + 1]);
-                const unsigned pl = s_pay[t];
-                te = (int)((pl >> 10) & 1u);
-                if (cmp_eps(cv, tv) < 0) {
-                    tv = cv;
-                    ti = (pl & SX_NOIDX) == SX_NOIDX ? -1 : t * SX_TILE + (int)(pl & SX_NOIDX);
-                }
-            }
-            const int anyall = __syncthreads_or(SX_ELIG(te));
-            block_argmin512(tv, ti, s_v, s_i);
-            if (t == 0) s_win = ti;
-            __syncthreads();
-            const int r = s_win;
             if (!anyall) {  // solver.cu:96-102
                 status = SX_UNBOUNDED;
                 break;
@@ -1029,23 +1109,31 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
             }
             // the objective blocks' pivot-row load does not wait for the winner's details
             double u = liveB ? T[tl.idx(r, mj)] : 0.0;
-            const int wt = r / SX_TILE;
-            if (!gather_tagged(gam + (size_t)wt * SX_GA_STRIDE + 4, 4 + 2 * q, [](int k) { return k; }, tag, s_g,
-                               &ch->abort_w, &s_ok)) {
+            // the winner's details (pivot, RHS, factor history), read by wave 0 into LDS
+            if (t < 64) {
+                const int wt = r / SX_TILE;
+                const int ok = poll_wave(gam + (size_t)wt * SX_GA_STRIDE + 4, 4 + 2 * q, [](int k) { return k; }, tag,
+                                         s_g, &ch->abort_w, 20000000ull, (unsigned *)nullptr);
+                if (ok) {
+                    if (t < q) s_fr[t] = gd(s_g[4 + 2 * t], s_g[5 + 2 * t]);
+                    if (t == 0) {
+                        s_p[q] = gd(s_g[0], s_g[1]);
+                        s_br = gd(s_g[2], s_g[3]);
+                        s_r[q] = r;
+                        s_e[q] = e;
+                    }
+                }
+                if (t == 0) s_det_ok = ok;
+            }
+            __syncthreads();
+            if (!s_det_ok) {
                 aborted = true;
                 break;
             }
-            const double p = gd(s_g[0], s_g[1]), br = gd(s_g[2], s_g[3]);
-            if (t < q) s_fr[t] = gd(s_g[4 + 2 * t], s_g[5 + 2 * t]);
-            if (t == 0) {
-                s_p[q] = p;
-                s_r[q] = r;
-                s_e[q] = e;
-            }
+            const double p = s_p[q], br = s_br;
             cnt = q + 1;
             last_r = r;
             last_e = e;
-            __syncthreads();
             if (isA) {
                 // ---- this pivot's factor column and the rows' new RHS (solver.cu:34-46)
                 const double f = -a / p;
@@ -1105,20 +1193,30 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                         i = ia;
                     }
                 }
-                block_argmin512(v, i, s_v, s_i);  // pass 1 (reduction.cu:51-80)
-                if (t == 0) {
-                    s_win = i >= 0 ? i - tb * SX_TILE : 0;
-                    s_wv = v;
-                    s_flag = i;
+                // pass 1 (reduction.cu:51-80): half-wave trees, one block barrier, wave 0 combines
+                // the half winners and publishes the record alone
+                half_argmin(v, i);
+                if ((t & 31) == 0) {
+                    s_v[t >> 5] = v;
+                    s_i[t >> 5] = i;
                 }
                 __syncthreads();
-                {  // the record: v (payload: index), pad, then U[s][winner] for s <= q
-                    const unsigned pl = s_flag >= 0 ? (unsigned)(s_flag - tb * SX_TILE) : SX_NOIDX;
+                if (t < 64) {
+                    double wv = t < 16 ? s_v[t] : DBL_MAX;
+                    int wi = t < 16 ? s_i[t] : -1;
+                    half_argmin(wv, wi);
+                    wi = __builtin_amdgcn_readfirstlane(wi);
+                    const long long vb = __double_as_longlong(wv);
+                    wv = __longlong_as_double(((long long)__builtin_amdgcn_readfirstlane((int)(vb >> 32)) << 32) |
+                                              (long long)(unsigned)__builtin_amdgcn_readfirstlane((int)vb));
+                    const int win = wi >= 0 ? wi - tb * SX_TILE : 0;
+                    // the record: v (payload: index), pad, then U[s][winner] for s <= q
+                    const unsigned pl = wi >= 0 ? (unsigned)win : SX_NOIDX;
                     const int nG = 4 + 2 * (q + 1);
-                    for (int idx = t; idx < nrep * nG; idx += SX_TILE) {
+                    for (int idx = t; idx < nrep * nG; idx += 64) {
                         const int r = idx / nG, k = idx - r * nG;
                         if (k == 2 || k == 3) continue;
-                        const double val = k < 2 ? s_wv : s_hist[((k - 4) >> 1) * SX_TILE + s_win];
+                        const double val = k < 2 ? wv : s_hist[((k - 4) >> 1) * SX_TILE + win];
                         const unsigned long long bits64 = (unsigned long long)__double_as_longlong(val);
                         put_g(gb + (size_t)r * sx_gb_size() + (size_t)tb * SX_GB_STRIDE + k,
                               (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64, k < 2 ? (tag | pl) : tag);
@@ -1126,40 +1224,66 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                 }
                 if (tb == 0) SX_STAMP(4);
             }
-            // ---- entering variable of pivot q + 1: every block runs pass 2 over the objective tiles
-            if (!gather_tagged(gbm, 2 * NB, rec2_b, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay, gw)) {
-                aborted = true;
-                break;
-            }
-            double ev = DBL_MAX;
-            int ei = -1;
-            if (t < NB) {
-                const double cv = gd(s_g[2 * t], s_g[2 * t + 1]);
-                const unsigned pl = s_pay[t] & SX_NOIDX;
-                if (cmp_eps(cv, ev) < 0) {
-                    ev = cv;
-                    ei = pl == SX_NOIDX ? -1 : t * SX_TILE + (int)pl;
+            // ---- entering variable of pivot q + 1: every block runs pass 2 over the objective
+            // tiles (wave 0 polls and runs the tree; one block barrier)
+            if (gw && 2 * NB <= 64 * SX_GATHER_PER_LANE) {
+                if (t < 64) {
+                    const int ok = poll_wave(gbm, 2 * NB, rec2_b, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
+                    double ev = DBL_MAX;
+                    int ei = -1, any = 0;
+                    if (ok) wave_pass2(s_g, s_pay, NB, s_v, s_i, ev, ei, any);
+                    if (t == 0) {
+                        s_ent_ok = ok;
+                        s_ent_e = ei;
+                        s_ent_v = ev;
+                    }
                 }
-            }
-            block_argmin512(ev, ei, s_v, s_i);
-            if (t == 0) {
-                s_win = ei;
-                s_wv = ev;
-            }
-            __syncthreads();
-            e = s_win;
-            dmin = s_wv;
-            if (liveA) a_pre = T[tl.idx(li, c.map(1 + (e >= 0 ? e : 0)))];
-            if (isA && blockIdx.x == 0) SX_STAMP(5);
-            // the ratio blocks need the pending pivot rows' entries in the new entering column
-            if (isA && q + 1 < K && e >= 0 && cmp_eps(dmin, 0.0) < 0) {
-                if (!gather_tagged(gbm + (size_t)(e / SX_TILE) * SX_GB_STRIDE + 4, 2 * (q + 1), [](int k) { return k; },
-                                   tag, s_g, &ch->abort_w, &s_ok)) {
+                __syncthreads();
+                if (!s_ent_ok) {
                     aborted = true;
                     break;
                 }
-                if (t <= q) s_ue[t] = gd(s_g[2 * t], s_g[2 * t + 1]);
+            } else {
+                if (!gather_tagged(gbm, 2 * NB, rec2_b, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay, gw)) {
+                    aborted = true;
+                    break;
+                }
+                double ev = DBL_MAX;
+                int ei = -1;
+                if (t < NB) {
+                    const double cv = gd(s_g[2 * t], s_g[2 * t + 1]);
+                    const unsigned pl = s_pay[t] & SX_NOIDX;
+                    if (cmp_eps(cv, ev) < 0) {
+                        ev = cv;
+                        ei = pl == SX_NOIDX ? -1 : t * SX_TILE + (int)pl;
+                    }
+                }
+                block_argmin512(ev, ei, s_v, s_i);
+                if (t == 0) {
+                    s_ent_e = ei;
+                    s_ent_v = ev;
+                }
                 __syncthreads();
+            }
+            e = s_ent_e;
+            dmin = s_ent_v;
+            if (liveA) a_pre = T[tl.idx(li, c.map(1 + (e >= 0 ? e : 0)))];
+            if (isA && blockIdx.x == 0) SX_STAMP(5);
+            // the ratio blocks need the pending pivot rows' entries in the new entering column
+            // (wave 0 reads them into LDS; one block barrier)
+            if (isA && q + 1 < K && e >= 0 && cmp_eps(dmin, 0.0) < 0) {
+                if (t < 64) {
+                    const int ok = poll_wave(gbm + (size_t)(e / SX_TILE) * SX_GB_STRIDE + 4, 2 * (q + 1),
+                                             [](int k) { return k; }, tag, s_g, &ch->abort_w, 20000000ull,
+                                             (unsigned *)nullptr);
+                    if (ok && t <= q) s_ue[t] = gd(s_g[2 * t], s_g[2 * t + 1]);
+                    if (t == 0) s_ue_ok = ok;
+                }
+                __syncthreads();
+                if (!s_ue_ok) {
+                    aborted = true;
+                    break;
+                }
             }
         }
         if (liveB) d[1 + ia] = dj;
@@ -1227,7 +1351,7 @@ __device__ __forceinline__ double ld_sys(const double *p) {
     return __longlong_as_double((long long)ld_sys(reinterpret_cast<const u64 *>(p)));
 }
 
-__global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, int rows, int row0, int rpr, size_t ld, TLay tl,
+__device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const double *__restrict__ T, int rows, int row0, int rpr, size_t ld, TLay tl,
                                                   Cols c, double *__restrict__ d, double *__restrict__ d_save, int *base,
                                                   DevState *st, double *U, double *F, PivRec *recs,
                                                   unsigned long long *PM, unsigned B, int K,
@@ -1246,7 +1370,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
     __shared__ int s_ok, s_flag, s_win;
     __shared__ double s_wv;
     const int t = threadIdx.x;
-    const bool isA = (int)blockIdx.x < slots;
+    const bool isA = bid < slots;
     const int NAg = W * slots;
     const int status0 = st->status;
     const long long piv0 = st->pivots, cap = st->max_pivots;
@@ -1257,10 +1381,10 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
     auto gather_a = [](int k) { return rec2_a(k); };
     auto gather_b = [](int k) { return rec2_b(k); };
     auto ident = [](int k) { return k; };
-    const int li = blockIdx.x * SX_TILE + t;
+    const int li = bid * SX_TILE + t;
     const bool liveA = isA && li < rows;
-    const int gt = rank * slots + (int)blockIdx.x;  // global ratio tile of this block
-    const int tb = tb0 + (int)blockIdx.x - slots;   // objective tile of this block
+    const int gt = rank * slots + bid;  // global ratio tile of this block
+    const int tb = tb0 + bid - slots;   // objective tile of this block
     const int L = c.N - 1;
     const int ia = tb * SX_TILE + t;
     const bool liveB = !isA && ia < L;
@@ -1271,7 +1395,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
         // this rank's whole objective row as the batch found it (restored by the host on
         // SX_HANG): every rank writes d slices only at the end of the batch, after hand-offs
         // that need every block of every rank, so this copy is complete before any change
-        for (int j = blockIdx.x * blockDim.x + t; j < c.N; j += gridDim.x * blockDim.x) d_save[j] = d[j];
+        for (int j = bid * blockDim.x + t; j < c.N; j += nbl * blockDim.x) d_save[j] = d[j];
         double b = liveA ? T[tl.idx(li, 0)] : 0.0;
         unsigned bits = 0u;
         // the entering column's stored value of this row: loaded as soon as the entering
@@ -1326,7 +1450,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
                 const int any = __syncthreads_or(elig);
                 block_argmin512(rv, ri, s_v, s_i);
                 if (t == 0) {
-                    s_win = ri >= 0 ? ri - row0 - (int)blockIdx.x * SX_TILE : 0;
+                    s_win = ri >= 0 ? ri - row0 - bid * SX_TILE : 0;
                     s_wv = rv;
                     s_flag = ri;
                 }
@@ -1414,7 +1538,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
                         b = fma(f, br, b);
                     }
                 }
-                if (blockIdx.x == 0 && t == 0) {  // every rank keeps the whole basis and the records
+                if (bid == 0 && t == 0) {  // every rank keeps the whole basis and the records
                     recs[q].r = r;                // (base[r] = e, solver.cu:105: at the end of the batch)
                     recs[q].e = e;
                     recs[q].p = p;
@@ -1523,7 +1647,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
     __syncthreads();
     if (t == 0) {
         const unsigned k = __hip_atomic_fetch_add(&ch->exit_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_flag = (k == gridDim.x - 1);
+        s_flag = (k == nbl - 1);
         if (s_flag) __hip_atomic_store(&ch->exit_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
@@ -1555,6 +1679,51 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
     }
     st->e_next = e;
     st->dmin_next = dmin;
+}
+
+
+__global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, int rows, int row0, int rpr, size_t ld, TLay tl,
+                                                  Cols c, double *__restrict__ d, double *__restrict__ d_save, int *base,
+                                                  DevState *st, double *U, double *F, PivRec *recs,
+                                                  unsigned long long *PM, unsigned B, int K,
+                                                  int slots, int W, int rank, int tb0, int tb1, int NBg,
+                                                  BatchChan *ch, const u64 *ga, const u64 *gb, const u64 *gdone,
+                                                  PeerView pv, unsigned long long timeout, int gw) {
+    batch_mr_body((int)blockIdx.x, gridDim.x, T, rows, row0, rpr, ld, tl, c, d, d_save, base, st, U, F, recs, PM, B, K, slots, W, rank, tb0, tb1, NBg, ch, ga, gb, gdone, pv, timeout, gw);
+}
+
+// All W virtual ranks' batches in ONE launch (ranks on one GPU): block b belongs to the rank k
+// with first[k] <= b < first[k + 1], as its block b - first[k].  One grid, so every rank's
+// blocks are resident together whenever the grid fits the device -- W launches on W streams
+// also need W hardware queues that run at once, which a process does not control.
+struct MrRank {
+    const double *T;
+    int rows, row0, rank, tb0, tb1;
+    const int *perm;
+    double *d, *d_save;
+    int *base;
+    DevState *st;
+    double *U, *F;
+    PivRec *recs;
+    unsigned long long *PM;
+    BatchChan *ch;
+    const u64 *ga, *gb, *gdone;
+};
+struct MrRanks {
+    MrRank r[SX_MAXW];
+    int first[SX_MAXW + 1];
+};
+__global__ __launch_bounds__(512) void k_batch_mr_multi(MrRanks R, int rpr, size_t ld, TLay tl, Cols c, unsigned B,
+                                                        int K, int slots, int W, int NBg, PeerView pv,
+                                                        unsigned long long timeout, int gw) {
+    int k = 0;
+    while (k + 1 < W && (int)blockIdx.x >= R.first[k + 1]) ++k;
+    const MrRank &x = R.r[k];
+    Cols cx = c;
+    cx.perm = x.perm;
+    batch_mr_body((int)blockIdx.x - R.first[k], (unsigned)(R.first[k + 1] - R.first[k]), x.T, x.rows, x.row0, rpr, ld,
+                  tl, cx, x.d, x.d_save, x.base, x.st, x.U, x.F, x.recs, x.PM, B, K, slots, W, x.rank, x.tb0, x.tb1,
+                  NBg, x.ch, x.ga, x.gb, x.gdone, pv, timeout, gw);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2257,6 +2426,8 @@ bool sx_batch_mr_fits(int slots, int nb_local, int k, int grids) {
         SX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
         SX_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_batch_mr),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)batch_lds(SX_KMAX)));
+        SX_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_batch_mr_multi),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)batch_lds(SX_KMAX)));
         int n = 0;
         SX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_batch_mr, SX_TILE, batch_lds(k)));
         per_cu[k] = n > 0 ? n : -1;
@@ -2276,6 +2447,43 @@ void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld,
                                                                   pd.recs, pd.PM, pd.batch, k, slots, W, rank, tb0,
                                                                   tb1, NBg, chan, ga, gb, gdone, pv, timeout,
                                                                   g_gather_wide);
+}
+
+void sx_launch_batch_mr_multi(const MrLaunchRank *ranks, int W, int rpr, size_t ld, TLay tl, Cols c, unsigned B, int k,
+                              int slots, const PeerView &pv, unsigned long long timeout, hipStream_t s) {
+    const int NBg = (c.N - 1 + SX_TILE - 1) / SX_TILE;
+    if (W < 1 || W > SX_MAXW || W * slots > SX_TILE || NBg > SX_TILE || NBg < 1)
+        SX_FATAL("multi-rank fused batch: bad shape");
+    MrRanks R;
+    R.first[0] = 0;
+    for (int i = 0; i < W; ++i) {
+        const MrLaunchRank &q = ranks[i];
+        if (q.tb0 < 0 || q.tb1 > NBg || q.tb0 > q.tb1) SX_FATAL("multi-rank fused batch: bad objective tiles");
+        MrRank &x = R.r[i];
+        x.T = q.T;
+        x.rows = q.rows;
+        x.row0 = q.row0;
+        x.rank = q.rank;
+        x.tb0 = q.tb0;
+        x.tb1 = q.tb1;
+        x.perm = q.perm;
+        x.d = q.d;
+        x.d_save = q.d_save;
+        x.base = q.base;
+        x.st = q.st;
+        x.U = q.pd.U;
+        x.F = q.pd.F;
+        x.recs = q.pd.recs;
+        x.PM = q.pd.PM;
+        x.ch = q.chan;
+        x.ga = q.ga;
+        x.gb = q.gb;
+        x.gdone = q.gdone;
+        R.first[i + 1] = R.first[i] + slots + (q.tb1 - q.tb0);
+    }
+    for (int i = W + 1; i <= SX_MAXW; ++i) R.first[i] = R.first[W];
+    k_batch_mr_multi<<<R.first[W], SX_TILE, batch_lds(k), s>>>(R, rpr, ld, tl, c, B, k, slots, W, NBg, pv, timeout,
+                                                               g_gather_wide);
 }
 
 // every XCD's L2 writes back its dirty lines (blocks are dealt over all XCDs; each block's

@@ -9,8 +9,8 @@ container) holds SHA-256 digests of the CPU oracle's phase-1 state -- logical ta
 Here the same instance is synthesised in HBM, 48 pivots run (one full 32-pivot batch and a
 partial one), and the digests of the GPU's state must match: on one shard (fused batch), on
 row-block virtual shards through both per-pivot exchanges (the W = 4 split of config 4, the
-W = 8 split of config 5), and through the peer-memory fused batch (W = 2, 3: the virtual
-shards' launches must run at once on one GPU's 4 hardware queues).
+W = 8 split of config 5), and through the peer-memory fused batch (W = 2, 3, and the multi-GPU
+splits W = 4 / 8: the virtual ranks' batches run as one launch on one GPU).
 """
 import hashlib
 import json
@@ -59,16 +59,16 @@ def run(name, W=1, mode=0, p2p=-1):
     assert sha(T) == pin["sha256_T"]
 
 
-@pytest.mark.parametrize("W,mode,p2p", [(1, 0, -1), (4, 1, 0), (4, 2, 0), (2, 0, 1), (3, 0, 1)])
+@pytest.mark.parametrize("W,mode,p2p", [(1, 0, -1), (4, 1, 0), (4, 2, 0), (2, 0, 1), (3, 0, 1), (4, 0, 1)])
 def test_config4_pivots_match_oracle(gpu, W, mode, p2p):
     run("config4", W, mode, p2p)
 
 
-@pytest.mark.parametrize("W,mode,p2p", [(1, 0, -1), (8, 1, 0), (8, 2, 0), (3, 0, 1)])
+@pytest.mark.parametrize("W,mode,p2p", [(1, 0, -1), (8, 1, 0), (8, 2, 0), (3, 0, 1), (8, 0, 1)])
 def test_config5_pivots_match_oracle(gpu, W, mode, p2p):
     run("config5", W, mode, p2p)
 
 
-@pytest.mark.parametrize("W,mode,p2p", [(1, 0, -1), (8, 1, 0), (2, 0, 1)])
+@pytest.mark.parametrize("W,mode,p2p", [(1, 0, -1), (8, 1, 0), (2, 0, 1), (8, 0, 1)])
 def test_config5_degenerate_variant_pivots_match_oracle(gpu, W, mode, p2p):
     run("config5_degenerate", W, mode, p2p)

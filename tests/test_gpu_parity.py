@@ -249,7 +249,7 @@ def test_large_batch_sweeps_bit_exact(gpu, batch, rb, sc1):
 
 
 @pytest.mark.parametrize("batch", [1, 16, 32])
-@pytest.mark.parametrize("W", [2, 3])
+@pytest.mark.parametrize("W", [2, 3, 4, 8])
 def test_p2p_fused_virtual_ranks(gpu, batch, W):
     """the multi-rank fused batch (ranks hand off through each other's memory, objective tiles
     split across ranks): W virtual shards on one GPU, their launches running at once"""
@@ -260,7 +260,27 @@ def test_p2p_fused_virtual_ranks(gpu, batch, W):
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 
+@pytest.mark.parametrize("single", [1, 0])
 @pytest.mark.parametrize("W", [2, 3])
+def test_p2p_fused_launch_forms(gpu, W, single):
+    """the virtual ranks' peer-memory batches as one launch and as one launch per rank on its own
+    stream (the RCCL ranks' form): bit-exact, and every batch completed on the fused path (no
+    hand-off timed out and fell back to the per-pivot path)"""
+    lib = sx.load()
+    T, d, base = _phase1_state(300, 1100, 11)
+    h0, f0 = lib.simplex_hang_recoveries(), lib.simplex_fused_batches()
+    try:
+        sx.set_mr_single_launch(single)
+        Tg, dg, bg, st, done = _pivots_with({"batch": 32, "W": W, "p2p": 1}, T, d, base, 150)
+    finally:
+        sx.set_mr_single_launch(1)
+    st_o, done_o = oracle.solve(T, d, base, max_pivots=150)
+    assert done == done_o
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+    assert lib.simplex_fused_batches() > f0 and lib.simplex_hang_recoveries() == h0
+
+
+@pytest.mark.parametrize("W", [2, 3, 8])
 @pytest.mark.parametrize("n,m,seed,lo,hi", [(300, 1100, 41100, 1, 100), (129, 1513, 77, -100, 100),
                                             (64, 128, 6528, 1, 100)])
 def test_p2p_fused_two_phase(gpu, W, n, m, seed, lo, hi):
