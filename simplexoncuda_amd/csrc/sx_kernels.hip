@@ -1367,8 +1367,11 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
     __shared__ double s_a[SX_TILE], s_b[SX_TILE];
     __shared__ unsigned s_g[4 * SX_TILE];
     __shared__ unsigned s_pay[SX_TILE];
-    __shared__ int s_ok, s_flag, s_win;
-    __shared__ double s_wv;
+    __shared__ int s_ok, s_flag;
+    // per-step results written by wave 0 before the step's one barrier (as in k_batch)
+    __shared__ int s_sel_ok, s_sel_r, s_sel_any, s_det_ok, s_ent_ok, s_ent_e, s_ue_ok;
+    __shared__ double s_ent_v, s_br;
+    __shared__ int s_welig[SX_TILE / 64];
     const int t = threadIdx.x;
     const bool isA = bid < slots;
     const int NAg = W * slots;
@@ -1447,52 +1450,86 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 }
                 s_a[t] = a;
                 s_b[t] = b;
-                const int any = __syncthreads_or(elig);
-                block_argmin512(rv, ri, s_v, s_i);
-                if (t == 0) {
-                    s_win = ri >= 0 ? ri - row0 - bid * SX_TILE : 0;
-                    s_wv = rv;
-                    s_flag = ri;
+                // pass 1: half-wave trees, one block barrier, wave 0 combines and publishes (k_batch)
+                half_argmin(rv, ri);
+                const int anyw = __ballot(elig) != 0ull;
+                if ((t & 31) == 0) {
+                    s_v[t >> 5] = rv;
+                    s_i[t >> 5] = ri;
                 }
+                if ((t & 63) == 0) s_welig[t >> 6] = anyw;
                 __syncthreads();
-                const int wl = s_win;
-                {  // the record (v, pad, a, b, F[winner][s < q]) into every rank's copy, one granule per thread
-                    const unsigned pl = (s_flag >= 0 ? (unsigned)(s_flag - gt * SX_TILE) : SX_NOIDX) |
-                                        ((unsigned)any << 10);
+                if (t < 64) {
+                    double wv = t < 16 ? s_v[t] : DBL_MAX;
+                    int wi = t < 16 ? s_i[t] : -1;
+                    half_argmin(wv, wi);
+                    int any = 0;
+#pragma unroll
+                    for (int w = 0; w < SX_TILE / 64; ++w) any |= s_welig[w];
+                    wi = __builtin_amdgcn_readfirstlane(wi);
+                    const long long vb = __double_as_longlong(wv);
+                    wv = __longlong_as_double(((long long)__builtin_amdgcn_readfirstlane((int)(vb >> 32)) << 32) |
+                                              (long long)(unsigned)__builtin_amdgcn_readfirstlane((int)vb));
+                    const int wl = wi >= 0 ? wi - row0 - bid * SX_TILE : 0;
+                    // the record (v, pad, a, b, F[winner][s < q]) into every rank's copy
+                    const unsigned pl = (wi >= 0 ? (unsigned)(wi - gt * SX_TILE) : SX_NOIDX) | ((unsigned)any << 10);
                     const int nG = 8 + 2 * q;
-                    for (int idx = t; idx < W * nG; idx += SX_TILE) {
+                    for (int idx = t; idx < W * nG; idx += 64) {
                         const int rk = idx / nG, k = idx - rk * nG;
                         if (k == 2 || k == 3) continue;
-                        const double val = k < 2 ? s_wv : k < 6 ? s_a[wl] : k < 8 ? s_b[wl]
-                                                                           : s_hist[((k - 8) >> 1) * SX_TILE + wl];
+                        const double val = k < 2 ? wv : k < 6 ? s_a[wl] : k < 8 ? s_b[wl]
+                                                                        : s_hist[((k - 8) >> 1) * SX_TILE + wl];
                         const unsigned long long bits64 = (unsigned long long)__double_as_longlong(val);
                         put_g_sys(pv.ga[rk] + (size_t)gt * SX_GA_STRIDE + k,
                                   (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64, k < 2 ? (tag | pl) : tag);
                     }
                 }
             }
-            // ---- selection: pass 2 over every rank's ratio tiles
-            if (!gather_tagged<decltype(gather_a), true>(ga, 2 * NAg, gather_a, tag, s_g, &ch->abort_w, &s_ok,
-                                                         timeout, s_pay, gw)) {
-                aborted = true;
-                break;
-            }
-            double tv = DBL_MAX;
-            int ti = -1, te = 0;
-            if (t < NAg) {
-                const double cv = gd(s_g[2 * t], s_g[2 * t + 1]);
-                const unsigned pl = s_pay[t];
-                te = (int)((pl >> 10) & 1u);
-                if (cmp_eps(cv, tv) < 0) {
-                    tv = cv;
-                    ti = (pl & SX_NOIDX) == SX_NOIDX ? -1 : t * SX_TILE + (int)(pl & SX_NOIDX);
+            // ---- selection: pass 2 over every rank's ratio tiles (wave 0 polls and reduces)
+            int r, anyall;
+            if (gw && 2 * NAg <= 64 * SX_GATHER_PER_LANE) {
+                if (t < 64) {
+                    const int ok = poll_wave<decltype(gather_a), true>(ga, 2 * NAg, gather_a, tag, s_g, &ch->abort_w,
+                                                                       timeout, s_pay);
+                    double tv = DBL_MAX;
+                    int ti = -1, any = 0;
+                    if (ok) wave_pass2(s_g, s_pay, NAg, s_v, s_i, tv, ti, any);
+                    if (t == 0) {
+                        s_sel_ok = ok;
+                        s_sel_r = ti;
+                        s_sel_any = any;
+                    }
                 }
+                __syncthreads();
+                if (!s_sel_ok) {
+                    aborted = true;
+                    break;
+                }
+                r = s_sel_r;
+                anyall = s_sel_any;
+            } else {
+                if (!gather_tagged<decltype(gather_a), true>(ga, 2 * NAg, gather_a, tag, s_g, &ch->abort_w, &s_ok,
+                                                             timeout, s_pay, gw)) {
+                    aborted = true;
+                    break;
+                }
+                double tv = DBL_MAX;
+                int ti = -1, te = 0;
+                if (t < NAg) {
+                    const double cv = gd(s_g[2 * t], s_g[2 * t + 1]);
+                    const unsigned pl = s_pay[t];
+                    te = (int)((pl >> 10) & 1u);
+                    if (cmp_eps(cv, tv) < 0) {
+                        tv = cv;
+                        ti = (pl & SX_NOIDX) == SX_NOIDX ? -1 : t * SX_TILE + (int)(pl & SX_NOIDX);
+                    }
+                }
+                anyall = __syncthreads_or(SX_ELIG(te));
+                block_argmin512(tv, ti, s_v, s_i);
+                if (t == 0) s_sel_r = ti;
+                __syncthreads();
+                r = s_sel_r;
             }
-            const int anyall = __syncthreads_or(SX_ELIG(te));
-            block_argmin512(tv, ti, s_v, s_i);
-            if (t == 0) s_win = ti;
-            __syncthreads();
-            const int r = s_win;
             if (!anyall) {  // solver.cu:96-102
                 status = SX_UNBOUNDED;
                 break;
@@ -1508,22 +1545,31 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 const double *src = pv.T[owner] + tl.idx(r - owner * rpr, mj);  // (every rank: the same layout)
                 u = owner == rank ? *src : ld_sys(src);
             }
-            if (!gather_tagged<decltype(ident), true>(ga + (size_t)(r / SX_TILE) * SX_GA_STRIDE + 4, 4 + 2 * q, ident,
-                                                      tag, s_g, &ch->abort_w, &s_ok, timeout)) {
+            // the winner's details (pivot, RHS, factor history), read by wave 0 into LDS
+            if (t < 64) {
+                const int ok = poll_wave<decltype(ident), true>(ga + (size_t)(r / SX_TILE) * SX_GA_STRIDE + 4, 4 + 2 * q,
+                                                                ident, tag, s_g, &ch->abort_w, timeout,
+                                                                (unsigned *)nullptr);
+                if (ok) {
+                    if (t < q) s_fr[t] = gd(s_g[4 + 2 * t], s_g[5 + 2 * t]);
+                    if (t == 0) {
+                        s_p[q] = gd(s_g[0], s_g[1]);
+                        s_br = gd(s_g[2], s_g[3]);
+                        s_r[q] = r;
+                        s_e[q] = e;
+                    }
+                }
+                if (t == 0) s_det_ok = ok;
+            }
+            __syncthreads();
+            if (!s_det_ok) {
                 aborted = true;
                 break;
             }
-            const double p = gd(s_g[0], s_g[1]), br = gd(s_g[2], s_g[3]);
-            if (t < q) s_fr[t] = gd(s_g[4 + 2 * t], s_g[5 + 2 * t]);
-            if (t == 0) {
-                s_p[q] = p;
-                s_r[q] = r;
-                s_e[q] = e;
-            }
+            const double p = s_p[q], br = s_br;
             cnt = q + 1;
             last_r = r;
             last_e = e;
-            __syncthreads();
             if (isA) {
                 const double f = -a / p;
                 s_hist[q * SX_TILE + t] = f;
@@ -1580,59 +1626,92 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                         i = ia;
                     }
                 }
-                block_argmin512(v, i, s_v, s_i);
-                if (t == 0) {
-                    s_win = i >= 0 ? i - tb * SX_TILE : 0;
-                    s_wv = v;
-                    s_flag = i;
+                half_argmin(v, i);
+                if ((t & 31) == 0) {
+                    s_v[t >> 5] = v;
+                    s_i[t >> 5] = i;
                 }
                 __syncthreads();
-                {  // the record (v, pad, U[s <= q][winner]) into every rank's copy, one granule per thread
-                    const unsigned pl = s_flag >= 0 ? (unsigned)(s_flag - tb * SX_TILE) : SX_NOIDX;
+                if (t < 64) {  // wave 0 combines the half winners and publishes (k_batch)
+                    double wv = t < 16 ? s_v[t] : DBL_MAX;
+                    int wi = t < 16 ? s_i[t] : -1;
+                    half_argmin(wv, wi);
+                    wi = __builtin_amdgcn_readfirstlane(wi);
+                    const long long vb = __double_as_longlong(wv);
+                    wv = __longlong_as_double(((long long)__builtin_amdgcn_readfirstlane((int)(vb >> 32)) << 32) |
+                                              (long long)(unsigned)__builtin_amdgcn_readfirstlane((int)vb));
+                    const int win = wi >= 0 ? wi - tb * SX_TILE : 0;
+                    // the record (v, pad, U[s <= q][winner]) into every rank's copy
+                    const unsigned pl = wi >= 0 ? (unsigned)win : SX_NOIDX;
                     const int nG = 4 + 2 * (q + 1);
-                    for (int idx = t; idx < W * nG; idx += SX_TILE) {
+                    for (int idx = t; idx < W * nG; idx += 64) {
                         const int rk = idx / nG, k = idx - rk * nG;
                         if (k == 2 || k == 3) continue;
-                        const double val = k < 2 ? s_wv : s_hist[((k - 4) >> 1) * SX_TILE + s_win];
+                        const double val = k < 2 ? wv : s_hist[((k - 4) >> 1) * SX_TILE + win];
                         const unsigned long long bits64 = (unsigned long long)__double_as_longlong(val);
                         put_g_sys(pv.gb[rk] + (size_t)tb * SX_GB_STRIDE + k,
                                   (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64, k < 2 ? (tag | pl) : tag);
                     }
                 }
             }
-            // ---- entering variable of pivot q + 1: pass 2 over every objective tile
-            if (!gather_tagged<decltype(gather_b), true>(gb, 2 * NBg, gather_b, tag, s_g, &ch->abort_w, &s_ok,
-                                                         timeout, s_pay, gw)) {
-                aborted = true;
-                break;
-            }
-            double ev = DBL_MAX;
-            int ei = -1;
-            if (t < NBg) {
-                const double cv = gd(s_g[2 * t], s_g[2 * t + 1]);
-                const unsigned pl = s_pay[t] & SX_NOIDX;
-                if (cmp_eps(cv, ev) < 0) {
-                    ev = cv;
-                    ei = pl == SX_NOIDX ? -1 : t * SX_TILE + (int)pl;
+            // ---- entering variable of pivot q + 1: pass 2 over every objective tile (wave 0)
+            if (gw && 2 * NBg <= 64 * SX_GATHER_PER_LANE) {
+                if (t < 64) {
+                    const int ok = poll_wave<decltype(gather_b), true>(gb, 2 * NBg, gather_b, tag, s_g, &ch->abort_w,
+                                                                       timeout, s_pay);
+                    double ev = DBL_MAX;
+                    int ei = -1, any = 0;
+                    if (ok) wave_pass2(s_g, s_pay, NBg, s_v, s_i, ev, ei, any);
+                    if (t == 0) {
+                        s_ent_ok = ok;
+                        s_ent_e = ei;
+                        s_ent_v = ev;
+                    }
                 }
-            }
-            block_argmin512(ev, ei, s_v, s_i);
-            if (t == 0) {
-                s_win = ei;
-                s_wv = ev;
-            }
-            __syncthreads();
-            e = s_win;
-            dmin = s_wv;
-            if (liveA) a_pre = T[tl.idx(li, c.map(1 + (e >= 0 ? e : 0)))];
-            if (isA && q + 1 < K && e >= 0 && cmp_eps(dmin, 0.0) < 0) {
-                if (!gather_tagged<decltype(ident), true>(gb + (size_t)(e / SX_TILE) * SX_GB_STRIDE + 4, 2 * (q + 1),
-                                                          ident, tag, s_g, &ch->abort_w, &s_ok, timeout)) {
+                __syncthreads();
+                if (!s_ent_ok) {
                     aborted = true;
                     break;
                 }
-                if (t <= q) s_ue[t] = gd(s_g[2 * t], s_g[2 * t + 1]);
+            } else {
+                if (!gather_tagged<decltype(gather_b), true>(gb, 2 * NBg, gather_b, tag, s_g, &ch->abort_w, &s_ok,
+                                                             timeout, s_pay, gw)) {
+                    aborted = true;
+                    break;
+                }
+                double ev = DBL_MAX;
+                int ei = -1;
+                if (t < NBg) {
+                    const double cv = gd(s_g[2 * t], s_g[2 * t + 1]);
+                    const unsigned pl = s_pay[t] & SX_NOIDX;
+                    if (cmp_eps(cv, ev) < 0) {
+                        ev = cv;
+                        ei = pl == SX_NOIDX ? -1 : t * SX_TILE + (int)pl;
+                    }
+                }
+                block_argmin512(ev, ei, s_v, s_i);
+                if (t == 0) {
+                    s_ent_e = ei;
+                    s_ent_v = ev;
+                }
                 __syncthreads();
+            }
+            e = s_ent_e;
+            dmin = s_ent_v;
+            if (liveA) a_pre = T[tl.idx(li, c.map(1 + (e >= 0 ? e : 0)))];
+            if (isA && q + 1 < K && e >= 0 && cmp_eps(dmin, 0.0) < 0) {
+                if (t < 64) {  // (wave 0 reads them into LDS)
+                    const int ok = poll_wave<decltype(ident), true>(gb + (size_t)(e / SX_TILE) * SX_GB_STRIDE + 4,
+                                                                    2 * (q + 1), ident, tag, s_g, &ch->abort_w, timeout,
+                                                                    (unsigned *)nullptr);
+                    if (ok && t <= q) s_ue[t] = gd(s_g[2 * t], s_g[2 * t + 1]);
+                    if (t == 0) s_ue_ok = ok;
+                }
+                __syncthreads();
+                if (!s_ue_ok) {
+                    aborted = true;
+                    break;
+                }
             }
         }
     }

@@ -1,6 +1,8 @@
 """Pivot rate of the multi-rank paths on ONE GPU (diagnostic): virtual shards with the per-pivot
 exchange vs the peer-memory fused batch, and the fused multi-rank kernel at W = 1 (force).
 
+Virtual shards share the one GPU (every shard's sweep runs on it), so the W > 1 rates show the
+hand-off costs, not a multi-GPU speed-up.
 usage: python tools/p2p_probe.py [config] [pivots]"""
 import os
 import sys
@@ -33,7 +35,7 @@ def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "config3"
     k = int(sys.argv[2]) if len(sys.argv) > 2 else 640
     n, m, seed = bench.CONFIGS[cfg]
-    for W, p2p, force in [(1, -1, 0), (1, 1, 1), (2, 0, 0), (2, 1, 0), (3, 0, 0), (3, 1, 0)]:
+    for W, p2p, force in [(1, -1, 0), (1, 1, 1), (2, 0, 0), (2, 1, 0), (3, 1, 0), (4, 1, 0), (8, 1, 0)]:
         t = run(sx, n, m, seed, k, W, p2p, force)
         print(f"{cfg} W={W} p2p={p2p} force_exchange={force}: {t.pivots / t.wall_ms * 1e3:9.1f} pivots/s "
               f"({t.wall_ms * 1e3 / max(t.pivots, 1):7.2f} us/pivot, sweep {t.update_ms * 1e3 / max(t.update_launches, 1):8.1f} us)"
