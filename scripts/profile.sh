@@ -6,7 +6,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+OUT=${PROF_OUT:-gpurun_out/prof}
 mkdir -p $OUT
 ARGS=${PROF_ARGS:---gpus 1 --steps 20 --warmup 5}
 echo "== kernel trace: bench.py $ARGS ($(date +%T))"
