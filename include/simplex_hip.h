@@ -86,6 +86,9 @@ void simplex_set_sweep_stages(int d);
 /* fused batches: pause between two polls of a hand-off, s_sleep 0/1/2/4/8/16 for k = 0..5
  * (default 1; diagnostic) */
 void simplex_set_poll_sleep(int k);
+/* fused batches: the pending-pivot chains of a ratio row / the pivot row run branch-free when no
+ * slot of the wave divides (1, default) or every slot through the guarded chain (0; A/B knob) */
+void simplex_set_hist_fast(int on);
 /* new engines' tableau layout: plain row-major rows (0), the two-region layout when aliasing and
  * m > 4096 (1, default), or region A forced to hold `mode` slack positions (>= 2,
  * test hook) */

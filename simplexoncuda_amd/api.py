@@ -356,6 +356,12 @@ def set_sweep_stages(d):
     _lib.load().simplex_set_sweep_stages(int(d))
 
 
+def set_hist_fast(on):
+    """Fused batches: branch-free pending-pivot chains when no slot of a wave divides (1,
+    default) or the guarded chain for every slot (0; A/B knob)."""
+    _lib.load().simplex_set_hist_fast(1 if on else 0)
+
+
 def set_verbose(on):
     _lib.load().simplex_set_verbose(1 if on else 0)
 

@@ -904,6 +904,102 @@ __host__ __device__ __forceinline__ size_t sx_ga_size() { return (size_t)SX_TILE
 __host__ __device__ __forceinline__ size_t sx_gb_size() { return (size_t)SX_TILE * SX_GB_STRIDE; }
 __device__ __forceinline__ int rec2_b(int k) { return (k >> 1) * SX_GB_STRIDE + (k & 1); }
 
+// branch-free history chains in the fused batch when no slot needs a division (1, default);
+// 0 runs every slot through the guarded chain (A/B knob, simplex_set_hist_fast)
+__constant__ int c_hist_fast = 1;
+
+// The batch's pending pivots s < q applied, in slot order, to a ratio row's entering-column
+// entry `a` (solver.cu:34-46 on that element): a / p_s at the slots in `bits` (the row itself
+// left the basis there), fma(F[row][s], U[s][e], a) at the others.  A wave none of whose rows
+// left the basis in this batch -- nearly always -- runs the plain fma chain: no per-slot
+// exec-mask branch, LDS reads batched 8 slots at a time (the guarded chain cost ~25
+// instructions per slot).
+__device__ __forceinline__ double hist_col(double a, int q, unsigned bits, const double *s_hist, const double *s_ue,
+                                           const double *s_p) {
+    const int t = threadIdx.x;
+    if (c_hist_fast && __ballot(bits != 0u) == 0ull) {
+        int s = 0;
+        for (; s + 8 <= q; s += 8) {
+            double h[8], ue[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                h[k] = s_hist[(s + k) * SX_TILE + t];
+                ue[k] = s_ue[s + k];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a = fma(h[k], ue[k], a);
+        }
+        for (; s < q; ++s) a = fma(s_hist[s * SX_TILE + t], s_ue[s], a);
+        return a;
+    }
+    for (int s0 = 0; s0 < q; s0 += 8) {  // (slots past q read slot s0 and are not used)
+        double h[8], ue[8], pp[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int s = s0 + k < q ? s0 + k : s0;
+            h[k] = s_hist[s * SX_TILE + t];
+            ue[k] = s_ue[s];
+            pp[k] = s_p[s];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (s0 + k < q) {
+                if ((bits >> (s0 + k)) & 1u)
+                    a = a / pp[k];
+                else
+                    a = fma(h[k], ue[k], a);
+            }
+        }
+    }
+    return a;
+}
+
+// The same for the pivot row's entry `u` on an objective tile's column: u / p_s at the slots
+// where the leaving row r itself left before (s_r[s] == r), else fma(F[r][s], U[s][j], u).
+// The slots where r left are wave-uniform (one ballot); when there are none the chain is
+// branch-free.
+__device__ __forceinline__ double hist_row(double u, int q, int r, const double *s_hist, const double *s_fr,
+                                           const double *s_p, const int *s_r) {
+    const int t = threadIdx.x, lane = t & 63;
+    if (c_hist_fast && __ballot(lane < q && s_r[lane < q ? lane : 0] == r) == 0ull) {
+        int s = 0;
+        for (; s + 8 <= q; s += 8) {
+            double h[8], fr[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                h[k] = s_hist[(s + k) * SX_TILE + t];
+                fr[k] = s_fr[s + k];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) u = fma(fr[k], h[k], u);
+        }
+        for (; s < q; ++s) u = fma(s_fr[s], s_hist[s * SX_TILE + t], u);
+        return u;
+    }
+    for (int s0 = 0; s0 < q; s0 += 8) {
+        double h[8], fr[8], pp[8];
+        int rr[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int s = s0 + k < q ? s0 + k : s0;
+            h[k] = s_hist[s * SX_TILE + t];
+            fr[k] = s_fr[s];
+            pp[k] = s_p[s];
+            rr[k] = s_r[s];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (s0 + k < q) {
+                if (rr[k] == r)
+                    u = u / pp[k];
+                else
+                    u = fma(fr[k], h[k], u);
+            }
+        }
+    }
+    return u;
+}
+
 __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int rows, size_t ld, TLay tl, Cols c,
                                                double *__restrict__ d, double *__restrict__ d_save, int *base,
                                                DevState *st, double *U, double *F, PivRec *recs,
@@ -980,28 +1076,8 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
             if (isA) {
                 // ---- ratio tile: current entering column, ratios, tile winner
                 if (blockIdx.x == 0) SX_STAMP(0);
-                a = a_pre;
-                // pending pivots of the batch, in order; LDS reads batched 8 slots at a time
-                // (slots past q read slot s0 and are not used)
-                for (int s0 = 0; s0 < q; s0 += 8) {
-                    double h[8], ue[8], pp[8];
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const int s = s0 + k < q ? s0 + k : s0;
-                        h[k] = s_hist[s * SX_TILE + t];
-                        ue[k] = s_ue[s];
-                        pp[k] = s_p[s];
-                    }
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        if (s0 + k < q) {
-                            if ((bits >> (s0 + k)) & 1u)
-                                a = a / pp[k];
-                            else
-                                a = fma(h[k], ue[k], a);
-                        }
-                    }
-                }
+                // pending pivots of the batch, in order
+                a = hist_col(a_pre, q, bits, s_hist, s_ue, s_p);
                 double rv = DBL_MAX;
                 int ri = -1, elig = 0;
                 if (liveA) {
@@ -1158,27 +1234,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
             } else {
                 // ---- objective tile: current pivot row on this column, d, tile winner
                 if (tb == 0) SX_STAMP(6);
-                for (int s0 = 0; s0 < q; s0 += 8) {  // (LDS reads batched as in the ratio tiles)
-                    double h[8], fr[8], pp[8];
-                    int rr[8];
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const int s = s0 + k < q ? s0 + k : s0;
-                        h[k] = s_hist[s * SX_TILE + t];
-                        fr[k] = s_fr[s];
-                        pp[k] = s_p[s];
-                        rr[k] = s_r[s];
-                    }
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        if (s0 + k < q) {
-                            if (rr[k] == r)
-                                u = u / pp[k];
-                            else
-                                u = fma(fr[k], h[k], u);
-                        }
-                    }
-                }
+                u = hist_row(u, q, r, s_hist, s_fr, s_p, s_r);
                 s_hist[q * SX_TILE + t] = u;
                 if (tb == 0) SX_STAMP(7);
                 if (liveB && 1 + ia < c.Ns) U[(size_t)q * ld + mj] = u;
@@ -1416,28 +1472,8 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
             }
             double a = 0.0;
             if (isA) {
-                a = a_pre;
-                // pending pivots of the batch, in order; LDS reads batched 8 slots at a time
-                // (slots past q read slot s0 and are not used)
-                for (int s0 = 0; s0 < q; s0 += 8) {
-                    double h[8], ue[8], pp[8];
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const int s = s0 + k < q ? s0 + k : s0;
-                        h[k] = s_hist[s * SX_TILE + t];
-                        ue[k] = s_ue[s];
-                        pp[k] = s_p[s];
-                    }
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        if (s0 + k < q) {
-                            if ((bits >> (s0 + k)) & 1u)
-                                a = a / pp[k];
-                            else
-                                a = fma(h[k], ue[k], a);
-                        }
-                    }
-                }
+                // pending pivots of the batch, in order
+                a = hist_col(a_pre, q, bits, s_hist, s_ue, s_p);
                 double rv = DBL_MAX;
                 int ri = -1, elig = 0;
                 if (liveA) {
@@ -1591,27 +1627,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                     U[(size_t)q * ld] = br;
                 }
             } else {
-                for (int s0 = 0; s0 < q; s0 += 8) {  // (LDS reads batched as in the ratio tiles)
-                    double h[8], fr[8], pp[8];
-                    int rr[8];
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const int s = s0 + k < q ? s0 + k : s0;
-                        h[k] = s_hist[s * SX_TILE + t];
-                        fr[k] = s_fr[s];
-                        pp[k] = s_p[s];
-                        rr[k] = s_r[s];
-                    }
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        if (s0 + k < q) {
-                            if (rr[k] == r)
-                                u = u / pp[k];
-                            else
-                                u = fma(fr[k], h[k], u);
-                        }
-                    }
-                }
+                u = hist_row(u, q, r, s_hist, s_fr, s_p, s_r);
                 s_hist[q * SX_TILE + t] = u;
                 if (liveB && 1 + ia < c.Ns)
                     for (int k = 0; k < W; ++k) st_sys(pv.U[k] + (size_t)q * ld + mj, u);
@@ -2456,6 +2472,10 @@ void sx_set_gather_wide(int on) { g_gather_wide = on ? 1 : 0; }
 void sx_set_poll_sleep(int k) {
     const int v = k < 0 ? 1 : k;
     SX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_poll_sleep), &v, sizeof(int)));
+}
+void sx_set_hist_fast(int on) {
+    const int v = on ? 1 : 0;
+    SX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_hist_fast), &v, sizeof(int)));
 }
 static int g_record_replicas = 1;
 void sx_set_record_replicas(int n) { g_record_replicas = n < 1 ? 1 : n > SX_GREP ? SX_GREP : n; }

@@ -209,7 +209,7 @@ def _pivots_with(cfg, T, d, base, k):
     setters = {"batch": (sx.set_batch, 0), "rb": (sx.set_update_rows, 0), "sc1": (sx.set_store_sc1, -1),
                "fused": (sx.set_fused, -1), "p2p": (sx.set_p2p, -1),
                "waves": (sx.set_update_waves, 0), "W": (sx.set_virtual_ranks, 1),
-               "stages": (sx.set_sweep_stages, 0)}
+               "stages": (sx.set_sweep_stages, 0), "hist": (sx.set_hist_fast, 1)}
     try:
         for key, val in cfg.items():
             setters[key][0](val)
@@ -341,6 +341,27 @@ def test_same_row_leaves_twice_in_a_batch(gpu, batch, fused):
     st_o, done_o = oracle.solve(*ref)
     Tg, dg, bg, st, done = _pivots_with({"batch": batch, "fused": fused}, T, d, base, 100000)
     assert st == st_o and done == done_o
+    assert same(Tg, ref[0]) and same(dg, ref[1]) and np.array_equal(bg, ref[2])
+
+
+@pytest.mark.parametrize("hist", [0, 1])
+@pytest.mark.parametrize("W", [1, 2])
+@pytest.mark.parametrize("case", [(20, 10, 2010, 100000), (333, 1025, 7, 70), (64, 128, 6528, 100000),
+                                  (300, 1100, 11, 150)])
+def test_fused_history_chains(gpu, hist, W, case):
+    """the fused batch's pending-pivot chains (ratio rows, pivot row): branch-free when no slot
+    of a wave divides, guarded otherwise -- both forms and the guarded form alone, one shard and
+    two peer-memory shards; the first instance's leaving rows repeat inside a batch (7, 6, 1, 7,
+    7, 7, ...), so waves of both kinds meet in one batch"""
+    n, m, seed, k = case
+    if W > 1 and m <= 512:
+        pytest.skip("one 512-row shard")
+    T, d, base = _phase1_state(n, m, seed)
+    ref = (T.copy(), d.copy(), base.copy())
+    st_o, done_o = oracle.solve(*ref, max_pivots=k)
+    Tg, dg, bg, st, done = _pivots_with({"batch": 32, "hist": hist, "W": W, "p2p": 1 if W > 1 else -1},
+                                        T, d, base, k)
+    assert done == done_o
     assert same(Tg, ref[0]) and same(dg, ref[1]) and np.array_equal(bg, ref[2])
 
 

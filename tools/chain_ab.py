@@ -50,8 +50,9 @@ def main():
 
     setter = {"gather_wide": lib.simplex_set_gather_wide, "ld_pad": lib.simplex_set_ld_pad,
               "replicas": lib.simplex_set_record_replicas, "sweep": set_sweep,
-              "sleep": lib.simplex_set_poll_sleep, "regions": lib.simplex_set_regions}[name]
-    reset = {"gather_wide": 1, "ld_pad": 0, "replicas": 1, "sweep": "0:0", "sleep": 1, "regions": 1}[name]
+              "sleep": lib.simplex_set_poll_sleep, "regions": lib.simplex_set_regions,
+              "hist_fast": lib.simplex_set_hist_fast}[name]
+    reset = {"gather_wide": 1, "ld_pad": 0, "replicas": 1, "sweep": "0:0", "sleep": 1, "regions": 1, "hist_fast": 1}[name]
     print("stamps (us): ratio compute | ratio argmin+publish | -> selection seen | pass2 + row details |"
           " row compute | obj argmin+publish | -> entering seen | entering history | pivot")
     for r in range(rounds):
