@@ -89,6 +89,8 @@ void simplex_set_poll_sleep(int k);
 /* fused batches: the pending-pivot chains of a ratio row / the pivot row run branch-free when no
  * slot of the wave divides (1, default) or every slot through the guarded chain (0; A/B knob) */
 void simplex_set_hist_fast(int on);
+/* full 32-slot sweeps: one column per thread (1; k_sweep1, A/B variant) or two (2, default) */
+void simplex_set_sweep_cols(int c);
 /* new engines' tableau layout: plain row-major rows (0), the two-region layout when aliasing and
  * m > 4096 (1, default), or region A forced to hold `mode` slack positions (>= 2,
  * test hook) */

@@ -362,6 +362,11 @@ def set_hist_fast(on):
     _lib.load().simplex_set_hist_fast(1 if on else 0)
 
 
+def set_sweep_cols(c):
+    """Full 32-slot sweeps with one column per thread (1; k_sweep1) or two (2, default)."""
+    _lib.load().simplex_set_sweep_cols(int(c))
+
+
 def set_verbose(on):
     _lib.load().simplex_set_verbose(1 if on else 0)
 

@@ -1317,6 +1317,7 @@ void simplex_set_record_replicas(int n) { sx_set_record_replicas(n); }
 void simplex_set_sweep_stages(int d) { sx_set_sweep_stages(d); }
 void simplex_set_poll_sleep(int k) { sx_set_poll_sleep(k); }
 void simplex_set_hist_fast(int on) { sx_set_hist_fast(on); }
+void simplex_set_sweep_cols(int c) { sx_set_sweep_cols(c); }
 void simplex_set_uncached_exchange(int on) { g_cfg.uncached_xchg = on ? 1 : 0; }
 void simplex_set_ld_pad(int doubles) { g_cfg.ld_pad = doubles > 0 ? (int)round_up((size_t)doubles, 16) : 0; }
 void simplex_set_exchange_mode(int mode) { g_cfg.exchange_mode = (mode >= 0 && mode <= 2) ? mode : 0; }

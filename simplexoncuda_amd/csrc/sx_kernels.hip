@@ -1932,6 +1932,83 @@ __global__ __launch_bounds__(256) void k_sweep(double *__restrict__ T, int rows,
     }
 }
 
+// k_sweep with ONE column per thread (simplex_set_sweep_cols(1); A/B variant): a column's KT
+// pivot-row values take KT VGPRs instead of 2 KT, so about twice as many waves are resident
+// and RB = 8 rows per step keep the same 4 KB in flight per wave; a wave moves 512 B per row
+// in 8-byte lanes.  256-column tiles (jB is a multiple of 512: a tile lies in one region).
+// Same operations, same order as k_sweep.
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+template <int KT, int RB, bool SC1>
+__global__ __launch_bounds__(256) void k_sweep1(double *__restrict__ T, int rows, size_t ld, TLay tl, int Ns,
+                                                const int *__restrict__ nact, int s0,
+                                                const double *__restrict__ F, const double *__restrict__ U,
+                                                const PivRec *__restrict__ recs,
+                                                const unsigned long long *__restrict__ PM,
+                                                const DevState *__restrict__ st, unsigned B, int rev) {
+    const int cnt = st->batch_tag == B ? st->batch_count : 0;
+    if (cnt <= 0) return;
+    if (nact && s0 + *nact < Ns) Ns = s0 + *nact;
+    const int cb = (Ns + 255) / 256;
+    const int lin = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    const int G = (int)(gridDim.x * gridDim.y) / cb;
+    const int tile = lin % cb, gy = lin / cb;
+    if (gy >= G) return;
+    const int bx = rev ? cb - 1 - tile : tile;
+    const int j = bx * 256 + (int)threadIdx.x;
+    if (j >= Ns) return;
+    const bool inB = bx * 256 >= tl.jB;
+    double *const Tr = inB ? T + tl.offB : T;
+    const size_t ldr = inB ? tl.ldB : tl.ldA;
+    const int jr = inB ? j - tl.jB : j;
+    const unsigned mask = slot_mask(cnt);
+    double u[KT];
+#pragma unroll
+    for (int s = 0; s < KT; ++s) u[s] = s < cnt ? U[(size_t)s * ld + j] : 0.0;
+    const int ng = (rows + RB - 1) / RB;
+    const int oob = (int)(ldr * 8);
+    for (int g = gy; g < ng; g += G) {
+        const int i0 = (rev ? ng - 1 - g : g) * RB;
+        double x[RB];
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+            const int i = i0 + k < rows ? i0 + k : i0;
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(Tr + (size_t)i * ldr, 0, oob, 0x00020000);
+            x[k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, i0 + k < rows ? jr * 8 : oob,
+                                                                                    0, 2));
+        }
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+            const int i = i0 + k;
+            if (i >= rows) break;
+            const double *Fr = F + (size_t)i * SX_KMAX;
+            double f[KT];
+#pragma unroll
+            for (int s = 0; s < KT; ++s) f[s] = Fr[s];
+            const unsigned bits = pend_bits(PM, i, B, mask);
+            double y = x[k];
+            if (bits == 0u && cnt == KT) {
+#pragma unroll
+                for (int s = 0; s < KT; ++s) y = fma(f[s], u[s], y);
+            } else {
+#pragma unroll
+                for (int s = 0; s < KT; ++s) {
+                    if (s < cnt) {
+                        if ((bits >> s) & 1u)
+                            y = y / recs[s].p;
+                        else
+                            y = fma(f[s], u[s], y);
+                    }
+                }
+            }
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(Tr + (size_t)i * ldr, 0, oob, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y), rs, jr * 8, 0, SC1 ? 16 : 0);
+        }
+    }
+}
+
 // One row of the sweep (the arithmetic of k_sweep above, shared by the staged variant).
 template <int KT>
 __device__ __forceinline__ double2 sweep_row(double2 y, const double2 (&u)[KT], const double *__restrict__ F,
@@ -2398,6 +2475,19 @@ static void launch_sweep_t(double *T, int rows, size_t ld, TLay tl, int Ns, cons
                                               rev);
 }
 
+// one column per thread (k_sweep1) for full 32-slot sweeps (1), or two (k_sweep, 2: default)
+static int g_sweep_cols = 2;
+void sx_set_sweep_cols(int c) { g_sweep_cols = c == 1 ? 1 : 2; }
+
+template <int KT, int RB, bool SC1>
+static void launch_sweep1_t(double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0, const Pending &pd,
+                            const DevState *st, int rev, hipStream_t s) {
+    const int cb = (Ns + 255) / 256;
+    dim3 grid(cb, row_slots(sweep_capacity(k_sweep1<KT, RB, SC1>), cb, rows, RB));
+    k_sweep1<KT, RB, SC1><<<grid, 256, 0, s>>>(T, rows, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st, pd.batch,
+                                               rev);
+}
+
 template <int KT>
 static void launch_sweep_k(int rb, bool sc1, double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0,
                            const Pending &pd, const DevState *st, int rev, hipStream_t s) {
@@ -2451,6 +2541,15 @@ void sx_launch_sweep(double *T, int rows, size_t ld, TLay tl, int Ns, const int 
     if (g_sweep_stages > 0 && k > 16 && k <= SX_KMAX && cfg.sc1 &&
         launch_sweep_lds(cfg.rows_per_block, g_sweep_stages, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s))
         return;
+    if (g_sweep_cols == 1 && k > 16 && k <= SX_KMAX) {
+        if (cfg.rows_per_block == 2)
+            cfg.sc1 ? launch_sweep1_t<SX_KMAX, 4, true>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s)
+                    : launch_sweep1_t<SX_KMAX, 4, false>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+        else
+            cfg.sc1 ? launch_sweep1_t<SX_KMAX, 8, true>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s)
+                    : launch_sweep1_t<SX_KMAX, 8, false>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+        return;
+    }
     if (k <= 1)
         launch_sweep_k<1>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else if (k <= 4)

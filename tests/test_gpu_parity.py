@@ -209,7 +209,8 @@ def _pivots_with(cfg, T, d, base, k):
     setters = {"batch": (sx.set_batch, 0), "rb": (sx.set_update_rows, 0), "sc1": (sx.set_store_sc1, -1),
                "fused": (sx.set_fused, -1), "p2p": (sx.set_p2p, -1),
                "waves": (sx.set_update_waves, 0), "W": (sx.set_virtual_ranks, 1),
-               "stages": (sx.set_sweep_stages, 0), "hist": (sx.set_hist_fast, 1)}
+               "stages": (sx.set_sweep_stages, 0), "hist": (sx.set_hist_fast, 1),
+               "cols": (sx.set_sweep_cols, 2)}
     try:
         for key, val in cfg.items():
             setters[key][0](val)
@@ -565,6 +566,44 @@ def test_two_region_two_phase(gpu, n, m, seed, lo, hi, W, p2p):
         sx.set_p2p(-1)
         sx.set_virtual_ranks(1)
         sx.set_regions(1)
+
+
+@pytest.mark.parametrize("batch", [20, 32])
+@pytest.mark.parametrize("rb", [2, 4])
+@pytest.mark.parametrize("sc1", [0, 1])
+def test_sweep_one_column_per_thread_bit_exact(gpu, batch, rb, sc1):
+    """k_sweep1 (one column per thread, 4 or 8 rows per step): full 32-slot sweeps and a partial
+    last batch, both store flavours"""
+    T, d, base = _phase1_state(333, 1025, 7)
+    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "rb": rb, "sc1": sc1, "cols": 1}, T, d, base, 70)
+    oracle.solve(T, d, base, max_pivots=70)
+    assert done == 70
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+@pytest.mark.parametrize("cap", [16, 300])
+@pytest.mark.parametrize("n,m,k,W,p2p", [(300, 1100, 200, 1, -1), (64, 700, 400, 1, -1), (200, 1500, 150, 2, 1)])
+def test_sweep_one_column_two_region(gpu, n, m, k, W, p2p, cap):
+    """k_sweep1 on the two-region layout with a small region A (sweeps cross into region B),
+    one shard and two peer-memory shards"""
+    p = sx.generateRandomProblem(n, m, n * 100 + m, 1, 100)
+    try:
+        sx.set_sweep_cols(1)
+        sx.set_regions(cap)
+        sx.set_p2p(p2p)
+        sx.set_virtual_ranks(W)
+        s = sx.Session(problem=p)
+        t = s.pivots(k)
+        Tg, dg, bg = s.tableau(m, 1 + n + 2 * m)
+        s.close()
+    finally:
+        sx.set_virtual_ranks(1)
+        sx.set_p2p(-1)
+        sx.set_regions(1)
+        sx.set_sweep_cols(2)
+    T, d, base, done = _oracle_after(p, k)
+    assert t.pivots == done
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 
 def test_slack_compaction_off_for_negated_rows(gpu):

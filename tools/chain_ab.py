@@ -7,7 +7,8 @@ usage: python tools/chain_ab.py <setting>=<v1>,<v2> [config=config5,config3] [ro
             replicas (simplex_set_record_replicas), sleep (simplex_set_poll_sleep),
             regions (simplex_set_regions: 0 plain rows, 1 two-region layout),
             sweep (rows per step:LDS stages, simplex_set_update_rows + simplex_set_sweep_stages;
-                   e.g. sweep=4:0,4:3,1:8 -- stages 0 = the register sweep)"""
+                   [:columns per thread, simplex_set_sweep_cols]; e.g. sweep=4:0,4:3,1:8,4:0:1 --
+                   stages 0 = the register sweep)"""
 import os
 import sys
 
@@ -44,9 +45,10 @@ def main():
     rounds = int(args.pop("rounds", "2"))
     (name, vals), = args.items()
     def set_sweep(v):
-        rb, d = (int(x) for x in str(v).split(":"))
-        lib.simplex_set_update_rows(rb)
-        lib.simplex_set_sweep_stages(d)
+        f = [int(x) for x in str(v).split(":")]
+        lib.simplex_set_update_rows(f[0])
+        lib.simplex_set_sweep_stages(f[1])
+        lib.simplex_set_sweep_cols(f[2] if len(f) > 2 else 2)
 
     setter = {"gather_wide": lib.simplex_set_gather_wide, "ld_pad": lib.simplex_set_ld_pad,
               "replicas": lib.simplex_set_record_replicas, "sweep": set_sweep,
