@@ -894,7 +894,8 @@ class Engine {
 
     // apply the batch's pivots to the tableau (a no-op kernel when none was selected) and
     // start a new batch
-    void enqueue_sweep(hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
+    // rec_shard0: the sweep record target (sx_set_sweep_record) is meant for shard 0's sweep
+    void enqueue_sweep(hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, bool rec_shard0 = false) {
         if (q_host == 0) return;
         const SweepCfg cfg = sweep_cfg(q_host);
         const int rev = (int)(sweeps & 1);  // alternate the sweep direction (Infinity-Cache reuse)
@@ -905,9 +906,12 @@ class Engine {
                 sx_launch_activate(x.perm, x.iperm, x.act, x.nact, m, x.T, x.rows, x.row0, ld, tl, 1 + n, pending(x), x.st,
                                    s);
         if (ev0) SX_HIP(hipEventRecord(ev0, s));
-        for (auto &x : sh)
+        for (auto &x : sh) {
             sx_launch_sweep(x.T, x.rows, ld, tl, cols(N).Ns, compact ? x.nact : nullptr, 1 + n, pending(x), x.st, rev, cfg,
                             s);
+            if (rec_shard0) sx_set_sweep_record(nullptr);  // (only shard 0's sweep records)
+        }
+        if (rec_shard0) sx_set_sweep_record(nullptr);
         if (ev1) SX_HIP(hipEventRecord(ev1, s));
         ++sweeps;
         q_host = 0;
@@ -1540,14 +1544,13 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
     auto sweep = [&]() {
         const bool timed = every && (nsw % every == 0) && ntimed < nt;
         const unsigned id = E.batch_id;
-        E.enqueue_sweep(timed ? evs[2 * ntimed] : nullptr, timed ? evs[2 * ntimed + 1] : nullptr);
+        // a timed sweep of shard 0 records its batch tag, count and swept slack columns itself
+        // (sx_set_sweep_record: no device copies between the kernels of the timed region)
+        if (timed) sx_set_sweep_record(tag_dev + 3 * ntimed);
+        E.enqueue_sweep(timed ? evs[2 * ntimed] : nullptr, timed ? evs[2 * ntimed + 1] : nullptr, timed);
+        sx_set_sweep_record(nullptr);
         if (timed) {
             ids[(size_t)ntimed] = id;
-            SX_HIP(hipMemcpyAsync(tag_dev + 3 * ntimed, &E.sh[0].st->batch_tag, 2 * sizeof(int),
-                                  hipMemcpyDeviceToDevice, E.s));
-            if (E.compact)
-                SX_HIP(hipMemcpyAsync(tag_dev + 3 * ntimed + 2, E.sh[0].nact, sizeof(int), hipMemcpyDeviceToDevice,
-                                      E.s));
             ++ntimed;
         }
         ++nsw;

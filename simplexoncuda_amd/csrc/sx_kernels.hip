@@ -1834,13 +1834,26 @@ __global__ __launch_bounds__(512) void k_batch_mr_multi(MrRanks R, int rpr, size
 // of the phase is still materialised.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// (batch tag, batch count, swept slack columns) of this sweep into rec[0..2] (bench sessions'
+// timed sweeps; null otherwise) -- written by the sweep itself instead of two device copies
+// between kernels (two dispatches, ~9 us per batch)
+__device__ __forceinline__ void sweep_record(int *rec, const DevState *st, const int *nact) {
+    if (rec && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+        rec[0] = (int)st->batch_tag;
+        rec[1] = st->batch_count;
+        if (nact) rec[2] = *nact;
+    }
+}
+
 template <int KT, int RB, bool SC1>
 __global__ __launch_bounds__(256) void k_sweep(double *__restrict__ T, int rows, size_t ld, TLay tl, int Ns,
                                                const int *__restrict__ nact, int s0,
                                                const double *__restrict__ F, const double *__restrict__ U,
                                                const PivRec *__restrict__ recs,
                                                const unsigned long long *__restrict__ PM,
-                                               const DevState *__restrict__ st, unsigned B, int rev) {
+                                               const DevState *__restrict__ st, unsigned B, int rev,
+                                               int *__restrict__ rec) {
+    sweep_record(rec, st, nact);
     const int cnt = st->batch_tag == B ? st->batch_count : 0;
     if (cnt <= 0) return;
     // slack compaction: the columns past s0 + *nact are untouched unit vectors (not swept);
@@ -1945,7 +1958,9 @@ __global__ __launch_bounds__(256) void k_sweep1(double *__restrict__ T, int rows
                                                 const double *__restrict__ F, const double *__restrict__ U,
                                                 const PivRec *__restrict__ recs,
                                                 const unsigned long long *__restrict__ PM,
-                                                const DevState *__restrict__ st, unsigned B, int rev) {
+                                                const DevState *__restrict__ st, unsigned B, int rev,
+                                               int *__restrict__ rec) {
+    sweep_record(rec, st, nact);
     const int cnt = st->batch_tag == B ? st->batch_count : 0;
     if (cnt <= 0) return;
     if (nact && s0 + *nact < Ns) Ns = s0 + *nact;
@@ -2069,8 +2084,10 @@ __global__ __launch_bounds__(256) void k_sweep_lds(double *__restrict__ T, int r
                                                    const double *__restrict__ F, const double *__restrict__ U,
                                                    const PivRec *__restrict__ recs,
                                                    const unsigned long long *__restrict__ PM,
-                                                   const DevState *__restrict__ st, unsigned B, int rev) {
+                                                   const DevState *__restrict__ st, unsigned B, int rev,
+                                               int *__restrict__ rec) {
     __shared__ double2 stage[D][RB][256];
+    sweep_record(rec, st, nact);
     const int cnt = st->batch_tag == B ? st->batch_count : 0;
     if (cnt <= 0) return;
     if (nact && s0 + *nact < Ns) Ns = s0 + *nact;
@@ -2438,6 +2455,10 @@ void sx_launch_pivot_row(const double *T, int rows, int row0, size_t ld, TLay tl
                                         pd.PM, enter_parts, pd.batch, pd.q, B1);
 }
 
+// record target of the next sweep launches (sx_set_sweep_record; null: none)
+static int *g_sweep_rec = nullptr;
+void sx_set_sweep_record(int *rec) { g_sweep_rec = rec; }
+
 // blocks of a kernel resident on the whole device at once
 template <typename K>
 static int sweep_capacity(K kernel) {
@@ -2472,7 +2493,7 @@ static void launch_sweep_t(double *T, int rows, size_t ld, TLay tl, int Ns, cons
     const int cb = (Ns + 511) / 512;
     dim3 grid(cb, row_slots(sweep_capacity(k_sweep<KT, RB, SC1>), cb, rows, RB));
     k_sweep<KT, RB, SC1><<<grid, 256, 0, s>>>(T, rows, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st, pd.batch,
-                                              rev);
+                                              rev, g_sweep_rec);
 }
 
 // one column per thread (k_sweep1) for full 32-slot sweeps (1), or two (k_sweep, 2: default)
@@ -2485,7 +2506,7 @@ static void launch_sweep1_t(double *T, int rows, size_t ld, TLay tl, int Ns, con
     const int cb = (Ns + 255) / 256;
     dim3 grid(cb, row_slots(sweep_capacity(k_sweep1<KT, RB, SC1>), cb, rows, RB));
     k_sweep1<KT, RB, SC1><<<grid, 256, 0, s>>>(T, rows, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st, pd.batch,
-                                               rev);
+                                               rev, g_sweep_rec);
 }
 
 template <int KT>
@@ -2516,7 +2537,7 @@ static void launch_sweep_lds_t(double *T, int rows, size_t ld, TLay tl, int Ns, 
     const int cb = (Ns + 511) / 512;
     dim3 grid(cb, row_slots(sweep_capacity(k_sweep_lds<SX_KMAX, RB, true, D>), cb, rows, RB));
     k_sweep_lds<SX_KMAX, RB, true, D><<<grid, 256, 0, s>>>(T, rows, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st,
-                                                           pd.batch, rev);
+                                                           pd.batch, rev, g_sweep_rec);
 }
 
 static bool launch_sweep_lds(int rb, int d, double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0,
