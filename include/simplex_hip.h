@@ -91,6 +91,9 @@ void simplex_set_poll_sleep(int k);
 void simplex_set_hist_fast(int on);
 /* full 32-slot sweeps: one column per thread (1; k_sweep1, A/B variant) or two (2, default) */
 void simplex_set_sweep_cols(int c);
+/* synthetic sweep bench (simplex_bench_sweep) only: sweeps read one buffer and write another,
+ * alternating (1), or in place (0, default; the pivot loop always sweeps in place) */
+void simplex_set_sweep_oop(int on);
 /* new engines' tableau layout: plain row-major rows (0), the two-region layout when aliasing and
  * m > 4096 (1, default), or region A forced to hold `mode` slack positions (>= 2,
  * test hook) */

@@ -108,6 +108,7 @@ SIGNATURES = {
     "simplex_set_poll_sleep": (None, [ctypes.c_int]),
     "simplex_set_hist_fast": (None, [ctypes.c_int]),
     "simplex_set_sweep_cols": (None, [ctypes.c_int]),
+    "simplex_set_sweep_oop": (None, [ctypes.c_int]),
     "simplex_set_regions": (None, [ctypes.c_int]),
     "simplex_set_mr_single_launch": (None, [ctypes.c_int]),
     "simplex_set_ld_pad": (None, [ctypes.c_int]),

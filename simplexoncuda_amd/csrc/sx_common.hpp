@@ -205,6 +205,7 @@ void sx_set_update_waves(float w);  // resident-grid multiple of the sweep (defa
 void sx_set_gather_wide(int on);
 void sx_set_record_replicas(int n);  // fused batch (one shard): tile records written in n <= 8 copies
 void sx_set_sweep_stages(int d);    // LDS-staged sweep with d stages per wave (0: register sweep)
+void sx_set_sweep_src(const double *src);  // register sweeps read src, write T (null: in place; synthetic bench)
 void sx_set_sweep_record(int *rec);  // next sweeps write (batch tag, count, nact) to rec[0..2] (null: off)
 void sx_set_sweep_cols(int c);     // full sweeps: 1 column per thread (k_sweep1) or 2 (k_sweep, default)
 void sx_set_hist_fast(int on);     // fused batch: branch-free history chains when no slot divides (default 1)

@@ -76,6 +76,7 @@ struct Config {
     long long inject_hang = -1;    // test hook: abort the n-th fused batch from now (-1 off)
     unsigned first_batch_id = 1;   // test hook: batch id of a new engine's first batch
     int ld_pad = 0;                // extra doubles per tableau row (multiple of 16; row stride tuning)
+    int sweep_oop = 0;             // synthetic sweep bench: read one buffer, write another (measurement)
     int ipc_rank = -1, ipc_world = 0;  // test hook: one shard per process, peers through IPC handles, no RCCL
     int uncached_xchg = 0;         // several shards: d and U in uncached memory (diagnostic; see alloc_shard)
     long long hang_recoveries = 0; // fused batches aborted and re-run on the per-pivot path
@@ -1322,6 +1323,7 @@ void simplex_set_sweep_stages(int d) { sx_set_sweep_stages(d); }
 void simplex_set_poll_sleep(int k) { sx_set_poll_sleep(k); }
 void simplex_set_hist_fast(int on) { sx_set_hist_fast(on); }
 void simplex_set_sweep_cols(int c) { sx_set_sweep_cols(c); }
+void simplex_set_sweep_oop(int on) { g_cfg.sweep_oop = on ? 1 : 0; }
 void simplex_set_uncached_exchange(int on) { g_cfg.uncached_xchg = on ? 1 : 0; }
 void simplex_set_ld_pad(int doubles) { g_cfg.ld_pad = doubles > 0 ? (int)round_up((size_t)doubles, 16) : 0; }
 void simplex_set_exchange_mode(int mode) { g_cfg.exchange_mode = (mode >= 0 && mode <= 2) ? mode : 0; }
@@ -1772,15 +1774,30 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     cfg.batch = pivots;
     cfg.rows_per_block = g_cfg.update_rows > 0 ? std::min(g_cfg.update_rows, 4) : (pivots > 16 ? 4 : 2);
     cfg.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : 1;  // (as sweep_cfg: write-through at every size)
+    // out of place (simplex_set_sweep_oop, measurement only): sweeps alternate between T and a
+    // copy T2, each reading one and writing the other
+    double *T2 = nullptr;
+    if (g_cfg.sweep_oop) {
+        T2 = dalloc<double>((size_t)rows * ld);
+        SX_HIP(hipMemcpyAsync(T2, T, sizeof(double) * (size_t)rows * ld, hipMemcpyDeviceToDevice, s));
+    }
     long long sweeps = 0;
-    for (int w = 0; w < warmup; ++w, ++sweeps)
-        sx_launch_sweep(T, rows, ld, btl, cols, nullptr, 0, pd, st, (int)(sweeps & 1), cfg, s);
+    auto one = [&]() {
+        double *dst = T, *src = T;
+        if (T2) {
+            src = (sweeps & 1) ? T2 : T;
+            dst = (sweeps & 1) ? T : T2;
+        }
+        sx_set_sweep_src(src);
+        sx_launch_sweep(dst, rows, ld, btl, cols, nullptr, 0, pd, st, (int)(sweeps & 1), cfg, s);
+        sx_set_sweep_src(nullptr);
+    };
+    for (int w = 0; w < warmup; ++w, ++sweeps) one();
     hipEvent_t e0, e1;
     SX_HIP(hipEventCreate(&e0));
     SX_HIP(hipEventCreate(&e1));
     SX_HIP(hipEventRecord(e0, s));
-    for (int it = 0; it < iters; ++it, ++sweeps)
-        sx_launch_sweep(T, rows, ld, btl, cols, nullptr, 0, pd, st, (int)(sweeps & 1), cfg, s);
+    for (int it = 0; it < iters; ++it, ++sweeps) one();
     SX_HIP(hipEventRecord(e1, s));
     SX_HIP(hipEventSynchronize(e1));
     float ms = 0.f;
@@ -1788,6 +1805,7 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     for (void *p : {(void *)T, (void *)U, (void *)F, (void *)recs, (void *)PM, (void *)st}) (void)hipFree(p);
+    if (T2) (void)hipFree(T2);
     (void)hipStreamDestroy(s);
     if (bytes) *bytes = 16.0 * (double)rows * (double)cols;
     return 1e3 * (double)ms / (double)iters;

@@ -1846,7 +1846,7 @@ __device__ __forceinline__ void sweep_record(int *rec, const DevState *st, const
 }
 
 template <int KT, int RB, bool SC1>
-__global__ __launch_bounds__(256) void k_sweep(double *__restrict__ T, int rows, size_t ld, TLay tl, int Ns,
+__global__ __launch_bounds__(256) void k_sweep(double *T, const double *Ts, int rows, size_t ld, TLay tl, int Ns,
                                                const int *__restrict__ nact, int s0,
                                                const double *__restrict__ F, const double *__restrict__ U,
                                                const PivRec *__restrict__ recs,
@@ -1870,6 +1870,7 @@ __global__ __launch_bounds__(256) void k_sweep(double *__restrict__ T, int rows,
     // this tile's storage region (jB is a multiple of 512: a tile lies in one region)
     const bool inB = bx * 512 >= tl.jB;
     double *const Tr = inB ? T + tl.offB : T;
+    const double *const Tsr = inB ? Ts + tl.offB : Ts;  // source (== T: in place)
     const size_t ldr = inB ? tl.ldB : tl.ldA;
     const int jr = inB ? j - tl.jB : j;
     const unsigned mask = slot_mask(cnt);
@@ -1887,8 +1888,8 @@ __global__ __launch_bounds__(256) void k_sweep(double *__restrict__ T, int rows,
 #pragma unroll
         for (int k = 0; k < RB; ++k) {
             const int i = i0 + k < rows ? i0 + k : i0;
-            const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(Tr + (size_t)i * ldr, 0, oob, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<double *>(Tsr) + (size_t)i * ldr, 0, oob, 0x00020000);
             x[k] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, i0 + k < rows ? jr * 8 : oob,
                                                                                       0, 2));
         }
@@ -2455,6 +2456,11 @@ void sx_launch_pivot_row(const double *T, int rows, int row0, size_t ld, TLay tl
                                         pd.PM, enter_parts, pd.batch, pd.q, B1);
 }
 
+// source of the next register sweeps (sx_set_sweep_src; null: in place).  Out-of-place sweeps
+// (read one buffer, write another) are a measurement of the synthetic bench only.
+static const double *g_sweep_src = nullptr;
+void sx_set_sweep_src(const double *src) { g_sweep_src = src; }
+
 // record target of the next sweep launches (sx_set_sweep_record; null: none)
 static int *g_sweep_rec = nullptr;
 void sx_set_sweep_record(int *rec) { g_sweep_rec = rec; }
@@ -2492,7 +2498,8 @@ static void launch_sweep_t(double *T, int rows, size_t ld, TLay tl, int Ns, cons
                            const DevState *st, int rev, hipStream_t s) {
     const int cb = (Ns + 511) / 512;
     dim3 grid(cb, row_slots(sweep_capacity(k_sweep<KT, RB, SC1>), cb, rows, RB));
-    k_sweep<KT, RB, SC1><<<grid, 256, 0, s>>>(T, rows, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st, pd.batch,
+    k_sweep<KT, RB, SC1><<<grid, 256, 0, s>>>(T, g_sweep_src ? g_sweep_src : T, rows, ld, tl, Ns, nact, s0, pd.F, pd.U,
+                                              pd.recs, pd.PM, st, pd.batch,
                                               rev, g_sweep_rec);
 }
 
