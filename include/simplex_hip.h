@@ -24,7 +24,6 @@ extern "C" {
 int simplex_version(void);
 void simplex_set_verbose(int on);            /* reference progress lines on stdout */
 void simplex_set_update_rows(int rb);        /* rows per sweep step: 1, 2, 4; 0 = auto */
-void simplex_set_snake(int mode);            /* kept for ABI compatibility: sweeps always alternate direction */
 void simplex_set_store_sc1(int mode);        /* write-through tableau stores: -1 auto, 0, 1 */
 /* pivots per tableau sweep (1..32, default 32): the pivots of a batch are selected on the
  * current values (pending pivots applied on the fly) and then applied to the tableau in one
@@ -73,27 +72,6 @@ int simplex_p2p_ready(void);
 void simplex_last_phase_seconds(double *out);
 /* the sweep's grid: waves x (blocks resident on the device) blocks (default 1; <= 0 resets) */
 void simplex_set_update_waves(double waves);
-/* fused batches: a hand-off of up to 512 granules is polled by one wave (1, default) or by
- * every thread of the block with a block vote per poll (0) */
-void simplex_set_gather_wide(int on);
-/* one shard: the fused batch's tile records are written in n copies (1..8) and each block polls
- * copy blockIdx % n, spreading the pollers of a large grid (default 1) */
-void simplex_set_record_replicas(int n);
-/* full-batch sweeps staged through LDS by LDS-DMA with d stages per wave (rows per step as
- * simplex_set_update_rows: 4 rows with d = 2 or 3, 2 rows with d = 4, 1 row with d = 4; 0 = the
- * register sweep, default; measured no faster) */
-void simplex_set_sweep_stages(int d);
-/* fused batches: pause between two polls of a hand-off, s_sleep 0/1/2/4/8/16 for k = 0..5
- * (default 1; diagnostic) */
-void simplex_set_poll_sleep(int k);
-/* fused batches: the pending-pivot chains of a ratio row / the pivot row run branch-free when no
- * slot of the wave divides (1, default) or every slot through the guarded chain (0; A/B knob) */
-void simplex_set_hist_fast(int on);
-/* full 32-slot sweeps: one column per thread (1; k_sweep1, A/B variant) or two (2, default) */
-void simplex_set_sweep_cols(int c);
-/* synthetic sweep bench (simplex_bench_sweep) only: sweeps read one buffer and write another,
- * alternating (1), or in place (0, default; the pivot loop always sweeps in place) */
-void simplex_set_sweep_oop(int on);
 /* new engines' tableau layout: plain row-major rows (0), the two-region layout when aliasing and
  * m > 4096 (1, default), or region A forced to hold `mode` slack positions (>= 2,
  * test hook) */
@@ -101,8 +79,6 @@ void simplex_set_regions(int mode);
 /* virtual shards with the peer-memory batch: every rank's batch in one launch (1, default) or one
  * launch per rank on its own stream (0; needs as many hardware queues running at once) */
 void simplex_set_mr_single_launch(int on);
-/* extra doubles appended to every tableau row of new engines (rounded up to 16; default 0) */
-void simplex_set_ld_pad(int doubles);
 /* several shards: keep d and U in uncached memory (1) or plain memory (0, default; uncached
  * was measured to corrupt results after earlier allocations were freed -- diagnostic only) */
 void simplex_set_uncached_exchange(int on);

@@ -9,7 +9,7 @@ from .api import (  # noqa: F401
     STATUS_NAMES, UNBOUNDED, Problem, Result, Session, bench_sweep, dev_argmin, dev_build_phase1,
     dev_build_phase1_generated, dev_pivots, dev_update_objective, generateRandomProblem,
     generateRandomProblemDevice, p2p_ready, printProblemToStream, readProblemFromFile, readRandomProblemFromFile,
-    set_alias, set_batch, set_compact, set_exchange_mode, set_force_exchange, set_fused, set_p2p, set_snake,
-    set_store_sc1, set_update_rows, set_update_waves, set_sweep_stages, set_hist_fast, set_sweep_cols, set_regions, set_mr_single_launch, set_verbose, set_virtual_ranks, twoPhaseMethod,
-    twoPhaseMethodEx)
+    set_alias, set_batch, set_compact, set_exchange_mode, set_force_exchange, set_fused, set_mr_single_launch,
+    set_p2p, set_regions, set_store_sc1, set_update_rows, set_update_waves, set_verbose, set_virtual_ranks,
+    twoPhaseMethod, twoPhaseMethodEx)
 from ._lib import LIB_PATH, load  # noqa: F401

@@ -83,7 +83,6 @@ SIGNATURES = {
     "simplex_version": (ctypes.c_int, []),
     "simplex_set_verbose": (None, [ctypes.c_int]),
     "simplex_set_update_rows": (None, [ctypes.c_int]),
-    "simplex_set_snake": (None, [ctypes.c_int]),
     "simplex_set_store_sc1": (None, [ctypes.c_int]),
     "simplex_set_batch": (None, [ctypes.c_int]),
     "simplex_set_device": (None, [ctypes.c_int]),
@@ -102,16 +101,8 @@ SIGNATURES = {
     "simplex_set_p2p": (None, [ctypes.c_int]),
     "simplex_p2p_ready": (ctypes.c_int, []),
     "simplex_set_update_waves": (None, [ctypes.c_double]),
-    "simplex_set_gather_wide": (None, [ctypes.c_int]),
-    "simplex_set_record_replicas": (None, [ctypes.c_int]),
-    "simplex_set_sweep_stages": (None, [ctypes.c_int]),
-    "simplex_set_poll_sleep": (None, [ctypes.c_int]),
-    "simplex_set_hist_fast": (None, [ctypes.c_int]),
-    "simplex_set_sweep_cols": (None, [ctypes.c_int]),
-    "simplex_set_sweep_oop": (None, [ctypes.c_int]),
     "simplex_set_regions": (None, [ctypes.c_int]),
     "simplex_set_mr_single_launch": (None, [ctypes.c_int]),
-    "simplex_set_ld_pad": (None, [ctypes.c_int]),
     "simplex_set_uncached_exchange": (None, [ctypes.c_int]),
     "simplex_hang_recoveries": (ctypes.c_longlong, []),
     "simplex_fused_batches": (ctypes.c_longlong, []),

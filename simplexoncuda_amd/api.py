@@ -351,32 +351,12 @@ def set_mr_single_launch(on):
     _lib.load().simplex_set_mr_single_launch(1 if on else 0)
 
 
-def set_sweep_stages(d):
-    """Full-batch sweeps staged through LDS by LDS-DMA, d stages per wave (0: register sweep)."""
-    _lib.load().simplex_set_sweep_stages(int(d))
-
-
-def set_hist_fast(on):
-    """Fused batches: branch-free pending-pivot chains when no slot of a wave divides (1,
-    default) or the guarded chain for every slot (0; A/B knob)."""
-    _lib.load().simplex_set_hist_fast(1 if on else 0)
-
-
-def set_sweep_cols(c):
-    """Full 32-slot sweeps with one column per thread (1; k_sweep1) or two (2, default)."""
-    _lib.load().simplex_set_sweep_cols(int(c))
-
-
 def set_verbose(on):
     _lib.load().simplex_set_verbose(1 if on else 0)
 
 
 def set_update_rows(rb):
     _lib.load().simplex_set_update_rows(int(rb))
-
-
-def set_snake(mode):
-    _lib.load().simplex_set_snake(int(mode))
 
 
 def set_store_sc1(mode):

@@ -202,14 +202,7 @@ struct MrLaunchRank {
 void sx_launch_batch_mr_multi(const MrLaunchRank *ranks, int W, int rpr, size_t ld, TLay tl, Cols c, unsigned B, int k,
                               int slots, const PeerView &pv, unsigned long long timeout, hipStream_t s);
 void sx_set_update_waves(float w);  // resident-grid multiple of the sweep (default 1)
-void sx_set_gather_wide(int on);
-void sx_set_record_replicas(int n);  // fused batch (one shard): tile records written in n <= 8 copies
-void sx_set_sweep_stages(int d);    // LDS-staged sweep with d stages per wave (0: register sweep)
-void sx_set_sweep_src(const double *src);  // register sweeps read src, write T (null: in place; synthetic bench)
 void sx_set_sweep_record(int *rec);  // next sweeps write (batch tag, count, nact) to rec[0..2] (null: off)
-void sx_set_sweep_cols(int c);     // full sweeps: 1 column per thread (k_sweep1) or 2 (k_sweep, default)
-void sx_set_hist_fast(int on);     // fused batch: branch-free history chains when no slot divides (default 1)
-void sx_set_poll_sleep(int k);      // hand-off polls pause s_sleep 0/1/2/4/8/16 for k = 0..5 (default 1)
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s);
 void sx_launch_l2_writeback(hipStream_t s);  // every XCD's L2 writes back its dirty lines
 

@@ -54,7 +54,6 @@ namespace {
 struct Config {
     int verbose = 0;
     int update_rows = 0;  // 0: auto (by tableau size)
-    int snake = -1;       // -1: auto, 0: off, 1: on
     int sc1 = -1;         // write-through tableau stores: -1 auto, 0, 1
     int batch = 32;          // pivots per tableau sweep (deferred updates), 1..SX_KMAX
     int device = -1;
@@ -75,8 +74,6 @@ struct Config {
     bool no_timer = false;         // the multi-GPU self-check: never write TIMER CSVs
     long long inject_hang = -1;    // test hook: abort the n-th fused batch from now (-1 off)
     unsigned first_batch_id = 1;   // test hook: batch id of a new engine's first batch
-    int ld_pad = 0;                // extra doubles per tableau row (multiple of 16; row stride tuning)
-    int sweep_oop = 0;             // synthetic sweep bench: read one buffer, write another (measurement)
     int ipc_rank = -1, ipc_world = 0;  // test hook: one shard per process, peers through IPC handles, no RCCL
     int uncached_xchg = 0;         // several shards: d and U in uncached memory (diagnostic; see alloc_shard)
     long long hang_recoveries = 0; // fused batches aborted and re-run on the per-pivot path
@@ -258,7 +255,7 @@ class Engine {
         N = N1;
         alias = alias_ && g_cfg.alias && m > 0;
         Ns1 = alias ? N2 : N1;
-        ld = round_up((size_t)Ns1, 16) + (size_t)g_cfg.ld_pad;
+        ld = round_up((size_t)Ns1, 16);
         batch_id = (g_cfg.first_batch_id >= 1 && g_cfg.first_batch_id < SX_BATCH_IDS) ? g_cfg.first_batch_id : 1;
         if (g_cfg.ipc_world > 1) {
             rccl = ipc = true;
@@ -292,8 +289,8 @@ class Engine {
             const int jB = (int)round_up((size_t)(1 + n + capA), SX_TILE);
             if (jB < Ns1) {
                 tl.jB = jB;
-                tl.ldA = (size_t)jB + (size_t)g_cfg.ld_pad;
-                tl.ldB = round_up((size_t)(Ns1 - jB), 16) + (size_t)g_cfg.ld_pad;
+                tl.ldA = (size_t)jB;
+                tl.ldB = round_up((size_t)(Ns1 - jB), 16);
                 tl.offB = (size_t)rpr * tl.ldA;  // every shard allocates rpr rows (peers index alike)
             }
         }
@@ -1296,7 +1293,6 @@ extern "C" {
 int simplex_version(void) { return 1; }
 void simplex_set_verbose(int on) { g_cfg.verbose = on; }
 void simplex_set_update_rows(int rb) { g_cfg.update_rows = (rb == 1 || rb == 2 || rb == 4 || rb == 8) ? rb : 0; }
-void simplex_set_snake(int mode) { g_cfg.snake = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_store_sc1(int mode) { g_cfg.sc1 = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_batch(int pivots) { g_cfg.batch = pivots > 0 ? std::min(pivots, SX_KMAX) : 32; }
 void simplex_set_device(int device) {
@@ -1317,15 +1313,7 @@ void simplex_last_phase_seconds(double *out) {
     out[1] = g_phase_seconds[1];
 }
 void simplex_set_update_waves(double waves) { sx_set_update_waves((float)waves); }
-void simplex_set_gather_wide(int on) { sx_set_gather_wide(on); }
-void simplex_set_record_replicas(int n) { sx_set_record_replicas(n); }
-void simplex_set_sweep_stages(int d) { sx_set_sweep_stages(d); }
-void simplex_set_poll_sleep(int k) { sx_set_poll_sleep(k); }
-void simplex_set_hist_fast(int on) { sx_set_hist_fast(on); }
-void simplex_set_sweep_cols(int c) { sx_set_sweep_cols(c); }
-void simplex_set_sweep_oop(int on) { g_cfg.sweep_oop = on ? 1 : 0; }
 void simplex_set_uncached_exchange(int on) { g_cfg.uncached_xchg = on ? 1 : 0; }
-void simplex_set_ld_pad(int doubles) { g_cfg.ld_pad = doubles > 0 ? (int)round_up((size_t)doubles, 16) : 0; }
 void simplex_set_exchange_mode(int mode) { g_cfg.exchange_mode = (mode >= 0 && mode <= 2) ? mode : 0; }
 void simplex_set_timer_dir(const char *dir) { g_cfg.timer_dir = dir ? dir : ""; }
 
@@ -1720,7 +1708,7 @@ long long simplex_session_rows(simplex_session *S, double *T_rows, long long ld_
 double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi, int pivots, int warmup, int iters,
                            double *bytes) {
     if (rows <= 0 || cols <= 1 || pivots < 1 || pivots > SX_KMAX || iters < 1 || rows < pivots) return -1.0;
-    const size_t ld = round_up((size_t)cols, 16) + (size_t)g_cfg.ld_pad;  // (ld_pad: sparse-row layouts)
+    const size_t ld = round_up((size_t)cols, 16);
     hipStream_t s;
     SX_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     uint32_t sd[3];
@@ -1774,24 +1762,8 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     cfg.batch = pivots;
     cfg.rows_per_block = g_cfg.update_rows > 0 ? std::min(g_cfg.update_rows, 4) : (pivots > 16 ? 4 : 2);
     cfg.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : 1;  // (as sweep_cfg: write-through at every size)
-    // out of place (simplex_set_sweep_oop, measurement only): sweeps alternate between T and a
-    // copy T2, each reading one and writing the other
-    double *T2 = nullptr;
-    if (g_cfg.sweep_oop) {
-        T2 = dalloc<double>((size_t)rows * ld);
-        SX_HIP(hipMemcpyAsync(T2, T, sizeof(double) * (size_t)rows * ld, hipMemcpyDeviceToDevice, s));
-    }
     long long sweeps = 0;
-    auto one = [&]() {
-        double *dst = T, *src = T;
-        if (T2) {
-            src = (sweeps & 1) ? T2 : T;
-            dst = (sweeps & 1) ? T : T2;
-        }
-        sx_set_sweep_src(src);
-        sx_launch_sweep(dst, rows, ld, btl, cols, nullptr, 0, pd, st, (int)(sweeps & 1), cfg, s);
-        sx_set_sweep_src(nullptr);
-    };
+    auto one = [&]() { sx_launch_sweep(T, rows, ld, btl, cols, nullptr, 0, pd, st, (int)(sweeps & 1), cfg, s); };
     for (int w = 0; w < warmup; ++w, ++sweeps) one();
     hipEvent_t e0, e1;
     SX_HIP(hipEventCreate(&e0));
@@ -1805,7 +1777,6 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     for (void *p : {(void *)T, (void *)U, (void *)F, (void *)recs, (void *)PM, (void *)st}) (void)hipFree(p);
-    if (T2) (void)hipFree(T2);
     (void)hipStreamDestroy(s);
     if (bytes) *bytes = 16.0 * (double)rows * (double)cols;
     return 1e3 * (double)ms / (double)iters;

@@ -719,18 +719,9 @@ __device__ __forceinline__ u64 ld_sys(const u64 *p) {
 // granules per lane of the one-wave gather (larger gathers use every thread of the block)
 #define SX_GATHER_PER_LANE 8
 
-// pause between two polls of a hand-off (s_sleep units of 64 clocks; diagnostic knob, default 1)
-__constant__ int c_poll_sleep = 1;
-__device__ __forceinline__ void poll_pause() {
-    switch (c_poll_sleep) {
-    case 0: break;
-    case 1: __builtin_amdgcn_s_sleep(1); break;
-    case 2: __builtin_amdgcn_s_sleep(2); break;
-    case 3: __builtin_amdgcn_s_sleep(4); break;
-    case 4: __builtin_amdgcn_s_sleep(8); break;
-    default: __builtin_amdgcn_s_sleep(16); break;
-    }
-}
+// pause between two polls of a hand-off (one s_sleep unit, 64 clocks: longer or no pauses
+// measured no different)
+__device__ __forceinline__ void poll_pause() { __builtin_amdgcn_s_sleep(1); }
 
 // Wave 0 of the block (threads 0..63) polls n <= 64 * SX_GATHER_PER_LANE granules, granule k
 // at base[off(k)], each until it carries `tag`, into out[k] (LDS), all of a round's loads in
@@ -847,10 +838,9 @@ __device__ __forceinline__ void wave_pass2(const unsigned *s_g, const unsigned *
 // thread of the block must call it.
 template <typename OFF, bool SYS = false>
 __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, unsigned *out, unsigned *abort_w,
-                              int *s_ok, unsigned long long timeout = 20000000ull, unsigned *pay = nullptr,
-                              int wide = 1) {
+                              int *s_ok, unsigned long long timeout = 20000000ull, unsigned *pay = nullptr) {
     const int t = threadIdx.x, nt = blockDim.x;
-    if (n <= 64 || (wide && n <= 64 * SX_GATHER_PER_LANE)) {
+    if (n <= 64 * SX_GATHER_PER_LANE) {
         if (t < 64) {
             const int ok = poll_wave<OFF, SYS>(base, n, off, tag, out, abort_w, timeout, pay);
             if (t == 0) *s_ok = ok;
@@ -898,15 +888,10 @@ __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, uns
 #define SX_GA_STRIDE (8 + 2 * SX_KMAX)  // ratio tile: v(2, payload: idx, elig) pad(2) a(2) b(2) | F[r][s] (2 per slot)
 #define SX_GB_STRIDE (4 + 2 * SX_KMAX)  // objective tile: v(2, payload: idx) pad(2) | U[s][e] (2 per slot)
 __device__ __forceinline__ int rec2_a(int k) { return (k >> 1) * SX_GA_STRIDE + (k & 1); }
-// granules of one replica of all tile records (k_batch keeps up to SX_GREP replicas)
-#define SX_GREP 8
+// granules of all tile records
 __host__ __device__ __forceinline__ size_t sx_ga_size() { return (size_t)SX_TILE * SX_GA_STRIDE; }
 __host__ __device__ __forceinline__ size_t sx_gb_size() { return (size_t)SX_TILE * SX_GB_STRIDE; }
 __device__ __forceinline__ int rec2_b(int k) { return (k >> 1) * SX_GB_STRIDE + (k & 1); }
-
-// branch-free history chains in the fused batch when no slot needs a division (1, default);
-// 0 runs every slot through the guarded chain (A/B knob, simplex_set_hist_fast)
-__constant__ int c_hist_fast = 1;
 
 // The batch's pending pivots s < q applied, in slot order, to a ratio row's entering-column
 // entry `a` (solver.cu:34-46 on that element): a / p_s at the slots in `bits` (the row itself
@@ -917,7 +902,7 @@ __constant__ int c_hist_fast = 1;
 __device__ __forceinline__ double hist_col(double a, int q, unsigned bits, const double *s_hist, const double *s_ue,
                                            const double *s_p) {
     const int t = threadIdx.x;
-    if (c_hist_fast && __ballot(bits != 0u) == 0ull) {
+    if (__ballot(bits != 0u) == 0ull) {
         int s = 0;
         for (; s + 8 <= q; s += 8) {
             double h[8], ue[8];
@@ -961,7 +946,7 @@ __device__ __forceinline__ double hist_col(double a, int q, unsigned bits, const
 __device__ __forceinline__ double hist_row(double u, int q, int r, const double *s_hist, const double *s_fr,
                                            const double *s_p, const int *s_r) {
     const int t = threadIdx.x, lane = t & 63;
-    if (c_hist_fast && __ballot(lane < q && s_r[lane < q ? lane : 0] == r) == 0ull) {
+    if (__ballot(lane < q && s_r[lane < q ? lane : 0] == r) == 0ull) {
         int s = 0;
         for (; s + 8 <= q; s += 8) {
             double h[8], fr[8];
@@ -1004,8 +989,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                                                double *__restrict__ d, double *__restrict__ d_save, int *base,
                                                DevState *st, double *U, double *F, PivRec *recs,
                                                unsigned long long *PM, unsigned B, int K, int NA, int NB,
-                                               BatchChan *ch, u64 *ga, u64 *gb, unsigned long long *stamps,
-                                               int gw, int nrep) {
+                                               BatchChan *ch, u64 *ga, u64 *gb, unsigned long long *stamps) {
     extern __shared__ double s_hist[];  // [K][512]: F history (ratio blocks) / U history (objective blocks)
     __shared__ double s_v[16];
     __shared__ int s_i[16];
@@ -1023,11 +1007,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
     __shared__ int s_welig[SX_TILE / 64];
     const int t = threadIdx.x;
     const bool isA = (int)blockIdx.x < NA;
-    // the tile records are written in nrep replicas; a block polls replica blockIdx % nrep, so
-    // the ~200 pollers of a large grid spread over nrep copies of each line (speed only: every
-    // replica carries the same granules)
-    const u64 *gam = ga + (size_t)(blockIdx.x % nrep) * sx_ga_size();
-    const u64 *gbm = gb + (size_t)(blockIdx.x % nrep) * sx_gb_size();
+    const u64 *gam = ga, *gbm = gb;
     // stamps (diagnostic, normally null): s_memrealtime (100 MHz) at hand-off points of ratio
     // block 0 and objective block 0, [q][8]
 #define SX_STAMP(k)                                                                           \
@@ -1118,13 +1098,12 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                     // the record: v (payload: index, "any" bit), pad, a, b, then F[winner][s] for s < q
                     const unsigned pl = (wi >= 0 ? (unsigned)wl : SX_NOIDX) | ((unsigned)any << 10);
                     const int nG = 8 + 2 * q;
-                    for (int idx = t; idx < nrep * nG; idx += 64) {
-                        const int r = idx / nG, k = idx - r * nG;
+                    for (int k = t; k < nG; k += 64) {
                         if (k == 2 || k == 3) continue;
                         const double val = k < 2 ? wv : k < 6 ? s_a[wl] : k < 8 ? s_b[wl]
                                                                         : s_hist[((k - 8) >> 1) * SX_TILE + wl];
                         const unsigned long long bits64 = (unsigned long long)__double_as_longlong(val);
-                        put_g(ga + (size_t)r * sx_ga_size() + (size_t)blockIdx.x * SX_GA_STRIDE + k,
+                        put_g(ga + (size_t)blockIdx.x * SX_GA_STRIDE + k,
                               (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64, k < 2 ? (tag | pl) : tag);
                     }
                 }
@@ -1133,7 +1112,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
             // ---- selection: every block runs pass 2 over the ratio-tile winners.  Wave 0 polls
             // the records and runs the tree in registers (wave_pass2); one block barrier.
             int r, anyall;
-            if (gw && 2 * NA <= 64 * SX_GATHER_PER_LANE) {
+            if (2 * NA <= 64 * SX_GATHER_PER_LANE) {
                 if (t < 64) {
                     const int ok = poll_wave(gam, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
                     double tv = DBL_MAX;
@@ -1153,7 +1132,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                 r = s_sel_r;
                 anyall = s_sel_any;
             } else {
-                if (!gather_tagged(gam, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay, gw)) {
+                if (!gather_tagged(gam, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay)) {
                     aborted = true;
                     break;
                 }
@@ -1269,12 +1248,11 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                     // the record: v (payload: index), pad, then U[s][winner] for s <= q
                     const unsigned pl = wi >= 0 ? (unsigned)win : SX_NOIDX;
                     const int nG = 4 + 2 * (q + 1);
-                    for (int idx = t; idx < nrep * nG; idx += 64) {
-                        const int r = idx / nG, k = idx - r * nG;
+                    for (int k = t; k < nG; k += 64) {
                         if (k == 2 || k == 3) continue;
                         const double val = k < 2 ? wv : s_hist[((k - 4) >> 1) * SX_TILE + win];
                         const unsigned long long bits64 = (unsigned long long)__double_as_longlong(val);
-                        put_g(gb + (size_t)r * sx_gb_size() + (size_t)tb * SX_GB_STRIDE + k,
+                        put_g(gb + (size_t)tb * SX_GB_STRIDE + k,
                               (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64, k < 2 ? (tag | pl) : tag);
                     }
                 }
@@ -1282,7 +1260,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
             }
             // ---- entering variable of pivot q + 1: every block runs pass 2 over the objective
             // tiles (wave 0 polls and runs the tree; one block barrier)
-            if (gw && 2 * NB <= 64 * SX_GATHER_PER_LANE) {
+            if (2 * NB <= 64 * SX_GATHER_PER_LANE) {
                 if (t < 64) {
                     const int ok = poll_wave(gbm, 2 * NB, rec2_b, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
                     double ev = DBL_MAX;
@@ -1300,7 +1278,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                     break;
                 }
             } else {
-                if (!gather_tagged(gbm, 2 * NB, rec2_b, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay, gw)) {
+                if (!gather_tagged(gbm, 2 * NB, rec2_b, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay)) {
                     aborted = true;
                     break;
                 }
@@ -1413,7 +1391,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                                                   unsigned long long *PM, unsigned B, int K,
                                                   int slots, int W, int rank, int tb0, int tb1, int NBg,
                                                   BatchChan *ch, const u64 *ga, const u64 *gb, const u64 *gdone,
-                                                  PeerView pv, unsigned long long timeout, int gw) {
+                                                  PeerView pv, unsigned long long timeout) {
     extern __shared__ double s_hist[];  // [K][512]: F history (ratio tiles) / U history (objective tiles)
     __shared__ double s_v[16];
     __shared__ int s_i[16];
@@ -1523,7 +1501,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
             }
             // ---- selection: pass 2 over every rank's ratio tiles (wave 0 polls and reduces)
             int r, anyall;
-            if (gw && 2 * NAg <= 64 * SX_GATHER_PER_LANE) {
+            if (2 * NAg <= 64 * SX_GATHER_PER_LANE) {
                 if (t < 64) {
                     const int ok = poll_wave<decltype(gather_a), true>(ga, 2 * NAg, gather_a, tag, s_g, &ch->abort_w,
                                                                        timeout, s_pay);
@@ -1545,7 +1523,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 anyall = s_sel_any;
             } else {
                 if (!gather_tagged<decltype(gather_a), true>(ga, 2 * NAg, gather_a, tag, s_g, &ch->abort_w, &s_ok,
-                                                             timeout, s_pay, gw)) {
+                                                             timeout, s_pay)) {
                     aborted = true;
                     break;
                 }
@@ -1671,7 +1649,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 }
             }
             // ---- entering variable of pivot q + 1: pass 2 over every objective tile (wave 0)
-            if (gw && 2 * NBg <= 64 * SX_GATHER_PER_LANE) {
+            if (2 * NBg <= 64 * SX_GATHER_PER_LANE) {
                 if (t < 64) {
                     const int ok = poll_wave<decltype(gather_b), true>(gb, 2 * NBg, gather_b, tag, s_g, &ch->abort_w,
                                                                        timeout, s_pay);
@@ -1691,7 +1669,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 }
             } else {
                 if (!gather_tagged<decltype(gather_b), true>(gb, 2 * NBg, gather_b, tag, s_g, &ch->abort_w, &s_ok,
-                                                             timeout, s_pay, gw)) {
+                                                             timeout, s_pay)) {
                     aborted = true;
                     break;
                 }
@@ -1783,8 +1761,9 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
                                                   unsigned long long *PM, unsigned B, int K,
                                                   int slots, int W, int rank, int tb0, int tb1, int NBg,
                                                   BatchChan *ch, const u64 *ga, const u64 *gb, const u64 *gdone,
-                                                  PeerView pv, unsigned long long timeout, int gw) {
-    batch_mr_body((int)blockIdx.x, gridDim.x, T, rows, row0, rpr, ld, tl, c, d, d_save, base, st, U, F, recs, PM, B, K, slots, W, rank, tb0, tb1, NBg, ch, ga, gb, gdone, pv, timeout, gw);
+                                                  PeerView pv, unsigned long long timeout) {
+    batch_mr_body((int)blockIdx.x, gridDim.x, T, rows, row0, rpr, ld, tl, c, d, d_save, base, st, U, F, recs, PM, B, K,
+                  slots, W, rank, tb0, tb1, NBg, ch, ga, gb, gdone, pv, timeout);
 }
 
 // All W virtual ranks' batches in ONE launch (ranks on one GPU): block b belongs to the rank k
@@ -1810,7 +1789,7 @@ struct MrRanks {
 };
 __global__ __launch_bounds__(512) void k_batch_mr_multi(MrRanks R, int rpr, size_t ld, TLay tl, Cols c, unsigned B,
                                                         int K, int slots, int W, int NBg, PeerView pv,
-                                                        unsigned long long timeout, int gw) {
+                                                        unsigned long long timeout) {
     int k = 0;
     while (k + 1 < W && (int)blockIdx.x >= R.first[k + 1]) ++k;
     const MrRank &x = R.r[k];
@@ -1818,7 +1797,7 @@ __global__ __launch_bounds__(512) void k_batch_mr_multi(MrRanks R, int rpr, size
     cx.perm = x.perm;
     batch_mr_body((int)blockIdx.x - R.first[k], (unsigned)(R.first[k + 1] - R.first[k]), x.T, x.rows, x.row0, rpr, ld,
                   tl, cx, x.d, x.d_save, x.base, x.st, x.U, x.F, x.recs, x.PM, B, K, slots, W, x.rank, x.tb0, x.tb1,
-                  NBg, x.ch, x.ga, x.gb, x.gdone, pv, timeout, gw);
+                  NBg, x.ch, x.ga, x.gb, x.gdone, pv, timeout);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1846,7 +1825,7 @@ __device__ __forceinline__ void sweep_record(int *rec, const DevState *st, const
 }
 
 template <int KT, int RB, bool SC1>
-__global__ __launch_bounds__(256) void k_sweep(double *T, const double *Ts, int rows, size_t ld, TLay tl, int Ns,
+__global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, TLay tl, int Ns,
                                                const int *__restrict__ nact, int s0,
                                                const double *__restrict__ F, const double *__restrict__ U,
                                                const PivRec *__restrict__ recs,
@@ -1870,7 +1849,6 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, const double *Ts, int 
     // this tile's storage region (jB is a multiple of 512: a tile lies in one region)
     const bool inB = bx * 512 >= tl.jB;
     double *const Tr = inB ? T + tl.offB : T;
-    const double *const Tsr = inB ? Ts + tl.offB : Ts;  // source (== T: in place)
     const size_t ldr = inB ? tl.ldB : tl.ldA;
     const int jr = inB ? j - tl.jB : j;
     const unsigned mask = slot_mask(cnt);
@@ -1889,7 +1867,7 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, const double *Ts, int 
         for (int k = 0; k < RB; ++k) {
             const int i = i0 + k < rows ? i0 + k : i0;
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<double *>(Tsr) + (size_t)i * ldr, 0, oob, 0x00020000);
+                Tr + (size_t)i * ldr, 0, oob, 0x00020000);
             x[k] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, i0 + k < rows ? jr * 8 : oob,
                                                                                       0, 2));
         }
@@ -1944,236 +1922,6 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, const double *Ts, int 
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, jr * 8, 0, SC1 ? 16 : 0);
         }
     }
-}
-
-// k_sweep with ONE column per thread (simplex_set_sweep_cols(1); A/B variant): a column's KT
-// pivot-row values take KT VGPRs instead of 2 KT, so about twice as many waves are resident
-// and RB = 8 rows per step keep the same 4 KB in flight per wave; a wave moves 512 B per row
-// in 8-byte lanes.  256-column tiles (jB is a multiple of 512: a tile lies in one region).
-// Same operations, same order as k_sweep.
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-
-template <int KT, int RB, bool SC1>
-__global__ __launch_bounds__(256) void k_sweep1(double *__restrict__ T, int rows, size_t ld, TLay tl, int Ns,
-                                                const int *__restrict__ nact, int s0,
-                                                const double *__restrict__ F, const double *__restrict__ U,
-                                                const PivRec *__restrict__ recs,
-                                                const unsigned long long *__restrict__ PM,
-                                                const DevState *__restrict__ st, unsigned B, int rev,
-                                               int *__restrict__ rec) {
-    sweep_record(rec, st, nact);
-    const int cnt = st->batch_tag == B ? st->batch_count : 0;
-    if (cnt <= 0) return;
-    if (nact && s0 + *nact < Ns) Ns = s0 + *nact;
-    const int cb = (Ns + 255) / 256;
-    const int lin = (int)(blockIdx.y * gridDim.x + blockIdx.x);
-    const int G = (int)(gridDim.x * gridDim.y) / cb;
-    const int tile = lin % cb, gy = lin / cb;
-    if (gy >= G) return;
-    const int bx = rev ? cb - 1 - tile : tile;
-    const int j = bx * 256 + (int)threadIdx.x;
-    if (j >= Ns) return;
-    const bool inB = bx * 256 >= tl.jB;
-    double *const Tr = inB ? T + tl.offB : T;
-    const size_t ldr = inB ? tl.ldB : tl.ldA;
-    const int jr = inB ? j - tl.jB : j;
-    const unsigned mask = slot_mask(cnt);
-    double u[KT];
-#pragma unroll
-    for (int s = 0; s < KT; ++s) u[s] = s < cnt ? U[(size_t)s * ld + j] : 0.0;
-    const int ng = (rows + RB - 1) / RB;
-    const int oob = (int)(ldr * 8);
-    for (int g = gy; g < ng; g += G) {
-        const int i0 = (rev ? ng - 1 - g : g) * RB;
-        double x[RB];
-#pragma unroll
-        for (int k = 0; k < RB; ++k) {
-            const int i = i0 + k < rows ? i0 + k : i0;
-            const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(Tr + (size_t)i * ldr, 0, oob, 0x00020000);
-            x[k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, i0 + k < rows ? jr * 8 : oob,
-                                                                                    0, 2));
-        }
-#pragma unroll
-        for (int k = 0; k < RB; ++k) {
-            const int i = i0 + k;
-            if (i >= rows) break;
-            const double *Fr = F + (size_t)i * SX_KMAX;
-            double f[KT];
-#pragma unroll
-            for (int s = 0; s < KT; ++s) f[s] = Fr[s];
-            const unsigned bits = pend_bits(PM, i, B, mask);
-            double y = x[k];
-            if (bits == 0u && cnt == KT) {
-#pragma unroll
-                for (int s = 0; s < KT; ++s) y = fma(f[s], u[s], y);
-            } else {
-#pragma unroll
-                for (int s = 0; s < KT; ++s) {
-                    if (s < cnt) {
-                        if ((bits >> s) & 1u)
-                            y = y / recs[s].p;
-                        else
-                            y = fma(f[s], u[s], y);
-                    }
-                }
-            }
-            const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(Tr + (size_t)i * ldr, 0, oob, 0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y), rs, jr * 8, 0, SC1 ? 16 : 0);
-        }
-    }
-}
-
-// One row of the sweep (the arithmetic of k_sweep above, shared by the staged variant).
-template <int KT>
-__device__ __forceinline__ double2 sweep_row(double2 y, const double2 (&u)[KT], const double *__restrict__ F,
-                                             const PivRec *__restrict__ recs, const unsigned long long *__restrict__ PM,
-                                             int i, unsigned B, unsigned mask, int cnt) {
-    const double *Fr = F + (size_t)i * SX_KMAX;
-    double f[KT];
-#pragma unroll
-    for (int s = 0; s < KT; ++s) f[s] = Fr[s];
-    const unsigned bits = pend_bits(PM, i, B, mask);
-    if (bits == 0u && cnt == KT) {
-#pragma unroll
-        for (int s = 0; s < KT; ++s) {
-            y.x = fma(f[s], u[s].x, y.x);
-            y.y = fma(f[s], u[s].y, y.y);
-        }
-    } else if (bits == 0u) {
-#pragma unroll
-        for (int s = 0; s < KT; ++s) {
-            if (s < cnt) {
-                y.x = fma(f[s], u[s].x, y.x);
-                y.y = fma(f[s], u[s].y, y.y);
-            }
-        }
-    } else {
-#pragma unroll
-        for (int s = 0; s < KT; ++s) {
-            if (s < cnt) {
-                if ((bits >> s) & 1u) {
-                    const double p = recs[s].p;
-                    y.x = y.x / p;
-                    y.y = y.y / p;
-                } else {
-                    y.x = fma(f[s], u[s].x, y.x);
-                    y.y = fma(f[s], u[s].y, y.y);
-                }
-            }
-        }
-    }
-    return y;
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// The same sweep with the tableau reads staged through LDS by LDS-DMA (global_load_lds_dwordx4,
-// no VGPR destination): each wave keeps D - 1 row groups of its own 1 KB column slice in
-// flight ahead of the one it updates, where k_sweep holds one group in registers.  A wave
-// reads back only what it loaded itself, so no block barrier is needed: a counted
-// `s_waitcnt vmcnt` retires a stage (the DMA is inline asm, invisible to the compiler's own
-// counting; every iteration issues exactly RB loads -- past its last group it re-reads that
-// group -- and RB stores, so the counts are exact).  Same operations, same order as k_sweep.
-template <int KT, int RB, bool SC1, int D>
-__global__ __launch_bounds__(256) void k_sweep_lds(double *__restrict__ T, int rows, size_t ld, TLay tl, int Ns,
-                                                   const int *__restrict__ nact, int s0,
-                                                   const double *__restrict__ F, const double *__restrict__ U,
-                                                   const PivRec *__restrict__ recs,
-                                                   const unsigned long long *__restrict__ PM,
-                                                   const DevState *__restrict__ st, unsigned B, int rev,
-                                               int *__restrict__ rec) {
-    __shared__ double2 stage[D][RB][256];
-    sweep_record(rec, st, nact);
-    const int cnt = st->batch_tag == B ? st->batch_count : 0;
-    if (cnt <= 0) return;
-    if (nact && s0 + *nact < Ns) Ns = s0 + *nact;
-    const int cb = (Ns + 511) / 512;
-    const int lin = (int)(blockIdx.y * gridDim.x + blockIdx.x);
-    const int G = (int)(gridDim.x * gridDim.y) / cb;
-    const int tile = lin % cb, gy = lin / cb;
-    if (gy >= G) return;
-    const int bx = rev ? cb - 1 - tile : tile;
-    const int j = (bx * 256 + (int)threadIdx.x) * 2;
-    if (j >= Ns) return;  // (whole lanes leave; a wave's DMA runs on the lanes left)
-    // this tile's storage region (jB is a multiple of 512: a tile lies in one region)
-    const bool inB = bx * 512 >= tl.jB;
-    double *const Tr = inB ? T + tl.offB : T;
-    const size_t ldr = inB ? tl.ldB : tl.ldA;
-    const int jr = inB ? j - tl.jB : j;
-    const int ng = (rows + RB - 1) / RB;
-    const int nmy = gy < ng ? (ng - gy + G - 1) / G : 0;
-    if (nmy == 0) return;
-    const unsigned mask = slot_mask(cnt);
-    const int w = (int)threadIdx.x >> 6;
-    double2 u[KT];
-#pragma unroll
-    for (int s = 0; s < KT; ++s)
-        u[s] = s < cnt ? *reinterpret_cast<const double2 *>(U + (size_t)s * ld + j) : make_double2(0.0, 0.0);
-    // the stage buffers of this wave (LDS byte addresses, wave-uniform)
-    const unsigned lds0 = (unsigned)(uintptr_t)&stage[0][0][w * 64];
-    auto first_row = [&](int it) {  // first row of this block's it-th group (past the last: the last)
-        const int g = gy + (it < nmy ? it : nmy - 1) * G;
-        return (rev ? ng - 1 - g : g) * RB;
-    };
-    auto issue = [&](int it) {
-        const int i0 = first_row(it);
-        const unsigned sb = lds0 + (unsigned)((it % D) * RB * 256 * 16);
-#pragma unroll
-        for (int k = 0; k < RB; ++k) {
-            const int i = i0 + k < rows ? i0 + k : rows - 1;
-            const double *src = Tr + (size_t)i * ldr + jr;
-            unsigned keep;
-            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
-                         "s_mov_b32 m0, %0"
-                         : "=&s"(keep)
-                         : "v"(src), "s"(__builtin_amdgcn_readfirstlane(sb + (unsigned)(k * 256 * 16)))
-                         : "memory");
-        }
-    };
-#pragma unroll
-    for (int it = 0; it < D - 1; ++it) issue(it);
-    const int oob = (int)(ldr * 8);
-    for (int it = 0; it < nmy; ++it) {
-        issue(it + D - 1);
-        // ops issued after stage it's loads: steady state 2 RB (D - 1); the first D - 1
-        // iterations RB (D - 1 + it)
-        if (it >= D - 1) {
-            wait_vm<2 * RB * (D - 1)>();
-        } else if (it == 0) {
-            wait_vm<RB * (D - 1)>();
-        } else if (it == 1) {
-            wait_vm<RB * D>();
-        } else if (it == 2) {
-            wait_vm<RB * (D + 1)>();
-        } else if (it == 3) {
-            wait_vm<RB * (D + 2)>();
-        } else {
-            wait_vm<RB * (D - 1)>();  // (D > 5: conservative)
-        }
-        const int i0 = first_row(it);
-        const int sl = it % D;
-        double2 x[RB];
-#pragma unroll
-        for (int k = 0; k < RB; ++k) x[k] = stage[sl][k][threadIdx.x];
-#pragma unroll
-        for (int k = 0; k < RB; ++k) {
-            const int i = i0 + k;
-            const bool live = i < rows;
-            const double2 y = sweep_row<KT>(x[k], u, F, recs, PM, live ? i : i0, B, mask, cnt);
-            const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(Tr + (size_t)(live ? i : i0) * ldr, 0, oob, 0x00020000);
-            // (a row past the end: the store goes out of range and is dropped -- one store per
-            // row slot always, so the counts above hold)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, live ? jr * 8 : oob, 0,
-                                                   SC1 ? 16 : 0);
-        }
-    }
-    wait_vm<0>();  // (the DMA of the trailing re-reads lands before the block's LDS is released)
 }
 
 // Slack compaction (sx_common.hpp Cols), between a batch's selections and its
@@ -2456,11 +2204,6 @@ void sx_launch_pivot_row(const double *T, int rows, int row0, size_t ld, TLay tl
                                         pd.PM, enter_parts, pd.batch, pd.q, B1);
 }
 
-// source of the next register sweeps (sx_set_sweep_src; null: in place).  Out-of-place sweeps
-// (read one buffer, write another) are a measurement of the synthetic bench only.
-static const double *g_sweep_src = nullptr;
-void sx_set_sweep_src(const double *src) { g_sweep_src = src; }
-
 // record target of the next sweep launches (sx_set_sweep_record; null: none)
 static int *g_sweep_rec = nullptr;
 void sx_set_sweep_record(int *rec) { g_sweep_rec = rec; }
@@ -2498,22 +2241,9 @@ static void launch_sweep_t(double *T, int rows, size_t ld, TLay tl, int Ns, cons
                            const DevState *st, int rev, hipStream_t s) {
     const int cb = (Ns + 511) / 512;
     dim3 grid(cb, row_slots(sweep_capacity(k_sweep<KT, RB, SC1>), cb, rows, RB));
-    k_sweep<KT, RB, SC1><<<grid, 256, 0, s>>>(T, g_sweep_src ? g_sweep_src : T, rows, ld, tl, Ns, nact, s0, pd.F, pd.U,
+    k_sweep<KT, RB, SC1><<<grid, 256, 0, s>>>(T, rows, ld, tl, Ns, nact, s0, pd.F, pd.U,
                                               pd.recs, pd.PM, st, pd.batch,
                                               rev, g_sweep_rec);
-}
-
-// one column per thread (k_sweep1) for full 32-slot sweeps (1), or two (k_sweep, 2: default)
-static int g_sweep_cols = 2;
-void sx_set_sweep_cols(int c) { g_sweep_cols = c == 1 ? 1 : 2; }
-
-template <int KT, int RB, bool SC1>
-static void launch_sweep1_t(double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0, const Pending &pd,
-                            const DevState *st, int rev, hipStream_t s) {
-    const int cb = (Ns + 255) / 256;
-    dim3 grid(cb, row_slots(sweep_capacity(k_sweep1<KT, RB, SC1>), cb, rows, RB));
-    k_sweep1<KT, RB, SC1><<<grid, 256, 0, s>>>(T, rows, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st, pd.batch,
-                                               rev, g_sweep_rec);
 }
 
 template <int KT>
@@ -2534,50 +2264,10 @@ void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, in
     k_activate<<<1, 256, 0, s>>>(perm, iperm, act, nact, m, T, rows, row0, ld, tl, s0, pd.U, pd.recs, st, pd.batch);
 }
 
-// the LDS-staged sweep (k_sweep_lds): stages per wave, 0 = the register sweep
-static int g_sweep_stages = 0;
-void sx_set_sweep_stages(int d) { g_sweep_stages = d < 0 ? 0 : d; }
-
-template <int RB, int D>
-static void launch_sweep_lds_t(double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0, const Pending &pd,
-                               const DevState *st, int rev, hipStream_t s) {
-    const int cb = (Ns + 511) / 512;
-    dim3 grid(cb, row_slots(sweep_capacity(k_sweep_lds<SX_KMAX, RB, true, D>), cb, rows, RB));
-    k_sweep_lds<SX_KMAX, RB, true, D><<<grid, 256, 0, s>>>(T, rows, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st,
-                                                           pd.batch, rev, g_sweep_rec);
-}
-
-static bool launch_sweep_lds(int rb, int d, double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0,
-                             const Pending &pd, const DevState *st, int rev, hipStream_t s) {
-#define SX_LDS_CASE(R, DD)                                                      \
-    if (rb == R && d == DD) {                                                   \
-        launch_sweep_lds_t<R, DD>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s); \
-        return true;                                                            \
-    }
-    SX_LDS_CASE(4, 2)
-    SX_LDS_CASE(4, 3)
-    SX_LDS_CASE(2, 4)
-    SX_LDS_CASE(1, 4)
-#undef SX_LDS_CASE
-    return false;
-}
-
 void sx_launch_sweep(double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0, const Pending &pd,
                      const DevState *st, int rev, SweepCfg cfg, hipStream_t s) {
     if (rows <= 0) return;
     const int k = cfg.batch;  // pivots the sweep may have to apply (register slots)
-    if (g_sweep_stages > 0 && k > 16 && k <= SX_KMAX && cfg.sc1 &&
-        launch_sweep_lds(cfg.rows_per_block, g_sweep_stages, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s))
-        return;
-    if (g_sweep_cols == 1 && k > 16 && k <= SX_KMAX) {
-        if (cfg.rows_per_block == 2)
-            cfg.sc1 ? launch_sweep1_t<SX_KMAX, 4, true>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s)
-                    : launch_sweep1_t<SX_KMAX, 4, false>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
-        else
-            cfg.sc1 ? launch_sweep1_t<SX_KMAX, 8, true>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s)
-                    : launch_sweep1_t<SX_KMAX, 8, false>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
-        return;
-    }
     if (k <= 1)
         launch_sweep_k<1>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else if (k <= 4)
@@ -2592,25 +2282,10 @@ void sx_launch_sweep(double *T, int rows, size_t ld, TLay tl, int Ns, const int 
         SX_FATAL("batch larger than SX_KMAX");
 }
 
-// fused batches: gathers of up to 512 granules polled by one wave (1, default) or by every
-// thread with a block vote per poll (0)
-static int g_gather_wide = 1;
-void sx_set_gather_wide(int on) { g_gather_wide = on ? 1 : 0; }
-void sx_set_poll_sleep(int k) {
-    const int v = k < 0 ? 1 : k;
-    SX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_poll_sleep), &v, sizeof(int)));
-}
-void sx_set_hist_fast(int on) {
-    const int v = on ? 1 : 0;
-    SX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_hist_fast), &v, sizeof(int)));
-}
-static int g_record_replicas = 1;
-void sx_set_record_replicas(int n) { g_record_replicas = n < 1 ? 1 : n > SX_GREP ? SX_GREP : n; }
-
 static size_t batch_lds(int k) { return (size_t)k * SX_TILE * sizeof(double); }
 
-size_t sx_batch_granules_a() { return sx_ga_size() * SX_GREP; }
-size_t sx_batch_granules_b() { return sx_gb_size() * SX_GREP; }
+size_t sx_batch_granules_a() { return sx_ga_size(); }
+size_t sx_batch_granules_b() { return sx_gb_size(); }
 
 bool sx_batch_fits(int rows, Cols c, int k) {
     if (k < 1 || k > SX_KMAX || rows <= 0) return false;
@@ -2638,8 +2313,7 @@ void sx_launch_batch(const double *T, int rows, size_t ld, TLay tl, Cols c, doub
     if (!sx_batch_fits(rows, c, k)) SX_FATAL("fused batch grid does not fit the device");
     const int NA = (rows + SX_TILE - 1) / SX_TILE, NB = (c.N - 1 + SX_TILE - 1) / SX_TILE;
     k_batch<<<NA + NB, SX_TILE, batch_lds(k), s>>>(T, rows, ld, tl, c, d, d_save, base, st, pd.U, pd.F, pd.recs, pd.PM,
-                                                   pd.batch, k, NA, NB, chan, ga, gb, stamps, g_gather_wide,
-                                                   g_record_replicas);
+                                                   pd.batch, k, NA, NB, chan, ga, gb, stamps);
 }
 
 bool sx_batch_mr_fits(int slots, int nb_local, int k, int grids) {
@@ -2671,8 +2345,7 @@ void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld,
         SX_FATAL("multi-rank fused batch: bad shape");
     k_batch_mr<<<slots + (tb1 - tb0), SX_TILE, batch_lds(k), s>>>(T, rows, row0, rpr, ld, tl, c, d, d_save, base, st, pd.U, pd.F,
                                                                   pd.recs, pd.PM, pd.batch, k, slots, W, rank, tb0,
-                                                                  tb1, NBg, chan, ga, gb, gdone, pv, timeout,
-                                                                  g_gather_wide);
+                                                                  tb1, NBg, chan, ga, gb, gdone, pv, timeout);
 }
 
 void sx_launch_batch_mr_multi(const MrLaunchRank *ranks, int W, int rpr, size_t ld, TLay tl, Cols c, unsigned B, int k,
@@ -2708,8 +2381,7 @@ void sx_launch_batch_mr_multi(const MrLaunchRank *ranks, int W, int rpr, size_t 
         R.first[i + 1] = R.first[i] + slots + (q.tb1 - q.tb0);
     }
     for (int i = W + 1; i <= SX_MAXW; ++i) R.first[i] = R.first[W];
-    k_batch_mr_multi<<<R.first[W], SX_TILE, batch_lds(k), s>>>(R, rpr, ld, tl, c, B, k, slots, W, NBg, pv, timeout,
-                                                               g_gather_wide);
+    k_batch_mr_multi<<<R.first[W], SX_TILE, batch_lds(k), s>>>(R, rpr, ld, tl, c, B, k, slots, W, NBg, pv, timeout);
 }
 
 // every XCD's L2 writes back its dirty lines (blocks are dealt over all XCDs; each block's

@@ -3,12 +3,9 @@ W untimed + K timed phase-1 pivots; per pivot: wall time, sweep time (HIP events
 (the chain: the fused batch + slack exchanges), plus the in-kernel stamp breakdown of one batch.
 
 usage: python tools/chain_ab.py <setting>=<v1>,<v2> [config=config5,config3] [rounds=2]
-  settings: gather_wide (simplex_set_gather_wide), ld_pad (simplex_set_ld_pad),
-            replicas (simplex_set_record_replicas), sleep (simplex_set_poll_sleep),
-            regions (simplex_set_regions: 0 plain rows, 1 two-region layout),
-            sweep (rows per step:LDS stages, simplex_set_update_rows + simplex_set_sweep_stages;
-                   [:columns per thread, simplex_set_sweep_cols]; e.g. sweep=4:0,4:3,1:8,4:0:1 --
-                   stages 0 = the register sweep)"""
+  settings: regions (simplex_set_regions: 0 plain rows, 1 two-region layout),
+            rows (simplex_set_update_rows: rows per sweep step, 0 = auto),
+            waves (simplex_set_update_waves: the sweep's grid as a multiple of the resident blocks)"""
 import os
 import sys
 
@@ -44,24 +41,17 @@ def main():
     configs = args.pop("config", "config5,config3").split(",")
     rounds = int(args.pop("rounds", "2"))
     (name, vals), = args.items()
-    def set_sweep(v):
-        f = [int(x) for x in str(v).split(":")]
-        lib.simplex_set_update_rows(f[0])
-        lib.simplex_set_sweep_stages(f[1])
-        lib.simplex_set_sweep_cols(f[2] if len(f) > 2 else 2)
-
-    setter = {"gather_wide": lib.simplex_set_gather_wide, "ld_pad": lib.simplex_set_ld_pad,
-              "replicas": lib.simplex_set_record_replicas, "sweep": set_sweep,
-              "sleep": lib.simplex_set_poll_sleep, "regions": lib.simplex_set_regions,
-              "hist_fast": lib.simplex_set_hist_fast}[name]
-    reset = {"gather_wide": 1, "ld_pad": 0, "replicas": 1, "sweep": "0:0", "sleep": 1, "regions": 1, "hist_fast": 1}[name]
+    setter = {"regions": lambda v: lib.simplex_set_regions(int(v)),
+              "rows": lambda v: lib.simplex_set_update_rows(int(v)),
+              "waves": lambda v: lib.simplex_set_update_waves(float(v))}[name]
+    reset = {"regions": 1, "rows": 0, "waves": 0}[name]
     print("stamps (us): ratio compute | ratio argmin+publish | -> selection seen | pass2 + row details |"
           " row compute | obj argmin+publish | -> entering seen | entering history | pivot")
     for r in range(rounds):
         for cfg in configs:
             n, m, seed = bench.CONFIGS[cfg]
             for v in vals.split(","):
-                setter(v if name == "sweep" else int(v))
+                setter(v)
                 s = sx.Session(generated=(n, m, seed, 1, 100))
                 s.pivots(64)
                 tim = s.pivots(PIVOTS[cfg], time_updates=1)
