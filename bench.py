@@ -11,9 +11,13 @@ steps, then K timed steps: by default pivots 64..2080 of phase 1 (SURVEY.md §8d
 curve is the first 2000 phase-1 pivots).  Every timed step is a full batch, so the timed
 window runs exactly the kernels the warmup ran.
 
-N GPUs (torchrun, one process per GPU): the constraint rows are split into N contiguous
-512-aligned blocks, each rank sweeps only its rows; per pivot the ranks exchange the tile
-winners and the pivot row (peer memory over xGMI inside one launch per batch, or RCCL).
+N GPUs: the constraint rows are split into N contiguous 512-aligned blocks, each GPU sweeps only
+its rows; per pivot the shards exchange the tile winners and the pivot row (peer memory over
+xGMI inside one launch per GPU per batch, or per-pivot collectives).  Two launch forms:
+  * torchrun (WORLD_SIZE > 1; the driver's form): one process per GPU, RCCL communicator;
+  * `python bench.py --gpus N` without torchrun: ONE process drives GPUs 0..N-1 through the
+    library's SIMPLEX_GPUS mode (the drop-in's own multi-GPU form); it exits
+    non-zero when fewer than N GPUs are visible.
 The problem is the same at every N ("strong" scaling).
 
 Secondary (same JSON line): config 3, the reference's own 8192 x 4096 -t instance, whose
@@ -132,6 +136,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.gpus not in (1, world):
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} processes", file=sys.stderr)
+        sys.exit(2)
+    single_process_gpus = world == 1 and args.gpus > 1
+    if single_process_gpus:
+        visible = torch.cuda.device_count()  # (counts devices without initialising them)
+        if visible < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, {visible} visible", file=sys.stderr)
+            sys.exit(2)
+    n_gpus = world if world > 1 else max(args.gpus, 1)
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -143,6 +157,8 @@ def main():
         sxdist.init_from_torch(local_rank)
     else:
         sx.load().simplex_set_device(local_rank)
+        if single_process_gpus:
+            sx.set_gpus(list(range(args.gpus)))
     sx.set_update_rows(args.update_rows)
     sx.set_batch(args.batch)
 
@@ -173,13 +189,24 @@ def main():
             tt = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             elapsed = float(tt.item())
+        # per-rank split of the pivot time: this rank's timed sweeps vs the rest (the chain: the
+        # fused batches, slack exchanges and launch gaps), from its own HIP events
+        mine = {"rank": rank, "rows": tim.local_rows, "pivots": tim.pivots,
+                "us_per_pivot": tim.wall_ms * 1e3 / max(tim.pivots, 1),
+                "sweep_us_per_pivot": tim.update_ms * 1e3 / max(tim.pivots, 1),
+                "chain_us_per_pivot": (tim.wall_ms - tim.update_ms) * 1e3 / max(tim.pivots, 1)}
+        if world > 1:
+            per_rank = [None] * world
+            dist.all_gather_object(per_rank, mine)
+        else:
+            per_rank = [mine]
         sess.close()
         avg_update_s = tim.update_ms / 1e3 / max(tim.update_launches, 1)
         # algorithmic bytes of a sweep: every stored tableau element it moves, read and written once
         achieved = tim.swept_bytes / (tim.update_ms / 1e3) / 1e9 if tim.update_launches else None
         return {"n": n, "m": m, "seed": seed, "tim": tim, "elapsed": elapsed, "pivots": tim.pivots,
                 "avg_update_s": avg_update_s, "achieved": achieved, "setup_s": t_setup,
-                "steps": steps, "warmup": warmup}
+                "steps": steps, "warmup": warmup, "per_rank": per_rank}
 
     def roofline(cfg, r):
         tim, achieved = r["tim"], r["achieved"]
@@ -213,6 +240,15 @@ def main():
             "sweep_share_of_time": tim.update_ms / max(tim.wall_ms, 1e-9),
         }
 
+    def exchange_name():
+        if n_gpus == 1:
+            return "none (one shard)"
+        if world > 1:
+            return ("peer-memory fused batch (xGMI)" if sx.p2p_ready() else
+                    "per-pivot RCCL collectives (FALLBACK: the peer-memory self-check failed; slower than 1 GPU)")
+        return ("peer-memory fused batch, one launch per GPU (xGMI)" if sx.load().simplex_p2p_ready() else
+                "per-pivot device copies (FALLBACK: the peer-memory self-check failed)")
+
     def workload(cfg, r):
         return (f"{cfg}: phase-1 pivots, {r['m']}x{1 + r['n'] + 2 * r['m']} fp64 tableau "
                 f"(m={r['m']}, n={r['n']}, seed={r['seed']})")
@@ -223,10 +259,11 @@ def main():
         "metric": "simplex pivots/sec + HBM GB/s on gaussian update, dense m×n tableau",
         "value": pivots / elapsed,
         "unit": "pivots/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / max(args.steps, 1),
+        "ms_per_pivot": elapsed * 1e3 / max(pivots, 1),
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": (pivots / elapsed) / REF_PIVOTS_PER_S[args.config] if args.config in REF_PIVOTS_PER_S else None,
@@ -238,10 +275,12 @@ def main():
             "step": f"one batch of {K} pivots + one sweep of the tableau",
             "pivots_per_step": K,
             "m": m, "n": n, "seed": seed, "tableau_width": tim.width, "stored_width": tim.stored_width,
-            "rows_per_gpu_rank0": tim.local_rows, "parallelism": f"row-block x{world}",
-            "exchange": ("none (one shard)" if world == 1 else
-                         "peer-memory fused batch (xGMI)" if sx.p2p_ready() else
-                         "per-pivot RCCL collectives (FALLBACK: the peer-memory self-check failed; slower than 1 GPU)"),
+            "rows_per_gpu_rank0": tim.local_rows, "parallelism": f"row-block x{n_gpus}",
+            "launch": ("one process per GPU (torchrun, RCCL)" if world > 1 else
+                       f"one process driving GPUs 0..{n_gpus - 1} (SIMPLEX_GPUS)" if single_process_gpus else
+                       "one process, one GPU"),
+            "exchange": exchange_name(),
+            "per_rank": r["per_rank"],
             "pivots_timed": pivots, "first_timed_pivot": args.warmup * K, "status_after": tim.status,
             "setup_s": r["setup_s"],
         },
@@ -261,7 +300,7 @@ def main():
             "status_after": r2["tim"].status, "rows_per_gpu_rank0": r2["tim"].local_rows, "setup_s": r2["setup_s"],
             "roofline": roofline(args.secondary, r2),
         }
-    if world == 1 and not args.no_update_bench:
+    if n_gpus == 1 and not args.no_update_bench:
         # SURVEY.md §8d config 3': the sweep kernel alone on a synthetic 4096 x 8192 fp64 matrix
         # (uniform [1,100], seed 823296) with 32 random pending pivots
         # (three runs of 10 untimed + 50 timed sweeps each; the median run is reported -- the
@@ -277,14 +316,17 @@ def main():
             "frac": gbs / HBM_PEAK_GBS, "per_pivot_equivalent_us": us / 32,
             "note": "the matrix (268 MB) is about the size of the 256 MB Infinity Cache, so sweeps partly hit it",
         }
-    if world == 1 and args.full_solves:
+    if args.full_solves:
         # the whole drop-in call, as main.cu -t times it: build + both phases + solution (problem
         # synthesised on the GPU and copied to the host first, outside the clock)
+        # (at N GPUs: the whole solve on N row-block shards -- every rank calls twoPhaseMethod with
+        # the whole problem and builds its own rows)
         out["full_solve"] = []
         for name in [c for c in args.full_solves.split(",") if c]:
             fn, fm, fseed = CONFIGS[name]
             prob = sx.generateRandomProblemDevice(fn, fm, fseed, 1, 100)
             torch.cuda.synchronize()
+            barrier()
             t0 = time.perf_counter()
             res = sx.twoPhaseMethodEx(prob)
             dt = time.perf_counter() - t0
@@ -303,7 +345,7 @@ def main():
                 full["reference_pivots"] = REF_SOLVE[name]["pivots"]
                 full["pivots_match_reference"] = list(res.pivots) == REF_SOLVE[name]["pivots"]
             out["full_solve"].append(full)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, m, seed, CPU_SAMPLE[args.config], sx)
     if rank == 0:
         print(json.dumps(out), flush=True)

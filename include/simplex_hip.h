@@ -42,6 +42,17 @@ int simplex_dist_finalize(void);
 /* single-process emulation of W row-block shards on the current device (collectives are
  * device copies); used to test the sharded path on one GPU. 0 or 1 disables. */
 void simplex_set_virtual_ranks(int world);
+/* ---- multi-GPU inside ONE process: the caller still makes one synchronous
+ * twoPhaseMethod / solve call.  The constraint rows are split into count 512-aligned blocks, one
+ * per listed device (a device may repeat); the shards hand off through peer memory (one fused
+ * launch per device per batch of pivots) when a start-up self-check on the list passes, else
+ * through per-pivot device copies.  Without this call the environment variable SIMPLEX_GPUS
+ * decides: "N" = devices 0..N-1, or a comma list ("0,1,2,3").  count <= 1 (or no list): one
+ * shard.  A device that is not visible is a fatal error (error.cu:5-12 convention). */
+void simplex_set_gpus(const int *devices, int count);
+/* the device list in effect (simplex_set_gpus, else SIMPLEX_GPUS); returns its length and
+ * copies up to cap entries */
+int simplex_gpus(int *devices, int cap);
 /* run the multi-shard exchange path (tile allgather + pivot-row allreduce) even with a
  * single shard; with simplex_dist_init(.., world=1, ..) it goes through a 1-rank RCCL
  * communicator.  Test hook. */
@@ -171,6 +182,10 @@ int simplex_ipc_handles_size(void);
 simplex_session *simplex_ipc_session_open(int n, int m, int rank, int world, const double *T_rows, long long ld_host,
                                           const double *d, const int *base, unsigned char *handles_out);
 int simplex_ipc_session_connect(simplex_session *s, const unsigned char *all_handles);
+/* after every process's pivots: write this rank's slice of the objective row into every peer's
+ * (between fused batches each rank keeps only its own slice current); barrier the processes
+ * before and after.  Returns 0, or -1 for a session that is not in IPC mode. */
+int simplex_session_sync_d(simplex_session *s);
 /* this process's rows of the resident tableau (logical columns), d and base; returns rows */
 long long simplex_session_rows(simplex_session *s, double *T_rows, long long ld_host, double *d, int *base);
 

@@ -8,8 +8,8 @@ from .api import (  # noqa: F401
     DEGENERATE, FEASIBLE, HANG, INFEASIBLE, NOT_ENDED, NUMERIC_FAIL, PIVOT_CAP, RAND_GLIBC, RAND_MSVC,
     STATUS_NAMES, UNBOUNDED, Problem, Result, Session, bench_sweep, dev_argmin, dev_build_phase1,
     dev_build_phase1_generated, dev_pivots, dev_update_objective, generateRandomProblem,
-    generateRandomProblemDevice, p2p_ready, printProblemToStream, readProblemFromFile, readRandomProblemFromFile,
+    generateRandomProblemDevice, gpus, p2p_ready, printProblemToStream, readProblemFromFile, readRandomProblemFromFile,
     set_alias, set_batch, set_compact, set_exchange_mode, set_force_exchange, set_fused, set_mr_single_launch,
-    set_p2p, set_regions, set_store_sc1, set_update_rows, set_update_waves, set_verbose, set_virtual_ranks,
+    set_gpus, set_p2p, set_regions, set_store_sc1, set_update_rows, set_update_waves, set_verbose, set_virtual_ranks,
     twoPhaseMethod, twoPhaseMethodEx)
 from ._lib import LIB_PATH, load  # noqa: F401

@@ -92,6 +92,8 @@ SIGNATURES = {
     "simplex_dist_init": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
     "simplex_dist_finalize": (ctypes.c_int, []),
     "simplex_set_virtual_ranks": (None, [ctypes.c_int]),
+    "simplex_set_gpus": (None, [c_int_p, ctypes.c_int]),
+    "simplex_gpus": (ctypes.c_int, [c_int_p, ctypes.c_int]),
     "simplex_set_force_exchange": (None, [ctypes.c_int]),
     "simplex_set_exchange_mode": (None, [ctypes.c_int]),
     "simplex_set_alias": (None, [ctypes.c_int]),
@@ -136,6 +138,7 @@ SIGNATURES = {
     "simplex_ipc_session_open": (ctypes.c_void_p, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_double_p,
                                                    ctypes.c_longlong, c_double_p, c_int_p, ctypes.c_char_p]),
     "simplex_ipc_session_connect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),
+    "simplex_session_sync_d": (ctypes.c_int, [ctypes.c_void_p]),
     "simplex_session_rows": (ctypes.c_longlong, [ctypes.c_void_p, c_double_p, ctypes.c_longlong, c_double_p,
                                                  c_int_p]),
     "simplex_bench_sweep": (ctypes.c_double, [ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_int, ctypes.c_int,

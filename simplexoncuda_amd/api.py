@@ -302,6 +302,23 @@ def set_virtual_ranks(w):
     _lib.load().simplex_set_virtual_ranks(int(w))
 
 
+def set_gpus(devices):
+    """One process, several GPUs (simplex_set_gpus): one row-block shard per listed device
+    (None or [] = the SIMPLEX_GPUS environment variable decides)."""
+    devs = list(devices or [])
+    arr = (ctypes.c_int * max(len(devs), 1))(*devs)
+    _lib.load().simplex_set_gpus(arr, len(devs))
+
+
+def gpus():
+    """The device list in effect (simplex_set_gpus, else SIMPLEX_GPUS); [] = one shard."""
+    lib = _lib.load()
+    n = lib.simplex_gpus(None, 0)
+    arr = (ctypes.c_int * max(n, 1))()
+    lib.simplex_gpus(arr, n)
+    return list(arr[:n])
+
+
 def set_force_exchange(on):
     _lib.load().simplex_set_force_exchange(1 if on else 0)
 

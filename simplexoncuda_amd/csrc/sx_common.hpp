@@ -187,7 +187,7 @@ void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld,
                         BatchChan *chan, const unsigned long long *ga, const unsigned long long *gb,
                         const unsigned long long *gdone, const PeerView &pv, unsigned long long timeout,
                         hipStream_t s);
-// all W virtual ranks' batches (ranks on one GPU) as one launch
+// one rank of a multi-rank launch
 struct MrLaunchRank {
     const double *T;
     int rows, row0, rank, tb0, tb1;
@@ -199,12 +199,15 @@ struct MrLaunchRank {
     BatchChan *chan;
     const unsigned long long *ga, *gb, *gdone;
 };
-void sx_launch_batch_mr_multi(const MrLaunchRank *ranks, int W, int rpr, size_t ld, TLay tl, Cols c, unsigned B, int k,
-                              int slots, const PeerView &pv, unsigned long long timeout, hipStream_t s);
+// the batches of the nloc ranks (of W) that share one GPU, as one launch
+void sx_launch_batch_mr_multi(const MrLaunchRank *ranks, int nloc, int W, int rpr, size_t ld, TLay tl, Cols c, unsigned B,
+                              int k, int slots, const PeerView &pv, unsigned long long timeout, hipStream_t s);
 void sx_set_update_waves(float w);  // resident-grid multiple of the sweep (default 1)
 void sx_set_sweep_record(int *rec);  // next sweeps write (batch tag, count, nact) to rec[0..2] (null: off)
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s);
 void sx_launch_l2_writeback(hipStream_t s);  // every XCD's L2 writes back its dirty lines
+// a rank's contribution to the objective-row gather: d on [j0, j1) (and d[0] if with0), -0.0 elsewhere
+void sx_launch_d_contrib(const double *d, double *out, int N, int j0, int j1, int with0, hipStream_t s);
 
 void sx_launch_coef(const double *d, const int *base, int row0, int rows, double *coef, hipStream_t s);
 void sx_launch_gemv_partials(const double *T, int rows, TLay tl, int Ns, const double *coef, double *partials,

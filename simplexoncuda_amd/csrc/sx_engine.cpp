@@ -58,6 +58,7 @@ struct Config {
     int batch = 32;          // pivots per tableau sweep (deferred updates), 1..SX_KMAX
     int device = -1;
     int virtual_ranks = 1;
+    std::vector<int> gpus;   // simplex_set_gpus: one process, one row-block shard per listed device
     int force_exchange = 0;  // run the multi-shard exchange path even with one shard
     std::string timer_dir;   // non-empty: write the reference's TIMER CSV there
     int exchange_mode = 0;   // 0 auto, 1 tile allgather + row allreduce, 2 row-gather
@@ -69,6 +70,7 @@ struct Config {
     int fused = -1;          // whole batches in one resident launch: -1 auto (one shard), 0 off
     int p2p = -1;            // several shards: fused batches exchanging over peer memory: -1 auto, 0 off, 1 force
     bool p2p_ready = false;  // RCCL ranks: the peer-memory path passed the start-up self-check
+    std::map<std::vector<int>, bool> p2p_checked;  // one process, several GPUs: self-check result per device list
     int debug = -1;          // -1: from SIMPLEX_DEBUG; 1: print the tableau after every step
     bool benchmark = false;
     bool no_timer = false;         // the multi-GPU self-check: never write TIMER CSVs
@@ -95,11 +97,15 @@ std::mutex g_mu;
 // in order).  So the uncached records are allocated once per process (after an
 // L2 write-back, so no dirty line of the pages' earlier cached use lands on them later) and
 // never freed; everything else, virtual shards included, uses plain device memory.
+// A pool of such sets, one per (device, concurrent engine): a second engine alive at the same
+// time (or a second shard on the device) takes another set instead of falling back to cached
+// memory.
 struct UncachedRecords {
+    int dev = -1;
     unsigned long long *ga = nullptr, *gb = nullptr, *gdone = nullptr;
     bool busy = false;
 };
-UncachedRecords g_urec;
+std::vector<UncachedRecords> g_urec;
 
 void say(const char *s) {
     if (g_cfg.verbose) {
@@ -177,6 +183,55 @@ struct Chrono {
     }
 };
 
+// Devices of a one-process multi-GPU engine ("Multi-GPU is internal: the caller
+// still sees one synchronous call; the device list comes from SIMPLEX_GPUS"): simplex_set_gpus,
+// else SIMPLEX_GPUS = "N" (devices 0..N-1) or a comma list ("0,1,2,3"; a device may repeat:
+// several shards on one GPU).  Empty: one shard on the current device.
+std::vector<int> shard_devices() {
+    std::vector<int> v = g_cfg.gpus;
+    if (v.empty()) {
+        const char *e = getenv("SIMPLEX_GPUS");
+        if (e == nullptr || *e == 0) return v;
+        if (strchr(e, ',') == nullptr) {
+            const int n = atoi(e);
+            for (int i = 0; i < n; ++i) v.push_back(i);
+        } else {
+            for (const char *p = e; *p;) {
+                v.push_back(atoi(p));
+                const char *c = strchr(p, ',');
+                if (c == nullptr) break;
+                p = c + 1;
+            }
+        }
+    }
+    if (v.size() <= 1) return v;
+    if ((int)v.size() > SX_MAXW) SX_FATAL("SIMPLEX_GPUS: at most 8 shards");
+    int count = 0;
+    SX_HIP(hipGetDeviceCount(&count));
+    for (int d : v)
+        if (d < 0 || d >= count) {
+            char msg[128];
+            snprintf(msg, sizeof(msg), "SIMPLEX_GPUS: device %d requested but %d visible", d, count);
+            SX_FATAL(msg);
+        }
+    return v;
+}
+
+bool gpus_selftest(const std::vector<int> &devs);  // (below two_phase)
+
+// makes `dev` current for its scope
+struct DevGuard {
+    int prev = -1;
+    explicit DevGuard(int dev) {
+        SX_HIP(hipGetDevice(&prev));
+        if (dev != prev) SX_HIP(hipSetDevice(dev));
+        else prev = -1;
+    }
+    ~DevGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
 // ------------------------------------------------------------------ shard + engine
 struct Shard {
     int rank = 0;
@@ -185,6 +240,7 @@ struct Shard {
     double *T = nullptr;
     double *d = nullptr;
     double *d_save = nullptr;         // fused batch: d as the batch found it (restored after SX_HANG)
+    double *dx = nullptr;             // RCCL ranks: this rank's objective-row slice, -0.0 elsewhere (gather_d)
     double *colE = nullptr;
     double *prow = nullptr;
     double *prow_send = nullptr;
@@ -212,7 +268,9 @@ struct Shard {
     unsigned long long *gb = nullptr; // fused batch kernel: objective-tile records (tagged granules)
     unsigned long long *gdone = nullptr;  // multi-rank fused batch: batch-end done granules (one per rank)
     hipStream_t ss = nullptr;         // virtual shards: the stream its multi-rank fused batch runs on
-    bool uncached = false;            // ga / gb / gdone allocated uncached (polled across devices / XCDs)
+    int dev = 0;                      // the device holding the shard's buffers
+    hipStream_t s = nullptr;          // the engine's stream on that device (every per-shard operation)
+    int urec = -1;                    // ga / gb / gdone: index of the uncached record set (g_urec), or -1
     DevState *st = nullptr;
 };
 
@@ -233,10 +291,15 @@ class Engine {
     TLay tl;               // T's storage regions (sx_common.hpp)
     int rpr = 0;           // rows per rank (multiple of 512)
     int slots = 0;         // argmin tiles / GEMV blocks per rank
-    int device = 0;
-    hipStream_t s = nullptr;
+    int device = 0;        // the primary device (shard 0's)
+    hipStream_t s = nullptr;  // the engine stream on the primary device
+    bool gpus_mode = false;   // one process, one shard per listed device (SIMPLEX_GPUS / simplex_set_gpus)
+    bool multidev = false;    // ... on more than one device
+    std::vector<int> shard_dev;            // gpus_mode: the device of each shard
+    std::map<int, hipStream_t> dstream;    // the engine stream of every device in use (s on the primary)
+    std::map<int, hipEvent_t> djoin;       // multidev: one join event per device stream
     std::vector<Shard> sh;
-    const double **sum_srcs = nullptr;  // device array of prow_send pointers (virtual ranks)
+    const double **sum_srcs = nullptr;  // pinned host array of prow_send pointers (virtual ranks)
     DevState *st_host = nullptr;        // pinned: 2 poll slots
     hipEvent_t poll_ev[2] = {nullptr, nullptr};
     double *c_dev = nullptr;            // objective coefficients c (phase 2)
@@ -257,22 +320,35 @@ class Engine {
         Ns1 = alias ? N2 : N1;
         ld = round_up((size_t)Ns1, 16);
         batch_id = (g_cfg.first_batch_id >= 1 && g_cfg.first_batch_id < SX_BATCH_IDS) ? g_cfg.first_batch_id : 1;
+        std::vector<int> devs;  // one process, several GPUs: the device of every shard
         if (g_cfg.ipc_world > 1) {
             rccl = ipc = true;
             W = g_cfg.ipc_world;
         } else if (g_cfg.dist && g_cfg.comm) {
             rccl = true;
             W = g_cfg.world;
+        } else if ((devs = shard_devices()).size() > 1) {
+            W = (int)devs.size();
+            gpus_mode = true;
         } else if (g_cfg.virtual_ranks > 1) {
             W = g_cfg.virtual_ranks;
         }
         xchg = W > 1 || g_cfg.force_exchange;
         slot_stride = ld + 2;
         int dev = 0;
-        if (g_cfg.device >= 0) SX_HIP(hipSetDevice(g_cfg.device));
+        if (gpus_mode)
+            SX_HIP(hipSetDevice(devs[0]));
+        else if (g_cfg.device >= 0)
+            SX_HIP(hipSetDevice(g_cfg.device));
         SX_HIP(hipGetDevice(&dev));
         device = dev;
         SX_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        dstream[device] = s;
+        if (gpus_mode) {
+            for (int d : devs) multidev = multidev || d != device;
+            shard_dev = devs;
+            if (multidev) open_devices();
+        }
         rpr = (int)round_up((size_t)((m + W - 1) / W), SX_TILE);
         if (rpr == 0) rpr = SX_TILE;
         slots = rpr / SX_TILE;
@@ -309,18 +385,76 @@ class Engine {
             x.rows = m - x.row0;
             if (x.rows < 0) x.rows = 0;
             if (x.rows > rpr) x.rows = rpr;
+            x.dev = gpus_mode ? shard_dev[(size_t)k] : device;
+            x.s = dstream[x.dev];
+            DevGuard g(x.dev);
             alloc_shard(x);
             sh.push_back(x);
         }
         if (!rccl && xchg) {
-            std::vector<const double *> ptrs;
-            for (auto &x : sh) ptrs.push_back(x.prow_send);
-            sum_srcs = dalloc<const double *>(W);
-            SX_HIP(hipMemcpy(sum_srcs, ptrs.data(), sizeof(double *) * W, hipMemcpyHostToDevice));
+            // the shards' pivot-row contributions (pinned host memory: read by every device's kernel)
+            SX_HIP(hipHostMalloc(reinterpret_cast<void **>(&sum_srcs), sizeof(double *) * W, hipHostMallocDefault));
+            for (int k = 0; k < W; ++k) sum_srcs[k] = sh[(size_t)k].prow_send;
         }
         SX_HIP(hipHostMalloc(reinterpret_cast<void **>(&st_host), 2 * sizeof(DevState), hipHostMallocDefault));
         for (auto &e : poll_ev) SX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         setup_peers();
+    }
+
+    // ---------------------------------------------------------------- one process, several devices
+    // peer access between every pair of the shards' devices, one engine stream and one join event
+    // per device
+    void open_devices() {
+        std::vector<int> ds;
+        for (int d : shard_dev)
+            if (std::find(ds.begin(), ds.end(), d) == ds.end()) ds.push_back(d);
+        for (int a : ds) {
+            DevGuard g(a);
+            for (int b : ds) {
+                if (a == b) continue;
+                int can = 0;
+                SX_HIP(hipDeviceCanAccessPeer(&can, a, b));
+                if (!can) {
+                    char msg[128];
+                    snprintf(msg, sizeof(msg), "SIMPLEX_GPUS: device %d cannot access device %d's memory", a, b);
+                    SX_FATAL(msg);
+                }
+                const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) SX_HIP(e);
+                (void)hipGetLastError();
+            }
+            if (!dstream.count(a)) {
+                hipStream_t st;
+                SX_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+                dstream[a] = st;
+            }
+            hipEvent_t ev;
+            SX_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            djoin[a] = ev;
+        }
+    }
+
+    // every device stream waits for the work enqueued so far on all of them (the shards'
+    // cross-device dependencies: collectives, gathers); a no-op on one device
+    void join() {
+        if (!multidev) return;
+        for (auto &kv : dstream) {
+            DevGuard g(kv.first);
+            SX_HIP(hipEventRecord(djoin[kv.first], kv.second));
+        }
+        for (auto &kv : dstream) {
+            DevGuard g(kv.first);
+            for (auto &ev : djoin)
+                if (ev.first != kv.first) SX_HIP(hipStreamWaitEvent(kv.second, ev.second, 0));
+        }
+    }
+
+    // the host waits for every device stream
+    void sync_all() {
+        for (auto &kv : dstream) {
+            DevGuard g(kv.first);
+            SX_HIP(hipStreamSynchronize(kv.second));
+        }
     }
 
     // ---------------------------------------------------------------- peer memory (multi-rank fused batch)
@@ -335,12 +469,15 @@ class Engine {
         if (ipc) return;  // the caller connects the peers (connect_peers)
         if (!xchg || W > SX_MAXW || g_cfg.p2p == 0) return;
         if (rccl && !(g_cfg.p2p == 1 || g_cfg.p2p_ready)) return;
-        SX_HIP(hipStreamSynchronize(s));
+        sync_all();
+        // one process, several GPUs (SIMPLEX_GPUS): when the start-up self-check passes (or p2p is
+        // forced); the batches run as one launch per device
+        if (gpus_mode && g_cfg.p2p != 1 && !gpus_selftest(shard_dev)) return;
         // virtual shards: only when asked for (a test hook); their batches run as one launch
         // (mr_single_launch), or as W launches on W streams for W <= 3 (the engine stream + W
         // streams on 4 hardware queues)
-        if (!rccl && (g_cfg.p2p != 1 || (W > 3 && !g_cfg.mr_single_launch))) return;
-        if (!rccl) {  // virtual shards: every shard's buffers on this device; one stream per shard
+        if (!rccl && !gpus_mode && (g_cfg.p2p != 1 || (W > 3 && !g_cfg.mr_single_launch))) return;
+        if (!rccl) {  // shards of this process: every shard's buffers mapped here; one stream per shard
             for (auto &x : sh) {
                 pv.T[x.rank] = x.T;
                 pv.ga[x.rank] = x.ga;
@@ -348,12 +485,13 @@ class Engine {
                 pv.gdone[x.rank] = x.gdone;
                 pv.U[x.rank] = x.U;
                 pv.d[x.rank] = x.d;
+                if (multidev) continue;  // (one launch per device on its engine stream)
                 SX_HIP(hipStreamCreateWithFlags(&x.ss, hipStreamNonBlocking));
                 hipEvent_t e;
                 SX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
                 ev_join.push_back(e);
             }
-            SX_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+            if (!multidev) SX_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
             p2p = true;
             return;
         }
@@ -457,20 +595,30 @@ class Engine {
     }
 
     ~Engine() {
-        (void)hipStreamSynchronize(s);
+        sync_all();
         close_peers();
         for (auto &x : sh)
             if (x.ss) (void)hipStreamDestroy(x.ss);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         for (auto &e : ev_join)
             if (e) (void)hipEventDestroy(e);
-        for (auto &x : sh) free_shard(x);
-        if (sum_srcs) (void)hipFree(sum_srcs);
+        for (auto &x : sh) {
+            DevGuard g(x.dev);
+            free_shard(x);
+        }
+        if (sum_srcs) (void)hipHostFree(sum_srcs);
         if (c_dev) (void)hipFree(c_dev);
         if (st_host) (void)hipHostFree(st_host);
         for (auto &e : poll_ev)
             if (e) (void)hipEventDestroy(e);
-        (void)hipStreamDestroy(s);
+        for (auto &kv : djoin) {
+            DevGuard g(kv.first);
+            (void)hipEventDestroy(kv.second);
+        }
+        for (auto &kv : dstream) {
+            DevGuard g(kv.first);
+            (void)hipStreamDestroy(kv.second);
+        }
     }
 
     // doubles of a shard's tableau allocation
@@ -478,6 +626,26 @@ class Engine {
         return tl.jB < Ns1 ? tl.offB + (size_t)rpr * tl.ldB : rows_alloc * ld;
     }
 
+    // a free uncached record set on `dev` (allocated, after an L2 write-back, the first time)
+    static int acquire_uncached_records(int dev, hipStream_t st) {
+        for (size_t i = 0; i < g_urec.size(); ++i)
+            if (g_urec[i].dev == dev && !g_urec[i].busy) {
+                g_urec[i].busy = true;
+                return (int)i;
+            }
+        UncachedRecords u;
+        u.dev = dev;
+        sx_launch_l2_writeback(st);
+        SX_HIP(hipStreamSynchronize(st));
+        SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&u.ga), sx_batch_granules_a() * 8, hipDeviceMallocUncached));
+        SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&u.gb), sx_batch_granules_b() * 8, hipDeviceMallocUncached));
+        SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&u.gdone), SX_MAXW * 8, hipDeviceMallocUncached));
+        u.busy = true;
+        g_urec.push_back(u);
+        return (int)g_urec.size() - 1;
+    }
+
+    // (on the shard's device)
     void alloc_shard(Shard &x) {
         const size_t rows_alloc = x.rows > 0 ? (size_t)x.rows : 1;
         x.T = dalloc<double>(t_doubles(rows_alloc));
@@ -517,49 +685,38 @@ class Engine {
         x.F = dalloc<double>(rows_alloc * SX_KMAX);
         x.recs = dalloc<PivRec>(SX_KMAX);
         x.PM = dalloc<unsigned long long>(rows_alloc);
-        SX_HIP(hipMemsetAsync(x.U, 0, (size_t)SX_KMAX * ld * sizeof(double), s));
-        SX_HIP(hipMemsetAsync(x.F, 0, rows_alloc * SX_KMAX * sizeof(double), s));
-        SX_HIP(hipMemsetAsync(x.recs, 0, SX_KMAX * sizeof(PivRec), s));
-        SX_HIP(hipMemsetAsync(x.PM, 0, rows_alloc * sizeof(unsigned long long), s));
+        SX_HIP(hipMemsetAsync(x.U, 0, (size_t)SX_KMAX * ld * sizeof(double), x.s));
+        SX_HIP(hipMemsetAsync(x.F, 0, rows_alloc * SX_KMAX * sizeof(double), x.s));
+        SX_HIP(hipMemsetAsync(x.recs, 0, SX_KMAX * sizeof(PivRec), x.s));
+        SX_HIP(hipMemsetAsync(x.PM, 0, rows_alloc * sizeof(unsigned long long), x.s));
         x.coef = dalloc<double>(rows_alloc);
         x.rhs_local = dalloc<double>(rpr);
         if (xchg) x.rhs_all = dalloc<double>((size_t)W * rpr);
         x.base = dalloc<int>(m);
         x.enter_parts = dalloc<TilePart>(SX_TILE);
         x.chan = dalloc<BatchChan>(1);
-        if (rccl && !ipc && !g_urec.busy) {
-            // polled while other GPUs write them: the process's uncached records (g_urec)
-            if (!g_urec.ga) {
-                sx_launch_l2_writeback(s);
-                SX_HIP(hipStreamSynchronize(s));
-                SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&g_urec.ga), sx_batch_granules_a() * 8,
-                                             hipDeviceMallocUncached));
-                SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&g_urec.gb), sx_batch_granules_b() * 8,
-                                             hipDeviceMallocUncached));
-                SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&g_urec.gdone), SX_MAXW * 8,
-                                             hipDeviceMallocUncached));
-            }
-            g_urec.busy = true;
-            x.uncached = true;
-            x.ga = g_urec.ga;
-            x.gb = g_urec.gb;
-            x.gdone = g_urec.gdone;
+        if ((rccl && !ipc) || multidev) {
+            // polled while other GPUs write them: one of the process's uncached record sets
+            x.urec = acquire_uncached_records(x.dev, x.s);
+            x.ga = g_urec[(size_t)x.urec].ga;
+            x.gb = g_urec[(size_t)x.urec].gb;
+            x.gdone = g_urec[(size_t)x.urec].gdone;
         } else {
             // one device (virtual shards, processes sharing a GPU): plain memory, sc1 hand-offs
             x.ga = dalloc<unsigned long long>(sx_batch_granules_a());
             x.gb = dalloc<unsigned long long>(sx_batch_granules_b());
             if (xchg) x.gdone = dalloc<unsigned long long>(SX_MAXW);
         }
-        if (x.gdone) SX_HIP(hipMemsetAsync(x.gdone, 0, SX_MAXW * 8, s));
-        SX_HIP(hipMemsetAsync(x.chan, 0, sizeof(BatchChan), s));
-        SX_HIP(hipMemsetAsync(x.ga, 0, sx_batch_granules_a() * sizeof(unsigned long long), s));
-        SX_HIP(hipMemsetAsync(x.gb, 0, sx_batch_granules_b() * sizeof(unsigned long long), s));
+        if (x.gdone) SX_HIP(hipMemsetAsync(x.gdone, 0, SX_MAXW * 8, x.s));
+        SX_HIP(hipMemsetAsync(x.chan, 0, sizeof(BatchChan), x.s));
+        SX_HIP(hipMemsetAsync(x.ga, 0, sx_batch_granules_a() * sizeof(unsigned long long), x.s));
+        SX_HIP(hipMemsetAsync(x.gb, 0, sx_batch_granules_b() * sizeof(unsigned long long), x.s));
         x.tiles_local = dalloc<TilePart>(slots);
         if (xchg) x.tiles_all = dalloc<TilePart>((size_t)W * slots);
         x.st = dalloc<DevState>(1);
-        SX_HIP(hipMemsetAsync(x.T, 0, t_doubles(rows_alloc) * sizeof(double), s));
-        SX_HIP(hipMemsetAsync(x.d, 0, round_up((size_t)N1, 16) * sizeof(double), s));
-        SX_HIP(hipMemsetAsync(x.prow, 0, ld * sizeof(double), s));
+        SX_HIP(hipMemsetAsync(x.T, 0, t_doubles(rows_alloc) * sizeof(double), x.s));
+        SX_HIP(hipMemsetAsync(x.d, 0, round_up((size_t)N1, 16) * sizeof(double), x.s));
+        SX_HIP(hipMemsetAsync(x.prow, 0, ld * sizeof(double), x.s));
         // padding tile entries must read (DBL_MAX, -1, not eligible)
         std::vector<TilePart> pad((size_t)W * slots);
         for (auto &t : pad) {
@@ -573,11 +730,12 @@ class Engine {
     }
 
     void free_shard(Shard &x) {
-        if (x.uncached) {  // the process's uncached records stay allocated (g_urec)
+        if (x.urec >= 0) {  // the process's uncached records stay allocated (g_urec)
             x.ga = x.gb = x.gdone = nullptr;
-            g_urec.busy = false;
+            g_urec[(size_t)x.urec].busy = false;
+            x.urec = -1;
         }
-        for (void *p : {(void *)x.T, (void *)x.d, (void *)x.d_save, (void *)x.colE, (void *)x.prow, (void *)x.prow_send,
+        for (void *p : {(void *)x.T, (void *)x.d, (void *)x.d_save, (void *)x.dx, (void *)x.colE, (void *)x.prow, (void *)x.prow_send,
                         (void *)x.slot_send, (void *)x.slot_all, (void *)x.U, (void *)x.F, (void *)x.recs, (void *)x.PM,
                         (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
                         (void *)x.rhs_all, (void *)x.base, (void *)x.enter_parts, (void *)x.tiles_local, (void *)x.chan,
@@ -588,20 +746,23 @@ class Engine {
     }
 
     // ---------------------------------------------------------------- phase-1 tableau
-    // fillTableu (twoPhaseMethod.cu:145-200): each shard copies only its rows of A.
+    // fillTableu (twoPhaseMethod.cu:145-200): each shard copies only its rows of A.  (b and c
+    // live on the primary device; the other devices' kernels read them through peer access.)
     void build_phase1(const problem_t *P) {
         double *b_dev = dalloc<double>(m);
         SX_HIP(hipMemcpyAsync(b_dev, P->knownTermsVector, sizeof(double) * m, hipMemcpyHostToDevice, s));
+        SX_HIP(hipStreamSynchronize(s));
         for (auto &x : sh) {
+            DevGuard g(x.dev);
             double *A_local = nullptr;
             if (x.rows > 0 && n > 0) {
                 A_local = dalloc<double>((size_t)x.rows * n);
                 SX_HIP(hipMemcpy2DAsync(A_local, sizeof(double) * x.rows, P->constraintsMatrix + x.row0,
-                                        sizeof(double) * m, sizeof(double) * x.rows, n, hipMemcpyHostToDevice, s));
+                                        sizeof(double) * m, sizeof(double) * x.rows, n, hipMemcpyHostToDevice, x.s));
             }
-            sx_launch_build_rows(x.T, x.rows, x.row0, tl, n, m, Ns1, A_local, b_dev, s);
-            sx_launch_init_vectors(x.d, N1, n, m, x.base, s);
-            SX_HIP(hipStreamSynchronize(s));
+            sx_launch_build_rows(x.T, x.rows, x.row0, tl, n, m, Ns1, A_local, b_dev, x.s);
+            sx_launch_init_vectors(x.d, N1, n, m, x.base, x.s);
+            SX_HIP(hipStreamSynchronize(x.s));
             if (A_local) (void)hipFree(A_local);
         }
         (void)hipFree(b_dev);
@@ -624,27 +785,36 @@ class Engine {
         sx_launch_gen_vector(sd[0], 0, m, lo, hi, b_dev, s);
         if (!c_dev) c_dev = dalloc<double>(n);
         sx_launch_gen_vector(sd[1], 0, n, lo, hi, c_dev, s);
-        for (auto &x : sh) {
-            sx_launch_gen_rows(sd[2], n, m, x.row0, x.rows, lo, hi, x.T, tl.ldA, nullptr, s);  // (region A)
-            sx_launch_build_rows(x.T, x.rows, x.row0, tl, n, m, Ns1, nullptr, b_dev, s);
-            sx_launch_init_vectors(x.d, N1, n, m, x.base, s);
-        }
         SX_HIP(hipStreamSynchronize(s));
+        for (auto &x : sh) {
+            DevGuard g(x.dev);
+            sx_launch_gen_rows(sd[2], n, m, x.row0, x.rows, lo, hi, x.T, tl.ldA, nullptr, x.s);  // (region A)
+            sx_launch_build_rows(x.T, x.rows, x.row0, tl, n, m, Ns1, nullptr, b_dev, x.s);
+            sx_launch_init_vectors(x.d, N1, n, m, x.base, x.s);
+        }
+        sync_all();
         (void)hipFree(b_dev);
         set_compact(lo >= 0);  // b in [lo, hi]: no row negated
     }
 
     // ---------------------------------------------------------------- collectives
+    // Shards of this process (virtual shards, or one per GPU): device copies between their
+    // buffers, after a join of the device streams (and before the next, so every device sees
+    // the result); RCCL ranks: one collective on the engine stream.
     void allgather_tiles() {
         if (rccl) {
             Shard &x = sh[0];
             SX_NCCL(ncclAllGather(x.tiles_local, x.tiles_all, sizeof(TilePart) * slots, ncclUint8, g_cfg.comm, s));
             return;
         }
-        for (auto &dst : sh)
+        join();
+        for (auto &dst : sh) {
+            DevGuard g(dst.dev);
             for (auto &src : sh)
                 SX_HIP(hipMemcpyAsync(dst.tiles_all + (size_t)src.rank * slots, src.tiles_local,
-                                      sizeof(TilePart) * slots, hipMemcpyDeviceToDevice, s));
+                                      sizeof(TilePart) * slots, hipMemcpyDeviceToDevice, dst.s));
+        }
+        join();
     }
 
     void allgather_slots() {
@@ -654,10 +824,14 @@ class Engine {
             SX_NCCL(ncclAllGather(x.slot_send, x.slot_all, count, ncclDouble, g_cfg.comm, s));
             return;
         }
-        for (auto &dst : sh)
+        join();
+        for (auto &dst : sh) {
+            DevGuard g(dst.dev);
             for (auto &src : sh)
                 SX_HIP(hipMemcpyAsync(dst.slot_all + (size_t)src.rank * count, src.slot_send, sizeof(double) * count,
-                                      hipMemcpyDeviceToDevice, s));
+                                      hipMemcpyDeviceToDevice, dst.s));
+        }
+        join();
     }
 
     void allreduce_prow() {
@@ -666,7 +840,12 @@ class Engine {
             SX_NCCL(ncclAllReduce(x.prow_send, x.prow, cols(N).Ns, ncclDouble, ncclSum, g_cfg.comm, s));
             return;
         }
-        for (auto &dst : sh) sx_launch_sum_rows(dst.prow, sum_srcs, W, cols(N).Ns, s);
+        join();
+        for (auto &dst : sh) {
+            DevGuard g(dst.dev);
+            sx_launch_sum_rows(dst.prow, sum_srcs, W, cols(N).Ns, dst.s);
+        }
+        join();
     }
 
     void allgather_doubles(double *Shard::*local, double *Shard::*all, size_t count) {
@@ -675,31 +854,106 @@ class Engine {
             SX_NCCL(ncclAllGather(x.*local, x.*all, count, ncclDouble, g_cfg.comm, s));
             return;
         }
-        for (auto &dst : sh)
+        join();
+        for (auto &dst : sh) {
+            DevGuard g(dst.dev);
             for (auto &src : sh)
                 SX_HIP(hipMemcpyAsync(dst.*all + (size_t)src.rank * count, src.*local, sizeof(double) * count,
-                                      hipMemcpyDeviceToDevice, s));
+                                      hipMemcpyDeviceToDevice, dst.s));
+        }
+        join();
+    }
+
+    // The objective row after fused multi-rank batches: each rank kept only its own slice current
+    // (the columns of its objective tiles, and d[0] on rank 0; sx_kernels.hip batch_mr_body); this
+    // hands every rank the whole row.  RCCL ranks: a sum all-reduce of rows that hold the rank's
+    // slice and -0.0 elsewhere (x + -0.0 == x for every x, -0.0 included: exact); shards of this
+    // process: device copies of the slices.  IPC test ranks: the caller's simplex_session_sync_d.
+    bool d_split = false;
+
+    // logical columns [j0, j1) of rank k's slice (d[0] is rank 0's)
+    void d_slice(int k, int &j0, int &j1) const {
+        const int NBg = (N - 1 + SX_TILE - 1) / SX_TILE;
+        const int tb0 = (int)((long long)k * NBg / W), tb1 = (int)((long long)(k + 1) * NBg / W);
+        j0 = 1 + tb0 * SX_TILE;
+        j1 = std::min(1 + tb1 * SX_TILE, N);
+        if (j0 > j1) j0 = j1;
+    }
+
+    void gather_d() {
+        if (!d_split) return;
+        d_split = false;
+        if (ipc) return;
+        if (rccl) {
+            Shard &x = sh[0];
+            if (!x.dx) x.dx = dalloc<double>(round_up((size_t)N1, 16));
+            int j0, j1;
+            d_slice(x.rank, j0, j1);
+            sx_launch_d_contrib(x.d, x.dx, N, j0, j1, x.rank == 0, s);
+            SX_NCCL(ncclAllReduce(x.dx, x.d, N, ncclDouble, ncclSum, g_cfg.comm, s));
+            return;
+        }
+        join();
+        for (auto &dst : sh) {
+            DevGuard g(dst.dev);
+            for (auto &src : sh) {
+                if (src.rank == dst.rank) continue;
+                int j0, j1;
+                d_slice(src.rank, j0, j1);
+                if (j1 > j0)
+                    SX_HIP(hipMemcpyAsync(dst.d + j0, src.d + j0, sizeof(double) * (j1 - j0), hipMemcpyDeviceToDevice,
+                                          dst.s));
+                if (src.rank == 0) SX_HIP(hipMemcpyAsync(dst.d, src.d, sizeof(double), hipMemcpyDeviceToDevice, dst.s));
+            }
+        }
+        join();
+    }
+
+    // IPC test ranks: write this rank's slice into every peer's objective row (the caller
+    // barriers the processes before and after)
+    void publish_d_ipc() {
+        if (!ipc) return;
+        d_split = false;
+        Shard &x = sh[0];
+        int j0, j1;
+        d_slice(x.rank, j0, j1);
+        for (int k = 0; k < W; ++k) {
+            if (k == x.rank || pv.d[k] == nullptr) continue;
+            if (j1 > j0)
+                SX_HIP(hipMemcpyAsync(pv.d[k] + j0, x.d + j0, sizeof(double) * (j1 - j0), hipMemcpyDeviceToDevice, s));
+            if (x.rank == 0) SX_HIP(hipMemcpyAsync(pv.d[k], x.d, sizeof(double), hipMemcpyDeviceToDevice, s));
+        }
+        SX_HIP(hipStreamSynchronize(s));
     }
 
     // ---------------------------------------------------------------- objective GEMV
     // updateObjectiveFunction (gaussian.cu:132-162), deterministic blocked order.
     void update_objective(int width) {
+        gather_d();
         const Cols c = cols(width);
         const size_t part = (size_t)slots * c.Ns;
         for (auto &x : sh) {
+            DevGuard g(x.dev);
             if (!x.gemv_local) x.gemv_local = dalloc<double>((size_t)slots * Ns1);
             if (xchg && !x.gemv_all) x.gemv_all = dalloc<double>((size_t)W * slots * Ns1);
-            SX_HIP(hipMemsetAsync(x.gemv_local, 0, part * sizeof(double), s));
-            sx_launch_coef(x.d, x.base, x.row0, x.rows, x.coef, s);
-            sx_launch_gemv_partials(x.T, x.rows, tl, c.Ns, x.coef, x.gemv_local, s);
+            SX_HIP(hipMemsetAsync(x.gemv_local, 0, part * sizeof(double), x.s));
+            sx_launch_coef(x.d, x.base, x.row0, x.rows, x.coef, x.s);
+            sx_launch_gemv_partials(x.T, x.rows, tl, c.Ns, x.coef, x.gemv_local, x.s);
         }
         if (xchg) allgather_doubles(&Shard::gemv_local, &Shard::gemv_all, part);
         const int nblk = (m + SX_TILE - 1) / SX_TILE;
-        for (auto &x : sh) sx_launch_gemv_apply(x.d, cols(width, x), xchg ? x.gemv_all : x.gemv_local, nblk, s);
+        for (auto &x : sh) {
+            DevGuard g(x.dev);
+            sx_launch_gemv_apply(x.d, cols(width, x), xchg ? x.gemv_all : x.gemv_local, nblk, x.s);
+        }
     }
 
     void phase2_costs() {
-        for (auto &x : sh) sx_launch_phase2_costs(x.d, n, m, c_dev, s);
+        gather_d();
+        for (auto &x : sh) {
+            DevGuard g(x.dev);
+            sx_launch_phase2_costs(x.d, n, m, c_dev, x.s);
+        }
     }
 
     // logical width of a phase -> stored columns
@@ -731,18 +985,19 @@ class Engine {
             std::vector<int> id((size_t)m);
             for (int k = 0; k < m; ++k) id[k] = k;
             for (auto &x : sh) {
+                DevGuard g(x.dev);
                 if (!x.perm) {
                     x.perm = dalloc<int>(m);
                     x.iperm = dalloc<int>(m);
                     x.act = dalloc<unsigned char>(m);
                     x.nact = dalloc<int>(1);
                 }
-                SX_HIP(hipMemcpyAsync(x.perm, id.data(), sizeof(int) * m, hipMemcpyHostToDevice, s));
-                SX_HIP(hipMemcpyAsync(x.iperm, id.data(), sizeof(int) * m, hipMemcpyHostToDevice, s));
-                SX_HIP(hipMemsetAsync(x.act, 0, m, s));
-                SX_HIP(hipMemsetAsync(x.nact, 0, sizeof(int), s));
+                SX_HIP(hipMemcpyAsync(x.perm, id.data(), sizeof(int) * m, hipMemcpyHostToDevice, x.s));
+                SX_HIP(hipMemcpyAsync(x.iperm, id.data(), sizeof(int) * m, hipMemcpyHostToDevice, x.s));
+                SX_HIP(hipMemsetAsync(x.act, 0, m, x.s));
+                SX_HIP(hipMemsetAsync(x.nact, 0, sizeof(int), x.s));
             }
-            SX_HIP(hipStreamSynchronize(s));
+            sync_all();
         }
         compact = on;
     }
@@ -792,29 +1047,42 @@ class Engine {
     // pass 1 of the entering argmin for the first pivot of a phase (later pivots get it
     // from k_pivot_row)
     void enqueue_enter_partials() {
-        for (auto &x : sh) sx_launch_enter(x.d, N - 1, x.enter_parts, x.st, s);
+        gather_d();
+        for (auto &x : sh) {
+            DevGuard g(x.dev);
+            sx_launch_enter(x.d, N - 1, x.enter_parts, x.st, x.s);
+        }
     }
 
     // one pivot into slot q_host of the current batch: ratio test + selection, the pivot
     // row, the objective row and the next entering variable.  The tableau is not touched.
     void enqueue_pivot() {
-        for (auto &x : sh)
+        gather_d();
+        for (auto &x : sh) {
+            DevGuard g(x.dev);
             sx_launch_ratio_select(x.T, x.rows, x.row0, ld, tl, x.tiles_local, x.colE, x.st, x.base, !xchg,
-                                   rowgather ? x.slot_send : nullptr, slot_stride, cols(N, x), pending(x), s);
+                                   rowgather ? x.slot_send : nullptr, slot_stride, cols(N, x), pending(x), x.s);
+        }
         if (rowgather) {
             allgather_slots();
-            for (auto &x : sh) sx_launch_select_gathered(x.slot_all, slot_stride, W * slots, x.base, x.st, pending(x), s);
+            for (auto &x : sh) {
+                DevGuard g(x.dev);
+                sx_launch_select_gathered(x.slot_all, slot_stride, W * slots, x.base, x.st, pending(x), x.s);
+            }
         } else if (xchg) {
             allgather_tiles();
-            for (auto &x : sh)
-                sx_launch_select_row(x.T, x.rows, x.row0, ld, tl, cols(N, x), x.tiles_all, W * slots, x.prow_send, x.base, x.st,
-                                     pending(x), s);
+            for (auto &x : sh) {
+                DevGuard g(x.dev);
+                sx_launch_select_row(x.T, x.rows, x.row0, ld, tl, cols(N, x), x.tiles_all, W * slots, x.prow_send, x.base,
+                                     x.st, pending(x), x.s);
+            }
             allreduce_prow();
         }
         for (auto &x : sh) {
+            DevGuard g(x.dev);
             const double *pb = rowgather ? x.slot_all : (xchg ? x.prow : nullptr);
             sx_launch_pivot_row(x.T, x.rows, x.row0, ld, tl, cols(N, x), x.d, pb, rowgather ? slot_stride : 0, x.colE, x.st,
-                                pending(x), x.enter_parts, s);
+                                pending(x), x.enter_parts, x.s);
         }
         ++q_host;
     }
@@ -826,27 +1094,40 @@ class Engine {
         if (!p2p) return false;
         const int NBg = (N - 1 + SX_TILE - 1) / SX_TILE;
         const int nbl = (NBg + W - 1) / W;
-        return sx_batch_mr_fits(slots, nbl, k, rccl ? 1 : W);
+        int grids = 1;  // ranks resident together on one device
+        if (!rccl) {
+            std::map<int, int> per_dev;
+            for (auto &x : sh) grids = std::max(grids, ++per_dev[x.dev]);
+        }
+        return sx_batch_mr_fits(slots, nbl, k, grids);
     }
 
     void enqueue_batch(int k) {
         if (q_host != 0) SX_FATAL("fused batch inside a started batch");
         ++g_cfg.fused_batches;
         if (g_cfg.inject_hang >= 0 && g_cfg.inject_hang-- == 0)  // test hook: this batch aborts
-            for (auto &x : sh) SX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&x.chan->abort_w), 1u, 1, s));
+            for (auto &x : sh) {
+                DevGuard g(x.dev);
+                SX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&x.chan->abort_w), 1u, 1, x.s));
+            }
         if (!xchg) {
             Shard &x = sh[0];
             sx_launch_batch(x.T, x.rows, ld, tl, cols(N, x), x.d, x.d_save, x.base, x.st, pending(x), k, x.chan, x.ga, x.gb,
                             stamps, s);
-        } else if (!rccl && g_cfg.mr_single_launch) {
-            // virtual shards (one GPU): every rank's batch in ONE launch, so all ranks' blocks
-            // are resident together whenever the grid fits; they hand off through each other's
+            q_host = k;
+            return;
+        }
+        d_split = true;  // (multi-rank batches keep only each rank's own slice of d current)
+        if (!rccl && (g_cfg.mr_single_launch || multidev)) {
+            // shards of this process: the ranks on one GPU as ONE launch (all of them for virtual
+            // shards; one launch per GPU when each shard has its own), so a device's ranks are
+            // resident together whenever the grid fits; they hand off through each other's
             // buffers exactly as RCCL ranks do through peer memory
             const int NBg = (N - 1 + SX_TILE - 1) / SX_TILE;
-            std::vector<MrLaunchRank> rk(sh.size());
+            std::map<int, std::vector<MrLaunchRank>> by_dev;
             for (size_t i = 0; i < sh.size(); ++i) {
                 Shard &x = sh[i];
-                MrLaunchRank &q = rk[i];
+                MrLaunchRank q;
                 q.T = x.T;
                 q.rows = x.rows;
                 q.row0 = x.row0;
@@ -863,8 +1144,14 @@ class Engine {
                 q.ga = x.ga;
                 q.gb = x.gb;
                 q.gdone = x.gdone;
+                by_dev[x.dev].push_back(q);
             }
-            sx_launch_batch_mr_multi(rk.data(), W, rpr, ld, tl, cols(N), rk[0].pd.batch, k, slots, pv, 100000000ull, s);
+            const unsigned long long timeout = multidev ? 200000000ull : 100000000ull;  // 2 s / 1 s at 100 MHz
+            for (auto &kv : by_dev) {
+                DevGuard g(kv.first);
+                sx_launch_batch_mr_multi(kv.second.data(), (int)kv.second.size(), W, rpr, ld, tl, cols(N), batch_id, k,
+                                         slots, pv, timeout, dstream[kv.first]);
+            }
         } else {
             // every rank's batch runs at once (virtual shards: one stream each, forked from and
             // joined back into the engine stream); the ranks hand off through peer memory
@@ -898,15 +1185,18 @@ class Engine {
         const SweepCfg cfg = sweep_cfg(q_host);
         const int rev = (int)(sweeps & 1);  // alternate the sweep direction (Infinity-Cache reuse)
         // the slack exchanges first (each shard's own buffers), so the events bracket the
-        // sweeps alone
+        // sweeps alone (ev0 / ev1 on the engine stream: shard 0's sweep)
         if (compact)
-            for (auto &x : sh)
+            for (auto &x : sh) {
+                DevGuard g(x.dev);
                 sx_launch_activate(x.perm, x.iperm, x.act, x.nact, m, x.T, x.rows, x.row0, ld, tl, 1 + n, pending(x), x.st,
-                                   s);
+                                   x.s);
+            }
         if (ev0) SX_HIP(hipEventRecord(ev0, s));
         for (auto &x : sh) {
+            DevGuard g(x.dev);
             sx_launch_sweep(x.T, x.rows, ld, tl, cols(N).Ns, compact ? x.nact : nullptr, 1 + n, pending(x), x.st, rev, cfg,
-                            s);
+                            x.s);
             if (rec_shard0) sx_set_sweep_record(nullptr);  // (only shard 0's sweep records)
         }
         if (rec_shard0) sx_set_sweep_record(nullptr);
@@ -922,15 +1212,18 @@ class Engine {
     void wrap_batch_ids() {
         batch_id = 1;
         for (auto &x : sh) {
-            SX_HIP(hipMemsetAsync(x.PM, 0, sizeof(unsigned long long) * (x.rows > 0 ? (size_t)x.rows : 1), s));
-            SX_HIP(hipMemsetAsync(x.ga, 0, sx_batch_granules_a() * sizeof(unsigned long long), s));
-            SX_HIP(hipMemsetAsync(x.gb, 0, sx_batch_granules_b() * sizeof(unsigned long long), s));
-            if (x.gdone) SX_HIP(hipMemsetAsync(x.gdone, 0, SX_MAXW * sizeof(unsigned long long), s));
+            DevGuard g(x.dev);
+            SX_HIP(hipMemsetAsync(x.PM, 0, sizeof(unsigned long long) * (x.rows > 0 ? (size_t)x.rows : 1), x.s));
+            SX_HIP(hipMemsetAsync(x.ga, 0, sx_batch_granules_a() * sizeof(unsigned long long), x.s));
+            SX_HIP(hipMemsetAsync(x.gb, 0, sx_batch_granules_b() * sizeof(unsigned long long), x.s));
+            if (x.gdone) SX_HIP(hipMemsetAsync(x.gdone, 0, SX_MAXW * sizeof(unsigned long long), x.s));
         }
         // peer ranks write into these records: no rank starts its next batch before every rank
-        // has cleared its own (an RCCL all-reduce behind the memsets on every rank)
+        // has cleared its own (an RCCL all-reduce behind the memsets on every rank; the shards of
+        // this process: a join of the device streams)
         if (rccl && !ipc) all_ranks(1);
-        SX_HIP(hipStreamSynchronize(s));
+        join();
+        sync_all();
     }
 
     void reset_state(long long max_pivots) {
@@ -942,8 +1235,11 @@ class Engine {
         init.r = -1;
         init.e_next = -1;
         init.max_pivots = max_pivots;
-        for (auto &x : sh) SX_HIP(hipMemcpyAsync(x.st, &init, sizeof(init), hipMemcpyHostToDevice, s));
-        SX_HIP(hipStreamSynchronize(s));
+        for (auto &x : sh) {
+            DevGuard g(x.dev);
+            SX_HIP(hipMemcpyAsync(x.st, &init, sizeof(init), hipMemcpyHostToDevice, x.s));
+        }
+        sync_all();
     }
 
     DevState read_state() {
@@ -1012,6 +1308,8 @@ class Engine {
                 if (st != SX_NOT_ENDED) break;
             }
         }
+        gather_d();
+        sync_all();  // (one synchronous call: every device's work is done)
         DevState f = read_state();
         if (timed) {
             const size_t iters = std::min(it_ev.size() / 2, (size_t)f.pivots + 1);
@@ -1030,17 +1328,20 @@ class Engine {
     // the basis (written only by a completed batch) nor the state (only the status); its
     // objective row is restored from d_save.  The batch behind it saw the SX_HANG status and
     // did nothing.  The batch is then re-run on the per-pivot path, under fresh batch ids.
+    // (Multi-rank batches: each rank restores its own slice -- the entries its threads saved --
+    // and the whole row is then gathered, so no rank depends on a peer's aborted batch.)
     void recover_hang(int K) {
-        SX_HIP(hipStreamSynchronize(s));
+        sync_all();
         ++g_cfg.hang_recoveries;
         const int ne = SX_NOT_ENDED;
         for (auto &x : sh) {
-            SX_HIP(hipMemcpyAsync(x.d, x.d_save, sizeof(double) * N, hipMemcpyDeviceToDevice, s));
-            SX_HIP(hipMemcpyAsync(&x.st->status, &ne, sizeof(int), hipMemcpyHostToDevice, s));
+            DevGuard g(x.dev);
+            SX_HIP(hipMemcpyAsync(x.d, x.d_save, sizeof(double) * N, hipMemcpyDeviceToDevice, x.s));
+            SX_HIP(hipMemcpyAsync(&x.st->status, &ne, sizeof(int), hipMemcpyHostToDevice, x.s));
         }
-        for (int b = 0; b < K; ++b) enqueue_pivot();
+        for (int b = 0; b < K; ++b) enqueue_pivot();  // (the first gathers d)
         enqueue_sweep();
-        SX_HIP(hipStreamSynchronize(s));
+        sync_all();
     }
 
     double read_d0() {
@@ -1056,14 +1357,20 @@ class Engine {
     }
 
     void write_base(const int *in) {
-        for (auto &x : sh) SX_HIP(hipMemcpyAsync(x.base, in, sizeof(int) * m, hipMemcpyHostToDevice, s));
-        SX_HIP(hipStreamSynchronize(s));
+        for (auto &x : sh) {
+            DevGuard g(x.dev);
+            SX_HIP(hipMemcpyAsync(x.base, in, sizeof(int) * m, hipMemcpyHostToDevice, x.s));
+        }
+        sync_all();
     }
 
     // RHS column of all rows (for the solution, getSolution twoPhaseMethod.cu:116-128)
     void read_rhs(std::vector<double> &out) {
         out.assign(m, 0.0);
-        for (auto &x : sh) sx_launch_gather_rhs(x.T, x.rows, tl.ldA, x.rhs_local, s);  // (column 0: region A)
+        for (auto &x : sh) {
+            DevGuard g(x.dev);
+            sx_launch_gather_rhs(x.T, x.rows, tl.ldA, x.rhs_local, x.s);  // (column 0: region A)
+        }
         if (xchg) {
             allgather_doubles(&Shard::rhs_local, &Shard::rhs_all, rpr);
             SX_HIP(hipMemcpyAsync(out.data(), sh[0].rhs_all, sizeof(double) * m, hipMemcpyDeviceToHost, s));
@@ -1076,6 +1383,8 @@ class Engine {
     // rows of the whole tableau (virtual or single shard only), logical columns: for tests
     // and printing (aliased artificial columns are expanded from their slack columns)
     void download(double *T_host, size_t ld_host, int width, double *d_host, bool local_rows = false) {
+        gather_d();
+        sync_all();
         const Cols c = cols(width);
         std::vector<double> tmp;
         std::vector<int> perm;
@@ -1089,12 +1398,13 @@ class Engine {
             if (x.rows <= 0) continue;
             tmp.assign((size_t)x.rows * c.Ns, 0.0);
             const int wa = std::min(c.Ns, tl.jB);  // region A's columns, then region B's
+            DevGuard g(x.dev);
             SX_HIP(hipMemcpy2DAsync(tmp.data(), c.Ns * sizeof(double), x.T, tl.ldA * sizeof(double),
-                                    wa * sizeof(double), x.rows, hipMemcpyDeviceToHost, s));
+                                    wa * sizeof(double), x.rows, hipMemcpyDeviceToHost, x.s));
             if (wa < c.Ns)
                 SX_HIP(hipMemcpy2DAsync(tmp.data() + wa, c.Ns * sizeof(double), x.T + tl.offB, tl.ldB * sizeof(double),
-                                        (c.Ns - wa) * sizeof(double), x.rows, hipMemcpyDeviceToHost, s));
-            SX_HIP(hipStreamSynchronize(s));
+                                        (c.Ns - wa) * sizeof(double), x.rows, hipMemcpyDeviceToHost, x.s));
+            SX_HIP(hipStreamSynchronize(x.s));
             for (int i = 0; i < x.rows; ++i) {
                 double *dst = T_host + (size_t)((local_rows ? 0 : x.row0) + i) * ld_host;
                 const double *src = tmp.data() + (size_t)i * c.Ns;
@@ -1113,21 +1423,23 @@ class Engine {
     void upload(const double *T_host, size_t ld_host, int width, const double *d_host, const int *base_host,
                 bool local_rows = false) {
         set_compact(false);  // a caller's tableau: any column may be touched
+        d_split = false;
         const Cols c = cols(width);
         for (auto &x : sh) {
+            DevGuard g(x.dev);
             if (x.rows > 0) {
                 const double *src = T_host + (size_t)(local_rows ? 0 : x.row0) * ld_host;
                 const int wa = std::min(c.Ns, tl.jB);  // region A's columns, then region B's
                 SX_HIP(hipMemcpy2DAsync(x.T, tl.ldA * sizeof(double), src, ld_host * sizeof(double),
-                                        wa * sizeof(double), x.rows, hipMemcpyHostToDevice, s));
+                                        wa * sizeof(double), x.rows, hipMemcpyHostToDevice, x.s));
                 if (wa < c.Ns)
                     SX_HIP(hipMemcpy2DAsync(x.T + tl.offB, tl.ldB * sizeof(double), src + wa, ld_host * sizeof(double),
-                                            (c.Ns - wa) * sizeof(double), x.rows, hipMemcpyHostToDevice, s));
+                                            (c.Ns - wa) * sizeof(double), x.rows, hipMemcpyHostToDevice, x.s));
             }
-            if (d_host) SX_HIP(hipMemcpyAsync(x.d, d_host, sizeof(double) * width, hipMemcpyHostToDevice, s));
-            if (base_host) SX_HIP(hipMemcpyAsync(x.base, base_host, sizeof(int) * m, hipMemcpyHostToDevice, s));
+            if (d_host) SX_HIP(hipMemcpyAsync(x.d, d_host, sizeof(double) * width, hipMemcpyHostToDevice, x.s));
+            if (base_host) SX_HIP(hipMemcpyAsync(x.base, base_host, sizeof(int) * m, hipMemcpyHostToDevice, x.s));
         }
-        SX_HIP(hipStreamSynchronize(s));
+        sync_all();
     }
 };
 
@@ -1285,6 +1597,48 @@ int two_phase(problem_t *P, double *solution, double *opt, int *base_out, long l
     return status;
 }
 
+// A small instance (n = 300, m = 1100: 1318 + 23 pivots, phases ending mid-batch) solved with the
+// multi-rank fused batch over peer memory and with the per-pivot exchange: true when the fused
+// path ran (no hand-off timed out) and both answers are bit-identical.
+bool selftest_solves() {
+    problem_t *P = generateRandomProblem(300, 1100, 41100, 1, 100);
+    const int n = P->vars, m = P->constraints;
+    std::vector<double> xa(n), xb(n);
+    std::vector<int> ba(m), bb(m);
+    long long pa[2] = {0, 0}, pb[2] = {0, 0};
+    double za = 0.0, zb = 0.0;
+    const int save = g_cfg.p2p;
+    const bool save_nt = g_cfg.no_timer;
+    g_cfg.no_timer = true;  // (timing would switch both solves to the per-pivot path; no CSVs either)
+    g_cfg.p2p = 1;
+    const long long fb0 = g_cfg.fused_batches, hr0 = g_cfg.hang_recoveries;
+    const int sa = two_phase(P, xa.data(), &za, ba.data(), pa, -1);
+    const bool went_fused = g_cfg.fused_batches > fb0 && g_cfg.hang_recoveries == hr0;
+    g_cfg.p2p = 0;
+    const int sb = two_phase(P, xb.data(), &zb, bb.data(), pb, -1);
+    g_cfg.p2p = save;
+    g_cfg.no_timer = save_nt;
+    const bool ok = went_fused && sa == sb && sa != SX_HANG && pa[0] == pb[0] && pa[1] == pb[1] &&
+                    std::memcmp(&za, &zb, sizeof(za)) == 0 && ba == bb &&
+                    std::memcmp(xa.data(), xb.data(), sizeof(double) * n) == 0;
+    freeProblem(P);
+    free(P);
+    return ok;
+}
+
+// One process, several GPUs (SIMPLEX_GPUS): the peer-memory batch is used on a device list only
+// when selftest_solves passes on it (once per list and process).
+bool gpus_selftest(const std::vector<int> &devs) {
+    auto it = g_cfg.p2p_checked.find(devs);
+    if (it != g_cfg.p2p_checked.end()) return it->second;
+    g_cfg.p2p_checked[devs] = false;  // (while the check runs)
+    const bool ok = selftest_solves();
+    g_cfg.p2p_checked[devs] = ok;
+    if (!ok) fprintf(stderr, "simplex: peer-memory fused batches disagree with the per-pivot exchange on these GPUs; "
+                             "using the per-pivot exchange\n");
+    return ok;
+}
+
 }  // namespace
 
 // ====================================================================== C-ABI
@@ -1300,6 +1654,15 @@ void simplex_set_device(int device) {
     if (device >= 0) SX_HIP(hipSetDevice(device));
 }
 void simplex_set_virtual_ranks(int world) { g_cfg.virtual_ranks = world > 1 ? world : 1; }
+void simplex_set_gpus(const int *devices, int count) {
+    g_cfg.gpus.clear();
+    for (int i = 0; devices != nullptr && i < count; ++i) g_cfg.gpus.push_back(devices[i]);
+}
+int simplex_gpus(int *devices, int cap) {
+    const std::vector<int> v = shard_devices();
+    for (int i = 0; devices != nullptr && i < cap && i < (int)v.size(); ++i) devices[i] = v[(size_t)i];
+    return (int)v.size();
+}
 void simplex_set_force_exchange(int on) { g_cfg.force_exchange = on ? 1 : 0; }
 void simplex_set_alias(int on) { g_cfg.alias = on ? 1 : 0; }
 void simplex_set_regions(int mode) { g_cfg.regions = mode < 0 ? 1 : mode; }
@@ -1307,7 +1670,14 @@ void simplex_set_mr_single_launch(int on) { g_cfg.mr_single_launch = on ? 1 : 0;
 void simplex_set_compact(int on) { g_cfg.compact = on ? 1 : 0; }
 void simplex_set_fused(int mode) { g_cfg.fused = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_p2p(int mode) { g_cfg.p2p = mode < 0 ? -1 : (mode ? 1 : 0); }
-int simplex_p2p_ready(void) { return g_cfg.p2p_ready ? 1 : 0; }
+int simplex_p2p_ready(void) {
+    const std::vector<int> v = g_cfg.dist ? std::vector<int>() : shard_devices();
+    if (v.size() > 1) {  // one process, several GPUs: the self-check of this device list
+        auto it = g_cfg.p2p_checked.find(v);
+        return it != g_cfg.p2p_checked.end() && it->second ? 1 : 0;
+    }
+    return g_cfg.p2p_ready ? 1 : 0;
+}
 void simplex_last_phase_seconds(double *out) {
     out[0] = g_phase_seconds[0];
     out[1] = g_phase_seconds[1];
@@ -1340,28 +1710,7 @@ int simplex_dist_get_unique_id(unsigned char *out) {
 static void p2p_selftest() {
     g_cfg.p2p_ready = false;
     if (g_cfg.world > SX_MAXW || g_cfg.p2p == 0) return;
-    problem_t *P = generateRandomProblem(300, 1100, 41100, 1, 100);
-    const int n = P->vars, m = P->constraints;
-    std::vector<double> xa(n), xb(n);
-    std::vector<int> ba(m), bb(m);
-    long long pa[2] = {0, 0}, pb[2] = {0, 0};
-    double za = 0.0, zb = 0.0;
-    const int save = g_cfg.p2p;
-    const bool save_nt = g_cfg.no_timer;
-    g_cfg.no_timer = true;  // (timing would switch both solves to the per-pivot path; no CSVs either)
-    g_cfg.p2p = 1;
-    const long long fb0 = g_cfg.fused_batches, hr0 = g_cfg.hang_recoveries;
-    const int sa = two_phase(P, xa.data(), &za, ba.data(), pa, -1);
-    const bool went_fused = g_cfg.fused_batches > fb0 && g_cfg.hang_recoveries == hr0;
-    g_cfg.p2p = 0;
-    const int sb = two_phase(P, xb.data(), &zb, bb.data(), pb, -1);
-    g_cfg.p2p = save;
-    g_cfg.no_timer = save_nt;
-    int ok = went_fused && sa == sb && sa != SX_HANG && pa[0] == pb[0] && pa[1] == pb[1] &&
-             std::memcmp(&za, &zb, sizeof(za)) == 0 && ba == bb &&
-             std::memcmp(xa.data(), xb.data(), sizeof(double) * n) == 0;
-    freeProblem(P);
-    free(P);
+    int ok = selftest_solves() ? 1 : 0;
     int *dv = nullptr;
     SX_HIP(hipMalloc(reinterpret_cast<void **>(&dv), sizeof(int)));
     SX_HIP(hipMemcpy(dv, &ok, sizeof(int), hipMemcpyHostToDevice));
@@ -1506,7 +1855,7 @@ static simplex_session *session_finish(simplex_session *S) {
     S->E->N = S->E->N1;
     S->E->reset_state(-1);
     S->E->enqueue_enter_partials();
-    SX_HIP(hipStreamSynchronize(S->E->s));
+    S->E->sync_all();
     return S;
 }
 
@@ -1558,8 +1907,10 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
         if (E.q_host >= K || (fused && E.q_host > 0)) sweep();
     }
     if (E.q_host > 0) sweep();
+    E.join();  // (the engine stream's end event follows every device's work)
     SX_HIP(hipEventRecord(w1, E.s));
     SX_HIP(hipEventSynchronize(w1));
+    E.sync_all();
     DevState f = E.read_state();
     simplex_timing_t t;
     std::memset(&t, 0, sizeof(t));
@@ -1600,6 +1951,8 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
     (void)hipEventDestroy(w0);
     (void)hipEventDestroy(w1);
     S->total = f.pivots;
+    E.gather_d();  // (outside the timed region: the whole objective row on every shard)
+    E.sync_all();
     if (out) *out = t;
     return f.status;
 }
@@ -1627,6 +1980,8 @@ int simplex_session_stamps(simplex_session *S, int k, unsigned long long *out) {
     E.enqueue_batch(k);
     E.stamps = nullptr;
     E.enqueue_sweep();
+    E.gather_d();
+    E.sync_all();
     SX_HIP(hipMemcpyAsync(out, dev, sizeof(unsigned long long) * k * 8, hipMemcpyDeviceToHost, E.s));
     SX_HIP(hipStreamSynchronize(E.s));
     (void)hipFree(dev);
@@ -1673,7 +2028,7 @@ simplex_session *simplex_ipc_session_open(int n, int m, int rank, int world, con
     E.N = E.N1;
     E.reset_state(-1);
     E.enqueue_enter_partials();
-    SX_HIP(hipStreamSynchronize(E.s));
+    E.sync_all();
     if (!E.export_handles(handles_out)) {
         simplex_session_close(S);
         return nullptr;
@@ -1686,6 +2041,13 @@ int simplex_ipc_session_connect(simplex_session *S, const unsigned char *all_han
     if (!E.ipc || !E.map_peers(all_handles, E.sh[0].rank)) return -1;
     E.p2p = true;
     return E.fused_ok(E.batch_size()) ? 0 : -2;
+}
+
+int simplex_session_sync_d(simplex_session *S) {
+    Engine &E = *S->E;
+    if (!E.ipc) return -1;
+    E.publish_d_ipc();
+    return 0;
 }
 
 long long simplex_session_rows(simplex_session *S, double *T_rows, long long ld_host, double *d, int *base) {

@@ -1022,10 +1022,6 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
     int status = SX_NOT_ENDED, cnt = 0, last_r = -1, last_e = -1;
     bool aborted = false;
     if (status0 == SX_NOT_ENDED) {
-        // the objective row as the batch found it, for the host to restore when the batch is
-        // aborted (SX_HANG): d is written only at the end of the batch, after hand-offs that
-        // need every block, so every block has copied its share before anything changes it
-        for (int j = blockIdx.x * blockDim.x + t; j < c.N; j += gridDim.x * blockDim.x) d_save[j] = d[j];
         // ratio block: its row; objective block: its logical column d[1 + ia]
         const int li = blockIdx.x * SX_TILE + t;
         const bool liveA = isA && li < rows;
@@ -1038,6 +1034,10 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
         unsigned bits = 0u;                            // slots where this row left the basis
         double dj = liveB ? d[1 + ia] : 0.0;
         double d0 = (!isA && tb == 0 && t == 0) ? d[0] : 0.0;
+        // the objective row as the batch found it, for the host to restore when the batch is
+        // aborted (SX_HANG): saved by the very thread that writes the entry at the end
+        if (liveB) d_save[1 + ia] = dj;
+        if (!isA && tb == 0 && t == 0) d_save[0] = d0;
         // the entering column's stored value of this row: loaded as soon as the entering
         // variable is known, so the load overlaps the wait for its pending history
         double a_pre = liveA ? T[tl.idx(li, c.map(1 + (e >= 0 ? e : 0)))] : 0.0;
@@ -1429,10 +1429,10 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
     double dj = liveB ? d[1 + ia] : 0.0;
     double d0 = (!isA && tb == 0 && t == 0) ? d[0] : 0.0;
     if (status0 == SX_NOT_ENDED) {
-        // this rank's whole objective row as the batch found it (restored by the host on
-        // SX_HANG): every rank writes d slices only at the end of the batch, after hand-offs
-        // that need every block of every rank, so this copy is complete before any change
-        for (int j = bid * blockDim.x + t; j < c.N; j += nbl * blockDim.x) d_save[j] = d[j];
+        // this rank's slice of the objective row as the batch found it (restored by the host on
+        // SX_HANG), saved by the very thread that writes the entry at the end
+        if (liveB) d_save[1 + ia] = dj;
+        if (!isA && tb == 0 && t == 0) d_save[0] = d0;
         double b = liveA ? T[tl.idx(li, 0)] : 0.0;
         unsigned bits = 0u;
         // the entering column's stored value of this row: loaded as soon as the entering
@@ -1709,30 +1709,39 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
             }
         }
     }
-    // every rank's d slices to every rank (each rank keeps the whole objective row between batches)
-    if (liveB)
-        for (int k = 0; k < W; ++k) st_sys(pv.d[k] + 1 + ia, dj);
-    if (!isA && tb == 0 && t == 0)
-        for (int k = 0; k < W; ++k) st_sys(pv.d[k], d0);
+    // this rank's slice of the objective row (its objective tiles' columns; d[0] on rank 0): between
+    // fused batches each rank keeps only its own slice current -- no rank writes another's d, so an
+    // aborted batch cannot overwrite a peer's restored row -- and the host gathers the whole row
+    // when it is needed (Engine::gather_d)
+    if (liveB) d[1 + ia] = dj;
+    if (!isA && tb == 0 && t == 0) d[0] = d0;
     // leave: the last block of this rank tells every rank it is done, waits until every rank
-    // is, and writes the batch's outcome into the state
+    // is, and writes the batch's outcome into the state.  Ordering: every wave
+    // drains its stores (U rows written into every rank, F, PM, its d slice), the block barrier
+    // joins them, and the block's arrival on exit_cnt is a system-scope RELEASE (its L2 writes
+    // back what is dirty); the last block's arrival is an acquire-release, so it observes every
+    // block's stores before its own system-scope release of the done granules; a rank reads a
+    // peer's done granule with system-scope loads and takes a system-scope acquire before it
+    // commits the batch.  The next kernel on this rank (the sweep) reads U after that commit.
     drain();
     __syncthreads();
     if (t == 0) {
-        const unsigned k = __hip_atomic_fetch_add(&ch->exit_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned k = __hip_atomic_fetch_add(&ch->exit_cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
         s_flag = (k == nbl - 1);
         if (s_flag) __hip_atomic_store(&ch->exit_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (!s_flag) return;
-    // every wave of this rank drained its system-scope stores (U, d, granules) before adding
-    // to exit_cnt; a system-scope release here orders them before the done granules
-    if (t == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if (t == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        drain();  // (MI355X_MICROARCH.md: the compiler may drop the wait behind the write-back)
+    }
     __syncthreads();
     const unsigned dtag = make_tag(B, 0);
     if (t < W) put_g_sys(pv.gdone[t] + rank, aborted ? 1u : 0u, dtag);
     const bool ok = gather_tagged<decltype(ident), true>(gdone, W, ident, dtag, s_g, &ch->abort_w, &s_ok, timeout);
     if (t != 0) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     bool peer_abort = false;
     for (int k = 0; ok && k < W; ++k) peer_abort |= s_g[k] != 0u;
     if (status0 != SX_NOT_ENDED) return;
@@ -1766,10 +1775,12 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
                   slots, W, rank, tb0, tb1, NBg, ch, ga, gb, gdone, pv, timeout);
 }
 
-// All W virtual ranks' batches in ONE launch (ranks on one GPU): block b belongs to the rank k
-// with first[k] <= b < first[k + 1], as its block b - first[k].  One grid, so every rank's
-// blocks are resident together whenever the grid fits the device -- W launches on W streams
-// also need W hardware queues that run at once, which a process does not control.
+// The batches of the nloc ranks (of W) that live on one GPU in ONE launch: block b belongs to
+// the local rank k with first[k] <= b < first[k + 1], as its block b - first[k].  One grid, so
+// every local rank's blocks are resident together whenever the grid fits the device -- nloc
+// launches on nloc streams also need nloc hardware queues that run at once, which a process
+// does not control.  (Virtual shards: all W ranks on one GPU; one process driving several
+// GPUs: one launch per GPU.)
 struct MrRank {
     const double *T;
     int rows, row0, rank, tb0, tb1;
@@ -1787,11 +1798,11 @@ struct MrRanks {
     MrRank r[SX_MAXW];
     int first[SX_MAXW + 1];
 };
-__global__ __launch_bounds__(512) void k_batch_mr_multi(MrRanks R, int rpr, size_t ld, TLay tl, Cols c, unsigned B,
-                                                        int K, int slots, int W, int NBg, PeerView pv,
+__global__ __launch_bounds__(512) void k_batch_mr_multi(MrRanks R, int nloc, int rpr, size_t ld, TLay tl, Cols c,
+                                                        unsigned B, int K, int slots, int W, int NBg, PeerView pv,
                                                         unsigned long long timeout) {
     int k = 0;
-    while (k + 1 < W && (int)blockIdx.x >= R.first[k + 1]) ++k;
+    while (k + 1 < nloc && (int)blockIdx.x >= R.first[k + 1]) ++k;
     const MrRank &x = R.r[k];
     Cols cx = c;
     cx.perm = x.perm;
@@ -2043,6 +2054,14 @@ __global__ void k_sum_rows(double *out, const double *const *srcs, int nsrc, int
         for (int k = 1; k < nsrc; ++k) s = s + srcs[k][j];
         out[j] = s;
     }
+}
+
+// A rank's contribution to the objective-row gather (Engine::gather_d): its slice [j0, j1) (and
+// d[0] on rank 0), -0.0 elsewhere; the sum all-reduce of the ranks' contributions is then the
+// whole row bit for bit (x + -0.0 == x).
+__global__ void k_d_contrib(const double *__restrict__ d, double *__restrict__ out, int N, int j0, int j1, int with0) {
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < N; j += gridDim.x * blockDim.x)
+        out[j] = ((j >= j0 && j < j1) || (j == 0 && with0)) ? d[j] : -0.0;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2328,8 +2347,12 @@ bool sx_batch_mr_fits(int slots, int nb_local, int k, int grids) {
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)batch_lds(SX_KMAX)));
         SX_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_batch_mr_multi),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)batch_lds(SX_KMAX)));
-        int n = 0;
+        // the kernel launched is k_batch_mr (RCCL / IPC ranks) or k_batch_mr_multi (ranks sharing
+        // a process): the grid must fit with either
+        int n = 0, n2 = 0;
         SX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_batch_mr, SX_TILE, batch_lds(k)));
+        SX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n2, k_batch_mr_multi, SX_TILE, batch_lds(k)));
+        n = n < n2 ? n : n2;
         per_cu[k] = n > 0 ? n : -1;
     }
     return per_cu[k] > 0 && (long long)grids * (slots + nb_local) <= (long long)per_cu[k] * cus - 16;
@@ -2348,14 +2371,14 @@ void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld,
                                                                   tb1, NBg, chan, ga, gb, gdone, pv, timeout);
 }
 
-void sx_launch_batch_mr_multi(const MrLaunchRank *ranks, int W, int rpr, size_t ld, TLay tl, Cols c, unsigned B, int k,
-                              int slots, const PeerView &pv, unsigned long long timeout, hipStream_t s) {
+void sx_launch_batch_mr_multi(const MrLaunchRank *ranks, int nloc, int W, int rpr, size_t ld, TLay tl, Cols c, unsigned B,
+                              int k, int slots, const PeerView &pv, unsigned long long timeout, hipStream_t s) {
     const int NBg = (c.N - 1 + SX_TILE - 1) / SX_TILE;
-    if (W < 1 || W > SX_MAXW || W * slots > SX_TILE || NBg > SX_TILE || NBg < 1)
+    if (W < 1 || W > SX_MAXW || nloc < 1 || nloc > W || W * slots > SX_TILE || NBg > SX_TILE || NBg < 1)
         SX_FATAL("multi-rank fused batch: bad shape");
     MrRanks R;
     R.first[0] = 0;
-    for (int i = 0; i < W; ++i) {
+    for (int i = 0; i < nloc; ++i) {
         const MrLaunchRank &q = ranks[i];
         if (q.tb0 < 0 || q.tb1 > NBg || q.tb0 > q.tb1) SX_FATAL("multi-rank fused batch: bad objective tiles");
         MrRank &x = R.r[i];
@@ -2380,8 +2403,9 @@ void sx_launch_batch_mr_multi(const MrLaunchRank *ranks, int W, int rpr, size_t 
         x.gdone = q.gdone;
         R.first[i + 1] = R.first[i] + slots + (q.tb1 - q.tb0);
     }
-    for (int i = W + 1; i <= SX_MAXW; ++i) R.first[i] = R.first[W];
-    k_batch_mr_multi<<<R.first[W], SX_TILE, batch_lds(k), s>>>(R, rpr, ld, tl, c, B, k, slots, W, NBg, pv, timeout);
+    for (int i = nloc + 1; i <= SX_MAXW; ++i) R.first[i] = R.first[nloc];
+    k_batch_mr_multi<<<R.first[nloc], SX_TILE, batch_lds(k), s>>>(R, nloc, rpr, ld, tl, c, B, k, slots, W, NBg, pv,
+                                                                  timeout);
 }
 
 // every XCD's L2 writes back its dirty lines (blocks are dealt over all XCDs; each block's
@@ -2395,6 +2419,13 @@ void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N,
     int g = (N + 255) / 256;
     if (g > 1024) g = 1024;
     k_sum_rows<<<g, 256, 0, s>>>(out, srcs, nsrc, N);
+}
+
+void sx_launch_d_contrib(const double *d, double *out, int N, int j0, int j1, int with0, hipStream_t s) {
+    int g = (N + 255) / 256;
+    if (g > 1024) g = 1024;
+    if (g < 1) g = 1;
+    k_d_contrib<<<g, 256, 0, s>>>(d, out, N, j0, j1, with0);
 }
 
 void sx_launch_coef(const double *d, const int *base, int row0, int rows, double *coef, hipStream_t s) {

@@ -4,7 +4,9 @@ the path simplex_dist_init's peer-memory mode uses across GPUs -- here without R
 processes can share one GPU.  Line protocol on stdin/stdout with the parent:
   -> HANDLES <hex>      <- ALL <hex of every rank's handles, rank order>
   -> CONNECTED <rc>     <- GO
-  -> DONE <status> <pivots>   (rows, d, base saved to <out>)   <- EXIT
+  -> DONE <status> <pivots>   <- SYNC
+  -> SYNCED                   <- READ
+  -> SAVED <hang recoveries> <fused batches>   (rows, d, base saved to <out>)   <- EXIT
 usage: python tests/ipc_worker.py rank world n m seed lo hi pivots out.npz"""
 import ctypes
 import os
@@ -53,12 +55,18 @@ def main():
     assert sys.stdin.readline().strip() == "GO"
     t = sx.api._lib.TimingT()
     st = lib.simplex_session_pivots(sess, pivots, 0, ctypes.byref(t))
+    say("DONE", st, t.pivots)
+    # every rank's objective-row slice into every peer's row, between two barriers
+    assert sys.stdin.readline().strip() == "SYNC"
+    assert lib.simplex_session_sync_d(sess) == 0
+    say("SYNCED")
+    assert sys.stdin.readline().strip() == "READ"
     Tg = np.zeros((max(r1 - r0, 1), N1))
     dg = np.zeros(N1)
     bg = np.zeros(m, dtype=np.int32)
     nr = lib.simplex_session_rows(sess, Tg.ctypes.data_as(dp), N1, dg.ctypes.data_as(dp), bg.ctypes.data_as(ip))
     np.savez(out, T=Tg[:max(nr, 0)], d=dg, base=bg, r0=r0)
-    say("DONE", st, t.pivots)
+    say("SAVED", lib.simplex_hang_recoveries(), lib.simplex_fused_batches())
     assert sys.stdin.readline().strip() == "EXIT"
     lib.simplex_session_close(sess)
     return 0

@@ -49,6 +49,14 @@ def run_ranks(tmp_path, world, n, m, seed, lo, hi, pivots):
             p.stdin.write("GO\n")
             p.stdin.flush()
         done = [expect(p, "DONE") for p in procs]
+        for step, reply in (("SYNC", "SYNCED"), ("READ", "SAVED")):
+            for p in procs:
+                p.stdin.write(step + "\n")
+                p.stdin.flush()
+            got = [expect(p, reply) for p in procs]
+        # every rank stayed on the peer-memory path: fused batches ran, none timed out and was re-run
+        for hr, fb in got:
+            assert int(hr) == 0 and int(fb) > 0, (hr, fb)
         for p in procs:
             p.stdin.write("EXIT\n")
             p.stdin.flush()

@@ -10,7 +10,9 @@ Here the same instance is synthesised in HBM, 48 pivots run (one full 32-pivot b
 partial one), and the digests of the GPU's state must match: on one shard (fused batch), on
 row-block virtual shards through both per-pivot exchanges (the W = 4 split of config 4, the
 W = 8 split of config 5), and through the peer-memory fused batch (W = 2, 3, and the multi-GPU
-splits W = 4 / 8: the virtual ranks' batches run as one launch on one GPU).
+splits W = 4 / 8: the virtual ranks' batches run as one launch on one GPU), and through the
+one-process multi-GPU mode (SIMPLEX_GPUS / simplex_set_gpus) with every shard mapped onto this
+GPU: device list [0] * W, the peer-memory batch enabled by the mode's own start-up self-check.
 """
 import hashlib
 import json
@@ -37,10 +39,15 @@ def sha(a):
     return h.hexdigest()
 
 
-def run(name, W=1, mode=0, p2p=-1):
+def run(name, W=1, mode=0, p2p=-1, gpus=None):
     pin = PINS[name]
     n, m = pin["n"], pin["m"]
-    sx.set_virtual_ranks(W)
+    lib = sx.load()
+    h0, f0 = lib.simplex_hang_recoveries(), lib.simplex_fused_batches()
+    if gpus:
+        sx.set_gpus(gpus)
+    else:
+        sx.set_virtual_ranks(W)
     sx.set_exchange_mode(mode)
     sx.set_p2p(p2p)
     try:
@@ -48,7 +55,11 @@ def run(name, W=1, mode=0, p2p=-1):
         tim = sess.pivots(pin["pivots"])
         T, d, base = sess.tableau(m, pin["width"])
         sess.close()
+        if gpus:  # the mode's self-check passed and its batches stayed on the peer-memory path
+            assert lib.simplex_p2p_ready() == 1
+            assert lib.simplex_fused_batches() > f0 and lib.simplex_hang_recoveries() == h0
     finally:
+        sx.set_gpus([])
         sx.set_virtual_ranks(1)
         sx.set_exchange_mode(0)
         sx.set_p2p(-1)
@@ -72,3 +83,9 @@ def test_config5_pivots_match_oracle(gpu, W, mode, p2p):
 @pytest.mark.parametrize("W,mode,p2p", [(1, 0, -1), (8, 1, 0), (2, 0, 1), (8, 0, 1)])
 def test_config5_degenerate_variant_pivots_match_oracle(gpu, W, mode, p2p):
     run("config5_degenerate", W, mode, p2p)
+
+
+@pytest.mark.parametrize("name,W", [("config4", 4), ("config5", 8), ("config5_degenerate", 8)])
+def test_simplex_gpus_mode_on_one_device(gpu, name, W):
+    """SIMPLEX_GPUS mapped onto one GPU: the multi-GPU splits of configs 4 and 5 bit-exact"""
+    run(name, gpus=[0] * W)

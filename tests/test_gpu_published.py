@@ -1,0 +1,87 @@
+"""Whole two-phase solves on the GPU against the reference's whole published set and against
+independent optima (needs an MI355X).
+
+* tests/golden/published_pivots.json: the per-phase pivot counts of all 36 instances of the
+  reference's -t benchmark (main.cu:50-77: n, m in 256..8192, seed n*100+m, +1 at n=1024 /
+  m=8192, values in [1, 100]), harvested from data/measures/rtx2070super/benchmark_<n>_<m>.txt
+  (one `solve` CSV row per loop iteration, chrono.cu:35-50).  Every instance must end FEASIBLE
+  with exactly those counts.
+* tests/golden/oracle_solves.json: whole solves by the serial CPU oracle (made in the build
+  container, tests/golden/scripts/make_oracle_solves.py): status, pivot counts, the objective's
+  bits, SHA-256 of the final basis and of the solution -- config 3 and the MX250's failing
+  instance (n=1024, m=8192, seed 110592).
+* tests/golden/highs_objectives.json: optimal objectives of the BASELINE configs from SciPy /
+  HiGHS (tests/golden/scripts/make_highs_objectives.py); north_star's bar is 1e-6 relative.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import simplexoncuda_amd as sx
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _load(name):
+    path = os.path.join(GOLDEN, name)
+    if not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        return json.load(f)
+
+
+PUBLISHED = [r for r in _load("published_pivots.json") if r["gpu"] == "rtx2070super"]
+ORACLE = _load("oracle_solves.json")
+HIGHS = _load("highs_objectives.json")
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def solve(n, m, seed, lo, hi):
+    # the device generator is bit-identical to generateRandomProblem (tests/test_gpu_generator.py)
+    p = sx.generateRandomProblemDevice(n, m, seed, lo, hi)
+    try:
+        return sx.twoPhaseMethodEx(p)
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("rec", PUBLISHED, ids=lambda r: f"n{r['n']}_m{r['m']}")
+def test_published_instance(gpu, rec):
+    assert len(PUBLISHED) == 36
+    got = solve(rec["n"], rec["m"], rec["seed"], rec["lo"], rec["hi"])
+    assert got.status == sx.FEASIBLE, got.status_name
+    assert tuple(got.pivots) == (rec["p1_pivots"], rec["p2_pivots"])
+
+
+@pytest.mark.parametrize("name", sorted(ORACLE))
+def test_oracle_whole_solve(gpu, name):
+    rec = ORACLE[name]
+    got = solve(rec["n"], rec["m"], rec["seed"], rec["lo"], rec["hi"])
+    assert got.status == rec["status"], got.status_name
+    assert list(got.pivots) == rec["pivots"]
+    assert sha(np.asarray(got.base, dtype=np.int32)) == rec["base_sha256"]
+    if rec["status"] == sx.FEASIBLE:
+        assert float(got.optimal_value).hex() == rec["opt_hex"]
+        assert sha(np.asarray(got.solution, dtype=np.float64)) == rec["x_sha256"]
+
+
+@pytest.mark.parametrize("name", sorted(k for k, r in HIGHS.items()
+                                        if r["highs_status"] in (0, 2, 3) and k.startswith("config")))
+def test_highs_objective(gpu, name):
+    """north_star: the optimal objective within 1e-6 relative of an independent LP solver"""
+    rec = HIGHS[name]
+    got = solve(rec["n"], rec["m"], rec["seed"], rec["lo"], rec["hi"])
+    if rec["highs_status"] == 0:
+        assert got.status == sx.FEASIBLE, got.status_name
+        assert got.optimal_value == pytest.approx(rec["highs_opt"], rel=1e-6)
+    elif rec["highs_status"] == 2:  # infeasible
+        assert got.status == sx.INFEASIBLE, got.status_name
+    else:  # unbounded
+        assert got.status == sx.UNBOUNDED, got.status_name
