@@ -175,9 +175,12 @@ void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, in
 bool sx_batch_fits(int rows, Cols c, int k);
 // d_save: the objective row as the batch found it (restored by the host after SX_HANG); the
 // basis is written only by a batch that completed
+// perm / iperm / act / nact (slack compaction, or null): the batch's last block also activates
+// the slack columns of the rows that left the basis for the first time (k_activate's work)
 void sx_launch_batch(const double *T, int rows, size_t ld, TLay tl, Cols c, double *d, double *d_save, int *base,
                      DevState *st, const Pending &pd, int k, BatchChan *chan, unsigned long long *ga,
-                     unsigned long long *gb, unsigned long long *stamps, hipStream_t s);
+                     unsigned long long *gb, unsigned long long *stamps, int *perm, int *iperm, unsigned char *act,
+                     int *nact, int m, hipStream_t s);
 size_t sx_batch_granules_a();
 size_t sx_batch_granules_b();
 // the multi-rank fused batch: `grids` co-resident launches of this shape must fit the device

@@ -308,6 +308,7 @@ class Engine {
     // slots inside the current one; every batch ends with a sweep of the tableau
     unsigned batch_id = 1;  // 1 .. 2^15 - 1 (the granule tags keep 15 bits; see enqueue_sweep)
     int q_host = 0;
+    bool batch_activated = false;  // the pending batch's fused kernel already activated its slack columns
     unsigned long long *stamps = nullptr;  // diagnostic: in-kernel timestamps of the fused batch
     long long sweeps = 0;
     std::function<void(int)> on_pivot;  // DEBUG trace: called after every pivot (solver.cu:112-116)
@@ -865,19 +866,23 @@ class Engine {
     }
 
     // The objective row after fused multi-rank batches: each rank kept only its own slice current
-    // (the columns of its objective tiles, and d[0] on rank 0; sx_kernels.hip batch_mr_body); this
+    // (the columns of its objective tiles, and d[0] on the rank holding tile 0; sx_kernels.hip
+    // batch_mr_body); this
     // hands every rank the whole row.  RCCL ranks: a sum all-reduce of rows that hold the rank's
     // slice and -0.0 elsewhere (x + -0.0 == x for every x, -0.0 included: exact); shards of this
     // process: device copies of the slices.  IPC test ranks: the caller's simplex_session_sync_d.
     bool d_split = false;
 
-    // logical columns [j0, j1) of rank k's slice (d[0] is rank 0's)
-    void d_slice(int k, int &j0, int &j1) const {
+    // logical columns [j0, j1) of rank k's slice; d[0] belongs to the rank whose objective tiles
+    // start with tile 0 (own0) -- not always rank 0: a rank can have no objective tile when the
+    // phase has fewer 512-column tiles than ranks
+    void d_slice(int k, int &j0, int &j1, bool &own0) const {
         const int NBg = (N - 1 + SX_TILE - 1) / SX_TILE;
         const int tb0 = (int)((long long)k * NBg / W), tb1 = (int)((long long)(k + 1) * NBg / W);
         j0 = 1 + tb0 * SX_TILE;
         j1 = std::min(1 + tb1 * SX_TILE, N);
         if (j0 > j1) j0 = j1;
+        own0 = tb0 == 0 && tb1 > 0;
     }
 
     void gather_d() {
@@ -888,8 +893,9 @@ class Engine {
             Shard &x = sh[0];
             if (!x.dx) x.dx = dalloc<double>(round_up((size_t)N1, 16));
             int j0, j1;
-            d_slice(x.rank, j0, j1);
-            sx_launch_d_contrib(x.d, x.dx, N, j0, j1, x.rank == 0, s);
+            bool own0;
+            d_slice(x.rank, j0, j1, own0);
+            sx_launch_d_contrib(x.d, x.dx, N, j0, j1, own0 ? 1 : 0, s);
             SX_NCCL(ncclAllReduce(x.dx, x.d, N, ncclDouble, ncclSum, g_cfg.comm, s));
             return;
         }
@@ -899,11 +905,12 @@ class Engine {
             for (auto &src : sh) {
                 if (src.rank == dst.rank) continue;
                 int j0, j1;
-                d_slice(src.rank, j0, j1);
+                bool own0;
+                d_slice(src.rank, j0, j1, own0);
                 if (j1 > j0)
                     SX_HIP(hipMemcpyAsync(dst.d + j0, src.d + j0, sizeof(double) * (j1 - j0), hipMemcpyDeviceToDevice,
                                           dst.s));
-                if (src.rank == 0) SX_HIP(hipMemcpyAsync(dst.d, src.d, sizeof(double), hipMemcpyDeviceToDevice, dst.s));
+                if (own0) SX_HIP(hipMemcpyAsync(dst.d, src.d, sizeof(double), hipMemcpyDeviceToDevice, dst.s));
             }
         }
         join();
@@ -916,12 +923,13 @@ class Engine {
         d_split = false;
         Shard &x = sh[0];
         int j0, j1;
-        d_slice(x.rank, j0, j1);
+        bool own0;
+        d_slice(x.rank, j0, j1, own0);
         for (int k = 0; k < W; ++k) {
             if (k == x.rank || pv.d[k] == nullptr) continue;
             if (j1 > j0)
                 SX_HIP(hipMemcpyAsync(pv.d[k] + j0, x.d + j0, sizeof(double) * (j1 - j0), hipMemcpyDeviceToDevice, s));
-            if (x.rank == 0) SX_HIP(hipMemcpyAsync(pv.d[k], x.d, sizeof(double), hipMemcpyDeviceToDevice, s));
+            if (own0) SX_HIP(hipMemcpyAsync(pv.d[k], x.d, sizeof(double), hipMemcpyDeviceToDevice, s));
         }
         SX_HIP(hipStreamSynchronize(s));
     }
@@ -1113,7 +1121,8 @@ class Engine {
         if (!xchg) {
             Shard &x = sh[0];
             sx_launch_batch(x.T, x.rows, ld, tl, cols(N, x), x.d, x.d_save, x.base, x.st, pending(x), k, x.chan, x.ga, x.gb,
-                            stamps, s);
+                            stamps, compact ? x.perm : nullptr, x.iperm, x.act, x.nact, m, s);
+            batch_activated = compact;  // (its last block did k_activate's work)
             q_host = k;
             return;
         }
@@ -1186,7 +1195,7 @@ class Engine {
         const int rev = (int)(sweeps & 1);  // alternate the sweep direction (Infinity-Cache reuse)
         // the slack exchanges first (each shard's own buffers), so the events bracket the
         // sweeps alone (ev0 / ev1 on the engine stream: shard 0's sweep)
-        if (compact)
+        if (compact && !batch_activated)
             for (auto &x : sh) {
                 DevGuard g(x.dev);
                 sx_launch_activate(x.perm, x.iperm, x.act, x.nact, m, x.T, x.rows, x.row0, ld, tl, 1 + n, pending(x), x.st,
@@ -1203,6 +1212,7 @@ class Engine {
         if (ev1) SX_HIP(hipEventRecord(ev1, s));
         ++sweeps;
         q_host = 0;
+        batch_activated = false;
         if (++batch_id >= SX_BATCH_IDS) wrap_batch_ids();
     }
 

@@ -661,30 +661,6 @@ __global__ __launch_bounds__(256) void k_pivot_row(const double *__restrict__ T,
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// K6: a whole batch of pivots in ONE resident launch (one shard).  Blocks [0, NA) own the
-// 512-row ratio tiles, blocks [NA, NA + NB) the 512-entry objective-row tiles.  Each block
-// keeps its slice of the state on chip for the whole batch: a ratio block its rows' current
-// RHS and factor history F[.][s] (LDS); an objective block its columns' d values (registers)
-// and pivot-row history U[s][.] (LDS).  Per pivot q:
-//   ratio blocks      form the current entering column of their rows (T[i][e] + pending
-//                     pivots), the ratio vector and the tile winner (reduction.cu:106-140);
-//   every block       reads all ratio-tile winners and runs pass 2 itself (the same tree, so
-//                     the same leaving row r in every block; solver.cu:96-105);
-//   objective blocks  form the current pivot row on their columns, update d and reduce it
-//                     per tile (solver.cu:48-56, reduction.cu:51-80);
-//   every block       reads all objective-tile winners and runs pass 2 itself: the entering
-//                     variable of pivot q + 1.
-// A tile winner is published as data-tagged granules: 8 bytes = {32 data bits, 32-bit tag
-// (batch << 8 | q)}, each a single write-through (sc1) store, so a consumer needs no flag and
-// no ordering between the granules: it polls (sc1 loads) until every granule it needs carries
-// the pivot's tag (MI355X_MICROARCH.md price list: handoff-1to1).  With its winner, a tile
-// also publishes the history the consumer needs of the winning line: the factors F[r][s] of
-// the winning row (ratio tiles) or the pivot-row values U[s][e] of the winning column
-// (objective tiles), so nothing else crosses blocks inside the launch.  Every wait is
-// bounded: past ~0.2 s the block raises abort_w and all blocks leave (status SX_HANG).  The
-// grid is launched only when all its blocks are resident at once (sx_batch_fits).
-
 typedef unsigned long long u64;
 
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -885,8 +861,10 @@ __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, uns
 }
 
 // granule layout of one tile record
-#define SX_GA_STRIDE (8 + 2 * SX_KMAX)  // ratio tile: v(2, payload: idx, elig) pad(2) a(2) b(2) | F[r][s] (2 per slot)
-#define SX_GB_STRIDE (4 + 2 * SX_KMAX)  // objective tile: v(2, payload: idx) pad(2) | U[s][e] (2 per slot)
+// (k_batch: the RV..RF / OV..OU layouts below; k_batch_mr: v(2) pad(2) a(2) b(2) F(2 per slot) and
+// v(2) pad(2) U(2 per slot) inside the same strides)
+#define SX_GA_STRIDE (10 + 2 * SX_KMAX)  // ratio tile record, granules
+#define SX_GB_STRIDE (8 + 2 * SX_KMAX)   // objective tile record, granules
 __device__ __forceinline__ int rec2_a(int k) { return (k >> 1) * SX_GA_STRIDE + (k & 1); }
 // granules of all tile records
 __host__ __device__ __forceinline__ size_t sx_ga_size() { return (size_t)SX_TILE * SX_GA_STRIDE; }
@@ -985,11 +963,166 @@ __device__ __forceinline__ double hist_row(double u, int q, int r, const double 
     return u;
 }
 
-__global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int rows, size_t ld, TLay tl, Cols c,
+// Slack compaction's bookkeeping for one batch (what k_activate does as its own launch; here
+// run by the fused batch's last block, after every other block has left): the first time row
+// r leaves the basis, its slack column -- still the unit vector e_r as built, never swept -- is
+// exchanged with the slack column at the first untouched stored position s0 + nact (also a
+// unit vector), so the swept block [0, s0 + nact) grows by one.  The exchanges of the batch are
+// resolved in slot order by wave 0, one list entry per lane (stored offset, slack held before
+// the batch, slack held now); their net effect is then applied at once: to the pending pivot
+// rows U[s] (whose entries at the two columns are the leaving rows' current values there; the
+// objective blocks stored them write-through, and they are read here with sc1 loads), to T
+// (zeros and ones of the unit vectors) and to perm / iperm / act / nact.  All threads of the
+// block call it; s_rr[0..cnt) are the batch's leaving rows (local = global: one shard).
+__device__ void activate_block(int *__restrict__ perm, int *__restrict__ iperm, unsigned char *__restrict__ act,
+                               int *__restrict__ nact_p, int m, double *__restrict__ T, int rows, TLay tl, int s0,
+                               double *__restrict__ U, size_t ld, const int *s_rr, int cnt, int *s_pl, int *s_ol,
+                               int *s_cl, int *s_src, int *s_misc, double *s_u) {
+    const int t = threadIdx.x;
+    if (t < 64) {
+        const int na0 = *nact_p;
+        int r = 0, a = 1, pr = 0, win = -1;
+        if (t < cnt) {
+            r = s_rr[t];
+            a = act[r];
+            pr = perm[r];
+            if (na0 + t < m) win = iperm[na0 + t];
+        }
+        int pl = -1, ol = -1, cl = -1;  // this lane's list entry
+        int nl = 0, added = 0;
+        for (int s = 0; s < cnt; ++s) {
+            const int rs = __shfl(r, s);
+            if (__shfl(a, s)) continue;  // its slack was touched in an earlier batch
+            // already moved into the window in this batch?
+            if (__ballot(t < nl && cl == rs && pl >= na0 && pl < na0 + added)) continue;
+            const unsigned long long hP = __ballot(t < nl && cl == rs);
+            int iP;
+            if (hP) {
+                iP = __ffsll((long long)hP) - 1;
+            } else {  // untouched in this batch: at its pre-batch offset
+                iP = nl++;
+                const int P = __shfl(pr, s);
+                if (t == iP) {
+                    pl = P;
+                    ol = rs;
+                    cl = rs;
+                }
+            }
+            const int pos = na0 + added;
+            const unsigned long long hW = __ballot(t < nl && pl == pos);
+            int iW;
+            if (hW) {
+                iW = __ffsll((long long)hW) - 1;
+            } else {
+                iW = nl++;
+                const int w = __shfl(win, added);
+                if (t == iW) {
+                    pl = pos;
+                    ol = w;
+                    cl = w;
+                }
+            }
+            const int cP = __shfl(cl, iP), cW = __shfl(cl, iW);
+            if (t == iP) cl = cW;
+            if (t == iW) cl = cP;
+            ++added;
+        }
+        if (t < nl) {
+            s_pl[t] = pl;
+            s_ol[t] = ol;
+            s_cl[t] = cl;
+        }
+        if (t == 0) {
+            s_misc[0] = nl;
+            s_misc[1] = added;
+            s_misc[2] = na0;
+        }
+    }
+    __syncthreads();
+    const int nl = s_misc[0];
+    if (nl == 0) return;
+    if (t < nl) {  // the entry whose pre-batch slack this position holds now
+        int j = 0;
+        while (s_ol[j] != s_cl[t]) ++j;
+        s_src[t] = j;
+    }
+    __syncthreads();
+    for (int k = t; k < cnt * nl; k += blockDim.x) {
+        const int s = k / nl, i = k - s * nl;
+        s_u[k] = __longlong_as_double(
+            (long long)ld_sc1(reinterpret_cast<const u64 *>(U + (size_t)s * ld + s0 + s_pl[s_src[i]])));
+    }
+    __syncthreads();
+    for (int k = t; k < cnt * nl; k += blockDim.x) {
+        const int s = k / nl, i = k - s * nl;
+        U[(size_t)s * ld + s0 + s_pl[i]] = s_u[k];
+    }
+    if (t < nl) {
+        const int x = s_pl[t], o = s_ol[t], cc = s_cl[t];
+        if (o != cc) {
+            if (o < rows) T[tl.idx(o, s0 + x)] = 0.0;
+            if (cc < rows) T[tl.idx(cc, s0 + x)] = 1.0;
+        }
+        iperm[x] = cc;
+        perm[cc] = x;
+        const int na0 = s_misc[2];
+        if (x >= na0 && x < na0 + s_misc[1]) act[cc] = 1;
+    }
+    if (t == 0) *nact_p = s_misc[2] + s_misc[1];
+}
+
+// Tile-record layouts of the fused batch (granule offsets; each value 2 granules):
+//   ratio tile q      kRV v (payload: winner index, "entry >= eps" bit) | kRD d_e of pivot q |
+//                     kRA a of the winner row | kRB its RHS | kRE e of pivot q | kRS status of the
+//                     ratio side (NOT_ENDED, or FEASIBLE: the phase ended) | kRF F[winner][s < q]
+//   objective tile q  kOV v (payload: winner index) | kOP pivot p | kOB the pivot row's RHS | kOR
+//                     leaving row r | kOS status of the objective side (NOT_ENDED, UNBOUNDED,
+//                     NUMERIC_FAIL) | kOU U[s <= q][winner]
+[[maybe_unused]] constexpr int kRV = 0;  // (the value granules come first: rec2_a / rec2_b index them)
+constexpr int kRD = 2;
+constexpr int kRA = 4;
+constexpr int kRB = 6;
+constexpr int kRE = 8;
+constexpr int kRS = 9;
+constexpr int kRF = 10;
+[[maybe_unused]] constexpr int kOV = 0;
+constexpr int kOP = 2;
+constexpr int kOB = 4;
+constexpr int kOR = 6;
+constexpr int kOS = 7;
+constexpr int kOU = 8;
+
+// K6: a whole batch of pivots in ONE resident launch (one shard).  Blocks [0, NA) own the
+// 512-row ratio tiles, blocks [NA, NA + NB) the 512-entry objective-row tiles.  Each block
+// keeps its slice of the state on chip for the whole batch: a ratio block its rows' current
+// RHS and factor history F[.][s] (LDS); an objective block its columns' d values (registers)
+// and pivot-row history U[s][.] (LDS).  Per pivot q, two hand-offs, each read only by the
+// blocks that need it:
+//   ratio blocks      form the current entering column of their rows (T[i][e] + pending
+//                     pivots), the ratio vector and the tile winner (reduction.cu:106-140), and
+//                     publish it with the pivot's e and d_e;
+//   objective blocks  read every ratio record and run pass 2 (the leaving row r, solver.cu:
+//                     96-105), take p, the RHS and F[r][s] from the winner's record, form the
+//                     current pivot row on their columns, update d and reduce it per tile
+//                     (solver.cu:48-56, reduction.cu:51-80), and publish that with r, p, the RHS;
+//   ratio blocks      read every objective record and run pass 2 (the entering variable of
+//                     pivot q + 1), take r, p, the RHS and U[s][e] from the winner's record, and
+//                     apply the pivot to their rows' RHS and factor history.
+// The ratio side decides the end of the phase (compare(d_e) >= 0, solver.cu:88) and tells the
+// objective side through its records; the objective side decides UNBOUNDED / NUMERIC_FAIL and
+// tells the ratio side through its records.  A record is tagged 8-byte granules {32 data bits,
+// 32-bit tag} (MI355X_MICROARCH.md price list: handoff-1to1), each one write-through store; a
+// consumer polls (sc1 loads) until every granule it needs carries the pivot's tag.  Every wait
+// is bounded: past ~0.2 s the block raises abort_w and all blocks leave (status SX_HANG).  The
+// last block out writes the batch's outcome -- and, with slack compaction, does the batch's
+// column activation (activate_block) -- so no launch sits between the batch and its sweep.  The
+// grid is launched only when all its blocks are resident at once (sx_batch_fits).
+__global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t ld, TLay tl, Cols c,
                                                double *__restrict__ d, double *__restrict__ d_save, int *base,
                                                DevState *st, double *U, double *F, PivRec *recs,
                                                unsigned long long *PM, unsigned B, int K, int NA, int NB,
-                                               BatchChan *ch, u64 *ga, u64 *gb, unsigned long long *stamps) {
+                                               BatchChan *ch, u64 *ga, u64 *gb, unsigned long long *stamps,
+                                               int *perm, int *iperm, unsigned char *act, int *nact, int m) {
     extern __shared__ double s_hist[];  // [K][512]: F history (ratio blocks) / U history (objective blocks)
     __shared__ double s_v[16];
     __shared__ int s_i[16];
@@ -999,15 +1132,14 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
     __shared__ double s_a[SX_TILE], s_b[SX_TILE];    // ratio blocks: entering column, RHS (winner lookup)
     __shared__ unsigned s_g[4 * SX_TILE];            // gathered granules
     __shared__ unsigned s_pay[SX_TILE];              // their payloads (two-granule records)
-    __shared__ int s_ok;
+    __shared__ int s_last;
     // per-step results written by wave 0 before the step's one barrier (each step its own
     // words, so no wave still reading an earlier step's result can see them change)
-    __shared__ int s_sel_ok, s_sel_r, s_sel_any, s_det_ok, s_ent_ok, s_ent_e, s_ue_ok;
-    __shared__ double s_ent_v, s_br;
+    __shared__ int s_sel_ok, s_sel_r, s_sel_any, s_det_ok, s_det_e, s_det_st, s_ent_ok, s_ent_e, s_ent_r, s_ent_st;
+    __shared__ double s_det_dmin, s_ent_v, s_br, s_ent_p;
     __shared__ int s_welig[SX_TILE / 64];
     const int t = threadIdx.x;
     const bool isA = (int)blockIdx.x < NA;
-    const u64 *gam = ga, *gbm = gb;
     // stamps (diagnostic, normally null): s_memrealtime (100 MHz) at hand-off points of ratio
     // block 0 and objective block 0, [q][8]
 #define SX_STAMP(k)                                                                           \
@@ -1019,7 +1151,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
     const long long piv0 = st->pivots, cap = st->max_pivots;
     int e = st->e_next;
     double dmin = st->dmin_next;
-    int status = SX_NOT_ENDED, cnt = 0, last_r = -1, last_e = -1;
+    int status = SX_NOT_ENDED, cnt = 0;
     bool aborted = false;
     if (status0 == SX_NOT_ENDED) {
         // ratio block: its row; objective block: its logical column d[1 + ia]
@@ -1048,19 +1180,14 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                 status = SX_PIVOT_CAP;
                 break;
             }
-            if (!(cmp_eps(dmin, 0.0) < 0)) {  // solver.cu:88
-                status = SX_FEASIBLE;
-                break;
-            }
-            double a = 0.0;
             if (isA) {
+                const bool done = !(cmp_eps(dmin, 0.0) < 0);  // solver.cu:88: optimal
                 // ---- ratio tile: current entering column, ratios, tile winner
                 if (blockIdx.x == 0) SX_STAMP(0);
-                // pending pivots of the batch, in order
-                a = hist_col(a_pre, q, bits, s_hist, s_ue, s_p);
+                const double a = done ? 0.0 : hist_col(a_pre, q, bits, s_hist, s_ue, s_p);
                 double rv = DBL_MAX;
                 int ri = -1, elig = 0;
-                if (liveA) {
+                if (liveA && !done) {
                     elig = a >= SX_EPS;
                     const double ratio = cmp_eps(a, 0.0) > 0 ? b / a : DBL_MAX;  // reduction.cu:106-114
                     if (cmp_eps(ratio, rv) < 0) {
@@ -1095,102 +1222,74 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                         ((long long)__builtin_amdgcn_readfirstlane((int)(vb >> 32)) << 32) |
                         (long long)(unsigned)__builtin_amdgcn_readfirstlane((int)vb));
                     const int wl = wi >= 0 ? wi - (int)blockIdx.x * SX_TILE : 0;
-                    // the record: v (payload: index, "any" bit), pad, a, b, then F[winner][s] for s < q
                     const unsigned pl = (wi >= 0 ? (unsigned)wl : SX_NOIDX) | ((unsigned)any << 10);
-                    const int nG = 8 + 2 * q;
+                    const int nG = kRF + 2 * q;
                     for (int k = t; k < nG; k += 64) {
-                        if (k == 2 || k == 3) continue;
-                        const double val = k < 2 ? wv : k < 6 ? s_a[wl] : k < 8 ? s_b[wl]
-                                                                        : s_hist[((k - 8) >> 1) * SX_TILE + wl];
-                        const unsigned long long bits64 = (unsigned long long)__double_as_longlong(val);
-                        put_g(ga + (size_t)blockIdx.x * SX_GA_STRIDE + k,
-                              (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64, k < 2 ? (tag | pl) : tag);
+                        unsigned data;
+                        if (k == kRE) {
+                            data = (unsigned)e;
+                        } else if (k == kRS) {
+                            data = (unsigned)(done ? SX_FEASIBLE : SX_NOT_ENDED);
+                        } else {
+                            const double val = k < kRD ? wv : k < kRA ? dmin : k < kRB ? s_a[wl] : k < kRE ? s_b[wl]
+                                                                           : s_hist[((k - kRF) >> 1) * SX_TILE + wl];
+                            const u64 bits64 = (u64)__double_as_longlong(val);
+                            data = (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64;
+                        }
+                        put_g(ga + (size_t)blockIdx.x * SX_GA_STRIDE + k, data, k < kRD ? (tag | pl) : tag);
                     }
                 }
                 if (blockIdx.x == 0) SX_STAMP(1);
-            }
-            // ---- selection: every block runs pass 2 over the ratio-tile winners.  Wave 0 polls
-            // the records and runs the tree in registers (wave_pass2); one block barrier.
-            int r, anyall;
-            if (2 * NA <= 64 * SX_GATHER_PER_LANE) {
+                if (done) {
+                    status = SX_FEASIBLE;
+                    break;
+                }
+                // ---- the objective side's answer: pass 2 over the objective tiles (the entering
+                // variable of pivot q + 1), then r, p, the RHS, the status and U[s <= q][e] from
+                // the winner's record (wave 0 polls; one block barrier)
                 if (t < 64) {
-                    const int ok = poll_wave(gam, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
-                    double tv = DBL_MAX;
-                    int ti = -1, any = 0;
-                    if (ok) wave_pass2(s_g, s_pay, NA, s_v, s_i, tv, ti, any);
+                    int ok = poll_wave(gb, 2 * NB, rec2_b, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
+                    double ev = DBL_MAX;
+                    int ei = -1, any = 0;
+                    if (ok) wave_pass2(s_g, s_pay, NB, s_v, s_i, ev, ei, any);
+                    ei = __builtin_amdgcn_readfirstlane(ei);
+                    if (ok) {
+                        const int wt = ei >= 0 ? ei / SX_TILE : 0;
+                        ok = poll_wave(gb + (size_t)wt * SX_GB_STRIDE + kOP, (kOU - kOP) + 2 * (q + 1),
+                                       [](int k) { return k; }, tag, s_g, &ch->abort_w, 20000000ull, (unsigned *)nullptr);
+                        if (ok && t <= q) s_ue[t] = gd(s_g[kOU - kOP + 2 * t], s_g[kOU - kOP + 1 + 2 * t]);
+                    }
                     if (t == 0) {
-                        s_sel_ok = ok;
-                        s_sel_r = ti;
-                        s_sel_any = any;
+                        s_ent_ok = ok;
+                        s_ent_e = ei;
+                        s_ent_v = ev;
+                        if (ok) {
+                            s_ent_p = gd(s_g[0], s_g[1]);
+                            s_br = gd(s_g[kOB - kOP], s_g[kOB - kOP + 1]);
+                            s_ent_r = (int)s_g[kOR - kOP];
+                            s_ent_st = (int)s_g[kOS - kOP];
+                        }
                     }
                 }
                 __syncthreads();
-                if (!s_sel_ok) {
+                if (blockIdx.x == 0) SX_STAMP(5);
+                if (!s_ent_ok) {
                     aborted = true;
                     break;
                 }
-                r = s_sel_r;
-                anyall = s_sel_any;
-            } else {
-                if (!gather_tagged(gam, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay)) {
-                    aborted = true;
+                if (s_ent_st != SX_NOT_ENDED) {  // the objective side found UNBOUNDED / NUMERIC_FAIL
+                    status = s_ent_st;
                     break;
                 }
-                double tv = DBL_MAX;
-                int ti = -1, te = 0;
-                if (t < NA) {
-                    const double cv = gd(s_g[2 * t], s_g[2 * t + 1]);
-                    const unsigned pl = s_pay[t];
-                    te = (int)((pl >> 10) & 1u);
-                    if (cmp_eps(cv, tv) < 0) {
-                        tv = cv;
-                        ti = (pl & SX_NOIDX) == SX_NOIDX ? -1 : t * SX_TILE + (int)(pl & SX_NOIDX);
-                    }
-                }
-                anyall = __syncthreads_or(SX_ELIG(te));
-                block_argmin512(tv, ti, s_v, s_i);
-                if (t == 0) s_sel_r = ti;
-                __syncthreads();
-                r = s_sel_r;
-            }
-            if (!isA && tb == 0) SX_STAMP(3);
-            if (!anyall) {  // solver.cu:96-102
-                status = SX_UNBOUNDED;
-                break;
-            }
-            if (r < 0) {
-                status = SX_NUMERIC_FAIL;
-                break;
-            }
-            // the objective blocks' pivot-row load does not wait for the winner's details
-            double u = liveB ? T[tl.idx(r, mj)] : 0.0;
-            // the winner's details (pivot, RHS, factor history), read by wave 0 into LDS
-            if (t < 64) {
-                const int wt = r / SX_TILE;
-                const int ok = poll_wave(gam + (size_t)wt * SX_GA_STRIDE + 4, 4 + 2 * q, [](int k) { return k; }, tag,
-                                         s_g, &ch->abort_w, 20000000ull, (unsigned *)nullptr);
-                if (ok) {
-                    if (t < q) s_fr[t] = gd(s_g[4 + 2 * t], s_g[5 + 2 * t]);
-                    if (t == 0) {
-                        s_p[q] = gd(s_g[0], s_g[1]);
-                        s_br = gd(s_g[2], s_g[3]);
-                        s_r[q] = r;
-                        s_e[q] = e;
-                    }
-                }
-                if (t == 0) s_det_ok = ok;
-            }
-            __syncthreads();
-            if (!s_det_ok) {
-                aborted = true;
-                break;
-            }
-            const double p = s_p[q], br = s_br;
-            cnt = q + 1;
-            last_r = r;
-            last_e = e;
-            if (isA) {
                 // ---- this pivot's factor column and the rows' new RHS (solver.cu:34-46)
+                const int r = s_ent_r;
+                const double p = s_ent_p, br = s_br;
+                if (t == 0) {
+                    s_p[q] = p;
+                    s_r[q] = r;
+                    s_e[q] = e;
+                }
+                cnt = q + 1;
                 const double f = -a / p;
                 s_hist[q * SX_TILE + t] = f;
                 if (liveA) {
@@ -1210,22 +1309,92 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                     recs[q].p = p;
                     U[(size_t)q * ld] = br;  // the pivot row's RHS entry, for the sweep
                 }
+                e = s_ent_e;
+                dmin = s_ent_v;
+                if (liveA) a_pre = T[tl.idx(li, c.map(1 + (e >= 0 ? e : 0)))];
+                __syncthreads();  // (s_p / s_ue of this step are read by the next pivot's chain)
             } else {
-                // ---- objective tile: current pivot row on this column, d, tile winner
-                if (tb == 0) SX_STAMP(6);
-                u = hist_row(u, q, r, s_hist, s_fr, s_p, s_r);
-                s_hist[q * SX_TILE + t] = u;
-                if (tb == 0) SX_STAMP(7);
-                if (liveB && 1 + ia < c.Ns) U[(size_t)q * ld + mj] = u;
-                const double fd = -dmin / p;  // updateCostsVector, solver.cu:48-56
-                if (tb == 0 && t == 0) d0 = fma(fd, br, d0);
+                // ---- selection: pass 2 over the ratio tiles (wave 0 polls and runs the tree)
+                if (t < 64) {
+                    const int ok = poll_wave(ga, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
+                    double tv = DBL_MAX;
+                    int ti = -1, any = 0;
+                    if (ok) wave_pass2(s_g, s_pay, NA, s_v, s_i, tv, ti, any);
+                    if (t == 0) {
+                        s_sel_ok = ok;
+                        s_sel_r = ti;
+                        s_sel_any = any;
+                    }
+                }
+                __syncthreads();
+                if (tb == 0) SX_STAMP(3);
+                if (!s_sel_ok) {
+                    aborted = true;
+                    break;
+                }
+                const int r = s_sel_r;
+                // the pivot-row load does not wait for the winner's details
+                double u = liveB && r >= 0 ? T[tl.idx(r, mj)] : 0.0;
+                // the winner's record (the ratio tile 0's when there is none): d_e, p, the RHS,
+                // e, the ratio side's status and F[r][s < q], read by wave 0 into LDS
+                if (t < 64) {
+                    const int wt = r >= 0 ? r / SX_TILE : 0;
+                    const int ok = poll_wave(ga + (size_t)wt * SX_GA_STRIDE + kRD, (kRF - kRD) + 2 * q,
+                                             [](int k) { return k; }, tag, s_g, &ch->abort_w, 20000000ull,
+                                             (unsigned *)nullptr);
+                    if (ok) {
+                        if (t < q) s_fr[t] = gd(s_g[kRF - kRD + 2 * t], s_g[kRF - kRD + 1 + 2 * t]);
+                        if (t == 0) {
+                            s_det_dmin = gd(s_g[0], s_g[1]);
+                            s_p[q] = gd(s_g[kRA - kRD], s_g[kRA - kRD + 1]);
+                            s_br = gd(s_g[kRB - kRD], s_g[kRB - kRD + 1]);
+                            s_det_e = (int)s_g[kRE - kRD];
+                            s_det_st = (int)s_g[kRS - kRD];
+                            s_r[q] = r;
+                            s_e[q] = (int)s_g[kRE - kRD];
+                        }
+                    }
+                    if (t == 0) s_det_ok = ok;
+                }
+                __syncthreads();
+                if (!s_det_ok) {
+                    aborted = true;
+                    break;
+                }
+                e = s_det_e;
+                dmin = s_det_dmin;
+                int ost = SX_NOT_ENDED;
+                if (s_det_st != SX_NOT_ENDED) {  // the ratio side ended the phase (optimal)
+                    status = s_det_st;
+                    break;
+                }
+                if (!s_sel_any) {
+                    ost = SX_UNBOUNDED;  // solver.cu:96-102
+                } else if (r < 0) {
+                    ost = SX_NUMERIC_FAIL;
+                }
+                const double p = s_p[q], br = s_br;
                 double v = DBL_MAX;
                 int i = -1;
-                if (liveB) {
-                    dj = fma(fd, u, dj);
-                    if (cmp_eps(dj, v) < 0) {
-                        v = dj;
-                        i = ia;
+                if (ost == SX_NOT_ENDED) {
+                    cnt = q + 1;
+                    // ---- objective tile: current pivot row on this column, d, tile winner
+                    if (tb == 0) SX_STAMP(6);
+                    u = hist_row(u, q, r, s_hist, s_fr, s_p, s_r);
+                    s_hist[q * SX_TILE + t] = u;
+                    if (tb == 0) SX_STAMP(7);
+                    // (write-through: the last block reads them back for the column activation)
+                    if (liveB && 1 + ia < c.Ns)
+                        __hip_atomic_store(reinterpret_cast<u64 *>(U + (size_t)q * ld + mj), (u64)__double_as_longlong(u),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const double fd = -dmin / p;  // updateCostsVector, solver.cu:48-56
+                    if (tb == 0 && t == 0) d0 = fma(fd, br, d0);
+                    if (liveB) {
+                        dj = fma(fd, u, dj);
+                        if (cmp_eps(dj, v) < 0) {
+                            v = dj;
+                            i = ia;
+                        }
                     }
                 }
                 // pass 1 (reduction.cu:51-80): half-wave trees, one block barrier, wave 0 combines
@@ -1245,112 +1414,89 @@ __global__ __launch_bounds__(512) void k_batch(const double *__restrict__ T, int
                     wv = __longlong_as_double(((long long)__builtin_amdgcn_readfirstlane((int)(vb >> 32)) << 32) |
                                               (long long)(unsigned)__builtin_amdgcn_readfirstlane((int)vb));
                     const int win = wi >= 0 ? wi - tb * SX_TILE : 0;
-                    // the record: v (payload: index), pad, then U[s][winner] for s <= q
                     const unsigned pl = wi >= 0 ? (unsigned)win : SX_NOIDX;
-                    const int nG = 4 + 2 * (q + 1);
+                    const int nG = kOU + 2 * (q + 1);
                     for (int k = t; k < nG; k += 64) {
-                        if (k == 2 || k == 3) continue;
-                        const double val = k < 2 ? wv : s_hist[((k - 4) >> 1) * SX_TILE + win];
-                        const unsigned long long bits64 = (unsigned long long)__double_as_longlong(val);
-                        put_g(gb + (size_t)tb * SX_GB_STRIDE + k,
-                              (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64, k < 2 ? (tag | pl) : tag);
+                        unsigned data;
+                        if (k == kOR) {
+                            data = (unsigned)r;
+                        } else if (k == kOS) {
+                            data = (unsigned)ost;
+                        } else {
+                            const double val = k < kOP ? wv : k < kOB ? p : k < kOR ? br
+                                                                          : s_hist[((k - kOU) >> 1) * SX_TILE + win];
+                            const u64 bits64 = (u64)__double_as_longlong(val);
+                            data = (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64;
+                        }
+                        put_g(gb + (size_t)tb * SX_GB_STRIDE + k, data, k < kOP ? (tag | pl) : tag);
                     }
                 }
                 if (tb == 0) SX_STAMP(4);
+                if (ost != SX_NOT_ENDED) {
+                    status = ost;
+                    break;
+                }
             }
-            // ---- entering variable of pivot q + 1: every block runs pass 2 over the objective
-            // tiles (wave 0 polls and runs the tree; one block barrier)
-            if (2 * NB <= 64 * SX_GATHER_PER_LANE) {
-                if (t < 64) {
-                    const int ok = poll_wave(gbm, 2 * NB, rec2_b, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
-                    double ev = DBL_MAX;
-                    int ei = -1, any = 0;
-                    if (ok) wave_pass2(s_g, s_pay, NB, s_v, s_i, ev, ei, any);
-                    if (t == 0) {
-                        s_ent_ok = ok;
-                        s_ent_e = ei;
-                        s_ent_v = ev;
-                    }
-                }
-                __syncthreads();
-                if (!s_ent_ok) {
-                    aborted = true;
-                    break;
-                }
-            } else {
-                if (!gather_tagged(gbm, 2 * NB, rec2_b, tag, s_g, &ch->abort_w, &s_ok, 20000000ull, s_pay)) {
-                    aborted = true;
-                    break;
-                }
+        }
+        // a batch that ended without a decision of the ratio side (all K pivots ran, or the pivot
+        // cap): the objective blocks learn the next entering variable, which only the ratio side
+        // computed, from the last objective records
+        if (!isA && !aborted && (status == SX_NOT_ENDED || status == SX_PIVOT_CAP) && cnt > 0) {
+            const unsigned tag = make_tag(B, cnt - 1);
+            if (t < 64) {
+                const int ok = poll_wave(gb, 2 * NB, rec2_b, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
                 double ev = DBL_MAX;
-                int ei = -1;
-                if (t < NB) {
-                    const double cv = gd(s_g[2 * t], s_g[2 * t + 1]);
-                    const unsigned pl = s_pay[t] & SX_NOIDX;
-                    if (cmp_eps(cv, ev) < 0) {
-                        ev = cv;
-                        ei = pl == SX_NOIDX ? -1 : t * SX_TILE + (int)pl;
-                    }
-                }
-                block_argmin512(ev, ei, s_v, s_i);
+                int ei = -1, any = 0;
+                if (ok) wave_pass2(s_g, s_pay, NB, s_v, s_i, ev, ei, any);
                 if (t == 0) {
+                    s_ent_ok = ok;
                     s_ent_e = ei;
                     s_ent_v = ev;
                 }
-                __syncthreads();
             }
+            __syncthreads();
+            if (!s_ent_ok) aborted = true;
             e = s_ent_e;
             dmin = s_ent_v;
-            if (liveA) a_pre = T[tl.idx(li, c.map(1 + (e >= 0 ? e : 0)))];
-            if (isA && blockIdx.x == 0) SX_STAMP(5);
-            // the ratio blocks need the pending pivot rows' entries in the new entering column
-            // (wave 0 reads them into LDS; one block barrier)
-            if (isA && q + 1 < K && e >= 0 && cmp_eps(dmin, 0.0) < 0) {
-                if (t < 64) {
-                    const int ok = poll_wave(gbm + (size_t)(e / SX_TILE) * SX_GB_STRIDE + 4, 2 * (q + 1),
-                                             [](int k) { return k; }, tag, s_g, &ch->abort_w, 20000000ull,
-                                             (unsigned *)nullptr);
-                    if (ok && t <= q) s_ue[t] = gd(s_g[2 * t], s_g[2 * t + 1]);
-                    if (t == 0) s_ue_ok = ok;
-                }
-                __syncthreads();
-                if (!s_ue_ok) {
-                    aborted = true;
-                    break;
-                }
-            }
         }
         if (liveB) d[1 + ia] = dj;
         if (!isA && tb == 0 && t == 0) d[0] = d0;
     }
     // leave; the last block out writes the batch's outcome into the state (every block holds
-    // the same outcome)
+    // the same outcome) and activates the batch's slack columns (every block's U stores were
+    // write-through and drained before its arrival; the last block reads them with sc1 loads)
     drain();
     __syncthreads();
     if (t == 0) {
         const unsigned k = __hip_atomic_fetch_add(&ch->exit_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (k == (unsigned)(NA + NB) - 1) {
-            __hip_atomic_store(&ch->exit_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (status0 != SX_NOT_ENDED) return;
-            if (ld_sc1(&ch->abort_w) != 0u || aborted) {
-                st->status = SX_HANG;
-                __hip_atomic_store(&ch->abort_w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                return;
-            }
-            // base[r] = e of every pivot, in order (solver.cu:105), only for a batch that completed
-            for (int s = 0; s < cnt; ++s) base[s_r[s]] = s_e[s];
-            st->status = status;
-            st->pivots = piv0 + cnt;
-            if (cnt > 0) {
-                st->r = last_r;
-                st->e = last_e;
-                st->batch_tag = B;
-                st->batch_count = cnt;
-            }
-            st->e_next = e;
-            st->dmin_next = dmin;
-        }
+        s_last = k == (unsigned)(NA + NB) - 1;
+        if (s_last) __hip_atomic_store(&ch->exit_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    __syncthreads();
+    if (!s_last || status0 != SX_NOT_ENDED) return;
+    const bool hang = ld_sc1(&ch->abort_w) != 0u || aborted;
+    if (!hang && perm != nullptr && cnt > 0)
+        activate_block(perm, iperm, act, nact, m, const_cast<double *>(T), rows, tl, c.s0, U, ld, s_r, cnt,
+                       reinterpret_cast<int *>(s_g), reinterpret_cast<int *>(s_g) + 64, reinterpret_cast<int *>(s_g) + 128,
+                       reinterpret_cast<int *>(s_g) + 192, reinterpret_cast<int *>(s_pay), s_hist);
+    if (t != 0) return;
+    if (hang) {
+        st->status = SX_HANG;
+        __hip_atomic_store(&ch->abort_w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    // base[r] = e of every pivot, in order (solver.cu:105), only for a batch that completed
+    for (int s = 0; s < cnt; ++s) base[s_r[s]] = s_e[s];
+    st->status = status;
+    st->pivots = piv0 + cnt;
+    if (cnt > 0) {
+        st->r = s_r[cnt - 1];
+        st->e = s_e[cnt - 1];
+        st->batch_tag = B;
+        st->batch_count = cnt;
+    }
+    st->e_next = e;
+    st->dmin_next = dmin;
 #undef SX_STAMP
 }
 
@@ -1709,7 +1855,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
             }
         }
     }
-    // this rank's slice of the objective row (its objective tiles' columns; d[0] on rank 0): between
+    // this rank's slice of the objective row (its objective tiles' columns; d[0] with tile 0): between
     // fused batches each rank keeps only its own slice current -- no rank writes another's d, so an
     // aborted batch cannot overwrite a peer's restored row -- and the host gathers the whole row
     // when it is needed (Engine::gather_d)
@@ -2057,7 +2203,7 @@ __global__ void k_sum_rows(double *out, const double *const *srcs, int nsrc, int
 }
 
 // A rank's contribution to the objective-row gather (Engine::gather_d): its slice [j0, j1) (and
-// d[0] on rank 0), -0.0 elsewhere; the sum all-reduce of the ranks' contributions is then the
+// d[0] on the rank holding tile 0), -0.0 elsewhere; the sum all-reduce of the ranks' contributions is then the
 // whole row bit for bit (x + -0.0 == x).
 __global__ void k_d_contrib(const double *__restrict__ d, double *__restrict__ out, int N, int j0, int j1, int with0) {
     for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < N; j += gridDim.x * blockDim.x)
@@ -2328,11 +2474,12 @@ bool sx_batch_fits(int rows, Cols c, int k) {
 
 void sx_launch_batch(const double *T, int rows, size_t ld, TLay tl, Cols c, double *d, double *d_save, int *base,
                      DevState *st, const Pending &pd, int k, BatchChan *chan, unsigned long long *ga,
-                     unsigned long long *gb, unsigned long long *stamps, hipStream_t s) {
+                     unsigned long long *gb, unsigned long long *stamps, int *perm, int *iperm, unsigned char *act,
+                     int *nact, int m, hipStream_t s) {
     if (!sx_batch_fits(rows, c, k)) SX_FATAL("fused batch grid does not fit the device");
     const int NA = (rows + SX_TILE - 1) / SX_TILE, NB = (c.N - 1 + SX_TILE - 1) / SX_TILE;
     k_batch<<<NA + NB, SX_TILE, batch_lds(k), s>>>(T, rows, ld, tl, c, d, d_save, base, st, pd.U, pd.F, pd.recs, pd.PM,
-                                                   pd.batch, k, NA, NB, chan, ga, gb, stamps);
+                                                   pd.batch, k, NA, NB, chan, ga, gb, stamps, perm, iperm, act, nact, m);
 }
 
 bool sx_batch_mr_fits(int slots, int nb_local, int k, int grids) {

@@ -85,3 +85,17 @@ def test_highs_objective(gpu, name):
         assert got.status == sx.INFEASIBLE, got.status_name
     else:  # unbounded
         assert got.status == sx.UNBOUNDED, got.status_name
+
+
+def test_mx250_numerical_failure_reproduced(gpu):
+    """The reference's one numerical-failure record: data/measures/mx250_2/benchmark_1024_8192.txt
+    holds 14,063 phase-1 pivots and no checkDegeneracy row, i.e. the solve returned INFEASIBLE
+    (twoPhaseMethod.cu:265-272) on a feasible instance (HiGHS: optimal 2.44407...,
+    tests/golden/highs_objectives.json).  The seed is n*100+m = 110592, from before the +1 the
+    authors added for this one instance (main.cu:63; the RTX record, seed 110593, is in the 36
+    above).  Bit-faithful arithmetic reproduces the failure: parity mode does not "fix" it."""
+    got = solve(1024, 8192, 110592, 1, 100)
+    assert got.status == sx.INFEASIBLE, got.status_name
+    assert tuple(got.pivots) == (14063, 0)
+    mx = [r for r in _load("published_pivots.json") if r["gpu"] == "mx250_2" and r["n"] == 1024 and r["m"] == 8192][0]
+    assert mx["p1_pivots"] == 14063 and mx["status"] == "infeasible"
