@@ -1,0 +1,78 @@
+"""The one-process multi-GPU mode of the drop-in ("Multi-GPU is internal: the
+caller still sees one synchronous call.  Device list comes from the env/flag SIMPLEX_GPUS"), and
+bench.py's --gpus N (needs an MI355X).
+
+On a one-GPU box the device list maps every shard onto GPU 0 ("0,0,0"): the same shards,
+exchanges and self-check as on N GPUs, minus the cross-device memory.  A list naming a GPU that
+is not visible must fail loudly, and `bench.py --gpus N` must refuse to print a line for fewer
+GPUs than asked.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+CHILD = r"""
+import sys, json
+sys.path.insert(0, {root!r})
+import numpy as np
+import simplexoncuda_amd as sx
+lib = sx.load()
+p = sx.generateRandomProblem({n}, {m}, {seed}, {lo}, {hi})
+r = sx.twoPhaseMethodEx(p)
+print(json.dumps({{"gpus": sx.gpus(), "status": r.status, "pivots": list(r.pivots), "opt": float(r.optimal_value).hex(),
+                  "x": [float(v).hex() for v in r.solution], "base": [int(b) for b in r.base],
+                  "p2p_ready": lib.simplex_p2p_ready(), "fused": lib.simplex_fused_batches(),
+                  "hangs": lib.simplex_hang_recoveries()}}))
+"""
+
+
+def run_child(env_gpus, n, m, seed, lo, hi):
+    env = dict(os.environ, SIMPLEX_GPUS=env_gpus)
+    code = CHILD.format(root=ROOT, n=n, m=m, seed=seed, lo=lo, hi=hi)
+    return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=240)
+
+
+@pytest.mark.parametrize("gpus", ["0,0", "0,0,0", "0,0,0,0,0,0,0,0"])
+@pytest.mark.parametrize("n,m,seed,lo,hi", [(300, 1100, 41100, 1, 100), (129, 1513, 77, -100, 100)])
+def test_unchanged_caller_gets_shards_from_env(gpu, gpus, n, m, seed, lo, hi):
+    import json
+    r = run_child(gpus, n, m, seed, lo, hi)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    assert got["gpus"] == [int(x) for x in gpus.split(",")]
+    A, b, c = oracle.generate(n, m, seed, lo, hi)
+    ref = oracle.two_phase(A, b, c)
+    assert got["status"] == ref["status"] and tuple(got["pivots"]) == ref["pivots"]
+    assert np.array_equal(np.array(got["base"]), ref["base"])
+    if ref["status"] == 0:
+        assert got["opt"] == float(ref["opt"]).hex()
+        assert got["x"] == [float(v).hex() for v in ref["x"]]
+    # the mode's start-up self-check passed: the batches ran on the peer-memory path, none re-run
+    assert got["p2p_ready"] == 1 and got["fused"] > 0 and got["hangs"] == 0
+
+
+def test_missing_device_is_fatal(gpu):
+    import torch
+    n_vis = torch.cuda.device_count()
+    r = run_child(",".join(str(i) for i in range(n_vis + 1)), 20, 10, 2010, 1, 100)
+    assert r.returncode != 0
+    assert f"SIMPLEX_GPUS: device {n_vis} requested but {n_vis} visible" in r.stdout + r.stderr
+
+
+def test_bench_refuses_more_gpus_than_visible(gpu):
+    import torch
+    n_vis = torch.cuda.device_count()
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "SIMPLEX_GPUS")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n_vis + 1), "--steps", "1",
+                        "--warmup", "0"], capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 2, r.stdout[-2000:] + r.stderr[-2000:]
+    assert f"--gpus {n_vis + 1} needs {n_vis + 1} GPUs, {n_vis} visible" in r.stderr
+    assert r.stdout.strip() == ""  # no bench line
