@@ -1506,20 +1506,23 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
 // exchanging over peer memory (xGMI) inside the launch instead of RCCL calls between
 // launches.  Rank k runs `slots` ratio tiles (its rows) and the objective tiles [tb0, tb1)
 // of the logical row (the objective work is split across ranks; every rank still gets every
-// decision).  Per pivot q:
-//   ratio tiles       as k_batch; each tile winner (+ the winning row's factor history) is
-//                     written as tagged granules into EVERY rank's ga[global tile];
-//   every block       reads all W * slots ratio tiles from its own ga and runs pass 2;
-//   objective tiles   read the leaving row's stored values straight from its owner's
-//                     tableau (remote loads), form the current pivot row on their columns,
-//                     write it into every rank's U[q] (the sweep's input), update their d,
-//                     and publish the tile winner (+ the winning column's pivot-row history)
-//                     into every rank's gb;
-//   every block       reads all objective tiles from its own gb and runs pass 2.
-// At the end of the batch the d slices go to every rank, then a done granule per rank: a
-// rank's last block leaves only when every rank's data has landed, so the sweep that follows
-// reads complete U and d.  Cross-rank stores and loads are system-scope (sc0 sc1); the polled
-// arrays are uncached allocations.  The same arithmetic, trees and order as k_batch.
+// decision).  The hand-offs are k_batch's, each read only by the blocks that need it:
+//   ratio tiles       as k_batch; each tile winner (+ the winning row's factor history, the
+//                     pivot's e and d_e) is written as tagged granules into EVERY rank's
+//                     ga[global tile];
+//   objective tiles   read all W * slots ratio records from their own ga and run pass 2, read
+//                     the leaving row's stored values straight from its owner's tableau (remote
+//                     loads), form the current pivot row on their columns, write it into every
+//                     rank's U[q] (the sweep's input), update their d slice, and publish the
+//                     tile winner (+ the winning column's pivot-row history, r, p, the RHS) into
+//                     every rank's gb;
+//   ratio tiles       read all objective records from their own gb and run pass 2 (the next
+//                     entering variable), and apply the pivot to their rows.
+// Between batches every rank keeps only its own slice of d current (Engine::gather_d).  At the
+// end of the batch a done granule per rank: a rank's last block leaves only when every rank's
+// data has landed, so the sweep that follows reads complete U.  Cross-rank stores and loads are
+// system-scope (sc0 sc1); the records polled across GPUs are uncached allocations.  The same
+// arithmetic, trees and order as k_batch.
 __device__ __forceinline__ void put_g_sys(u64 *g, unsigned data, unsigned tag) {
     __hip_atomic_store(g, ((u64)tag << 32) | data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -1531,13 +1534,13 @@ __device__ __forceinline__ double ld_sys(const double *p) {
     return __longlong_as_double((long long)ld_sys(reinterpret_cast<const u64 *>(p)));
 }
 
-__device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const double *__restrict__ T, int rows, int row0, int rpr, size_t ld, TLay tl,
-                                                  Cols c, double *__restrict__ d, double *__restrict__ d_save, int *base,
-                                                  DevState *st, double *U, double *F, PivRec *recs,
-                                                  unsigned long long *PM, unsigned B, int K,
-                                                  int slots, int W, int rank, int tb0, int tb1, int NBg,
-                                                  BatchChan *ch, const u64 *ga, const u64 *gb, const u64 *gdone,
-                                                  PeerView pv, unsigned long long timeout) {
+__device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const double *__restrict__ T, int rows, int row0,
+                                              int rpr, size_t ld, TLay tl, Cols c, double *__restrict__ d,
+                                              double *__restrict__ d_save, int *base, DevState *st, double *U, double *F,
+                                              PivRec *recs, unsigned long long *PM, unsigned B, int K, int slots, int W,
+                                              int rank, int tb0, int tb1, int NBg, BatchChan *ch, const u64 *ga,
+                                              const u64 *gb, const u64 *gdone, PeerView pv,
+                                              unsigned long long timeout) {
     extern __shared__ double s_hist[];  // [K][512]: F history (ratio tiles) / U history (objective tiles)
     __shared__ double s_v[16];
     __shared__ int s_i[16];
@@ -1549,8 +1552,8 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
     __shared__ unsigned s_pay[SX_TILE];
     __shared__ int s_ok, s_flag;
     // per-step results written by wave 0 before the step's one barrier (as in k_batch)
-    __shared__ int s_sel_ok, s_sel_r, s_sel_any, s_det_ok, s_ent_ok, s_ent_e, s_ue_ok;
-    __shared__ double s_ent_v, s_br;
+    __shared__ int s_sel_ok, s_sel_r, s_sel_any, s_det_ok, s_det_e, s_det_st, s_ent_ok, s_ent_e, s_ent_r, s_ent_st;
+    __shared__ double s_det_dmin, s_ent_v, s_br, s_ent_p;
     __shared__ int s_welig[SX_TILE / 64];
     const int t = threadIdx.x;
     const bool isA = bid < slots;
@@ -1559,7 +1562,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
     const long long piv0 = st->pivots, cap = st->max_pivots;
     int e = st->e_next;
     double dmin = st->dmin_next;
-    int status = SX_NOT_ENDED, cnt = 0, last_r = -1, last_e = -1;
+    int status = SX_NOT_ENDED, cnt = 0;
     bool aborted = false;
     auto gather_a = [](int k) { return rec2_a(k); };
     auto gather_b = [](int k) { return rec2_b(k); };
@@ -1590,17 +1593,12 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 status = SX_PIVOT_CAP;
                 break;
             }
-            if (!(cmp_eps(dmin, 0.0) < 0)) {  // solver.cu:88
-                status = SX_FEASIBLE;
-                break;
-            }
-            double a = 0.0;
             if (isA) {
-                // pending pivots of the batch, in order
-                a = hist_col(a_pre, q, bits, s_hist, s_ue, s_p);
+                const bool done = !(cmp_eps(dmin, 0.0) < 0);  // solver.cu:88: optimal
+                const double a = done ? 0.0 : hist_col(a_pre, q, bits, s_hist, s_ue, s_p);
                 double rv = DBL_MAX;
                 int ri = -1, elig = 0;
-                if (liveA) {
+                if (liveA && !done) {
                     elig = a >= SX_EPS;
                     const double ratio = cmp_eps(a, 0.0) > 0 ? b / a : DBL_MAX;  // reduction.cu:106-114
                     if (cmp_eps(ratio, rv) < 0) {
@@ -1631,23 +1629,99 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                     wv = __longlong_as_double(((long long)__builtin_amdgcn_readfirstlane((int)(vb >> 32)) << 32) |
                                               (long long)(unsigned)__builtin_amdgcn_readfirstlane((int)vb));
                     const int wl = wi >= 0 ? wi - row0 - bid * SX_TILE : 0;
-                    // the record (v, pad, a, b, F[winner][s < q]) into every rank's copy
+                    // the record into every rank's copy
                     const unsigned pl = (wi >= 0 ? (unsigned)(wi - gt * SX_TILE) : SX_NOIDX) | ((unsigned)any << 10);
-                    const int nG = 8 + 2 * q;
+                    const int nG = kRF + 2 * q;
                     for (int idx = t; idx < W * nG; idx += 64) {
                         const int rk = idx / nG, k = idx - rk * nG;
-                        if (k == 2 || k == 3) continue;
-                        const double val = k < 2 ? wv : k < 6 ? s_a[wl] : k < 8 ? s_b[wl]
-                                                                        : s_hist[((k - 8) >> 1) * SX_TILE + wl];
-                        const unsigned long long bits64 = (unsigned long long)__double_as_longlong(val);
-                        put_g_sys(pv.ga[rk] + (size_t)gt * SX_GA_STRIDE + k,
-                                  (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64, k < 2 ? (tag | pl) : tag);
+                        unsigned data;
+                        if (k == kRE) {
+                            data = (unsigned)e;
+                        } else if (k == kRS) {
+                            data = (unsigned)(done ? SX_FEASIBLE : SX_NOT_ENDED);
+                        } else {
+                            const double val = k < kRD ? wv : k < kRA ? dmin : k < kRB ? s_a[wl] : k < kRE ? s_b[wl]
+                                                                           : s_hist[((k - kRF) >> 1) * SX_TILE + wl];
+                            const u64 bits64 = (u64)__double_as_longlong(val);
+                            data = (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64;
+                        }
+                        put_g_sys(pv.ga[rk] + (size_t)gt * SX_GA_STRIDE + k, data, k < kRD ? (tag | pl) : tag);
                     }
                 }
-            }
-            // ---- selection: pass 2 over every rank's ratio tiles (wave 0 polls and reduces)
-            int r, anyall;
-            if (2 * NAg <= 64 * SX_GATHER_PER_LANE) {
+                if (done) {
+                    status = SX_FEASIBLE;
+                    break;
+                }
+                // ---- the objective side's answer (every rank's objective tiles, from this rank's gb):
+                // the next entering variable, then r, p, the RHS, the status and U[s <= q][e]
+                if (t < 64) {
+                    int ok = poll_wave<decltype(gather_b), true>(gb, 2 * NBg, gather_b, tag, s_g, &ch->abort_w, timeout,
+                                                                 s_pay);
+                    double ev = DBL_MAX;
+                    int ei = -1, any = 0;
+                    if (ok) wave_pass2(s_g, s_pay, NBg, s_v, s_i, ev, ei, any);
+                    ei = __builtin_amdgcn_readfirstlane(ei);
+                    if (ok) {
+                        const int wt = ei >= 0 ? ei / SX_TILE : 0;
+                        ok = poll_wave<decltype(ident), true>(gb + (size_t)wt * SX_GB_STRIDE + kOP,
+                                                              (kOU - kOP) + 2 * (q + 1), ident, tag, s_g, &ch->abort_w,
+                                                              timeout, (unsigned *)nullptr);
+                        if (ok && t <= q) s_ue[t] = gd(s_g[kOU - kOP + 2 * t], s_g[kOU - kOP + 1 + 2 * t]);
+                    }
+                    if (t == 0) {
+                        s_ent_ok = ok;
+                        s_ent_e = ei;
+                        s_ent_v = ev;
+                        if (ok) {
+                            s_ent_p = gd(s_g[0], s_g[1]);
+                            s_br = gd(s_g[kOB - kOP], s_g[kOB - kOP + 1]);
+                            s_ent_r = (int)s_g[kOR - kOP];
+                            s_ent_st = (int)s_g[kOS - kOP];
+                        }
+                    }
+                }
+                __syncthreads();
+                if (!s_ent_ok) {
+                    aborted = true;
+                    break;
+                }
+                if (s_ent_st != SX_NOT_ENDED) {
+                    status = s_ent_st;
+                    break;
+                }
+                const int r = s_ent_r;
+                const double p = s_ent_p, br = s_br;
+                if (t == 0) {
+                    s_p[q] = p;
+                    s_r[q] = r;
+                    s_e[q] = e;
+                }
+                cnt = q + 1;
+                const double f = -a / p;
+                s_hist[q * SX_TILE + t] = f;
+                if (liveA) {
+                    F[(size_t)li * SX_KMAX + q] = f;
+                    if (row0 + li == r) {
+                        b = b / p;
+                        bits |= 1u << q;
+                        const u64 w = PM[li];
+                        PM[li] = (((unsigned)(w >> 32) == B) ? w : ((u64)B << 32)) | (1ull << q);
+                    } else {
+                        b = fma(f, br, b);
+                    }
+                }
+                if (bid == 0 && t == 0) {  // every rank keeps the whole basis and the records
+                    recs[q].r = r;         // (base[r] = e, solver.cu:105: at the end of the batch)
+                    recs[q].e = e;
+                    recs[q].p = p;
+                    U[(size_t)q * ld] = br;
+                }
+                e = s_ent_e;
+                dmin = s_ent_v;
+                if (liveA) a_pre = T[tl.idx(li, c.map(1 + (e >= 0 ? e : 0)))];
+                __syncthreads();
+            } else {
+                // ---- selection: pass 2 over every rank's ratio tiles (wave 0 polls and reduces)
                 if (t < 64) {
                     const int ok = poll_wave<decltype(gather_a), true>(ga, 2 * NAg, gather_a, tag, s_g, &ch->abort_w,
                                                                        timeout, s_pay);
@@ -1665,105 +1739,69 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                     aborted = true;
                     break;
                 }
-                r = s_sel_r;
-                anyall = s_sel_any;
-            } else {
-                if (!gather_tagged<decltype(gather_a), true>(ga, 2 * NAg, gather_a, tag, s_g, &ch->abort_w, &s_ok,
-                                                             timeout, s_pay)) {
+                const int r = s_sel_r;
+                // the leaving row's stored values, from its owner's tableau (read-only in this launch)
+                double u = 0.0;
+                if (liveB && r >= 0) {
+                    const int owner = r / rpr;
+                    const double *src = pv.T[owner] + tl.idx(r - owner * rpr, mj);  // (every rank: the same layout)
+                    u = owner == rank ? *src : ld_sys(src);
+                }
+                // the winner's record (ratio tile 0's when there is none): d_e, p, the RHS, e, the
+                // ratio side's status and F[r][s < q], read by wave 0 into LDS
+                if (t < 64) {
+                    const int wt = r >= 0 ? r / SX_TILE : 0;
+                    const int ok = poll_wave<decltype(ident), true>(ga + (size_t)wt * SX_GA_STRIDE + kRD,
+                                                                    (kRF - kRD) + 2 * q, ident, tag, s_g, &ch->abort_w,
+                                                                    timeout, (unsigned *)nullptr);
+                    if (ok) {
+                        if (t < q) s_fr[t] = gd(s_g[kRF - kRD + 2 * t], s_g[kRF - kRD + 1 + 2 * t]);
+                        if (t == 0) {
+                            s_det_dmin = gd(s_g[0], s_g[1]);
+                            s_p[q] = gd(s_g[kRA - kRD], s_g[kRA - kRD + 1]);
+                            s_br = gd(s_g[kRB - kRD], s_g[kRB - kRD + 1]);
+                            s_det_e = (int)s_g[kRE - kRD];
+                            s_det_st = (int)s_g[kRS - kRD];
+                            s_r[q] = r;
+                            s_e[q] = (int)s_g[kRE - kRD];
+                        }
+                    }
+                    if (t == 0) s_det_ok = ok;
+                }
+                __syncthreads();
+                if (!s_det_ok) {
                     aborted = true;
                     break;
                 }
-                double tv = DBL_MAX;
-                int ti = -1, te = 0;
-                if (t < NAg) {
-                    const double cv = gd(s_g[2 * t], s_g[2 * t + 1]);
-                    const unsigned pl = s_pay[t];
-                    te = (int)((pl >> 10) & 1u);
-                    if (cmp_eps(cv, tv) < 0) {
-                        tv = cv;
-                        ti = (pl & SX_NOIDX) == SX_NOIDX ? -1 : t * SX_TILE + (int)(pl & SX_NOIDX);
-                    }
+                e = s_det_e;
+                dmin = s_det_dmin;
+                if (s_det_st != SX_NOT_ENDED) {  // the ratio side ended the phase (optimal)
+                    status = s_det_st;
+                    break;
                 }
-                anyall = __syncthreads_or(SX_ELIG(te));
-                block_argmin512(tv, ti, s_v, s_i);
-                if (t == 0) s_sel_r = ti;
-                __syncthreads();
-                r = s_sel_r;
-            }
-            if (!anyall) {  // solver.cu:96-102
-                status = SX_UNBOUNDED;
-                break;
-            }
-            if (r < 0) {
-                status = SX_NUMERIC_FAIL;
-                break;
-            }
-            // the leaving row's stored values, from its owner's tableau (read-only in this launch)
-            const int owner = r / rpr;
-            double u = 0.0;
-            if (liveB) {
-                const double *src = pv.T[owner] + tl.idx(r - owner * rpr, mj);  // (every rank: the same layout)
-                u = owner == rank ? *src : ld_sys(src);
-            }
-            // the winner's details (pivot, RHS, factor history), read by wave 0 into LDS
-            if (t < 64) {
-                const int ok = poll_wave<decltype(ident), true>(ga + (size_t)(r / SX_TILE) * SX_GA_STRIDE + 4, 4 + 2 * q,
-                                                                ident, tag, s_g, &ch->abort_w, timeout,
-                                                                (unsigned *)nullptr);
-                if (ok) {
-                    if (t < q) s_fr[t] = gd(s_g[4 + 2 * t], s_g[5 + 2 * t]);
-                    if (t == 0) {
-                        s_p[q] = gd(s_g[0], s_g[1]);
-                        s_br = gd(s_g[2], s_g[3]);
-                        s_r[q] = r;
-                        s_e[q] = e;
-                    }
+                int ost = SX_NOT_ENDED;
+                if (!s_sel_any) {
+                    ost = SX_UNBOUNDED;  // solver.cu:96-102
+                } else if (r < 0) {
+                    ost = SX_NUMERIC_FAIL;
                 }
-                if (t == 0) s_det_ok = ok;
-            }
-            __syncthreads();
-            if (!s_det_ok) {
-                aborted = true;
-                break;
-            }
-            const double p = s_p[q], br = s_br;
-            cnt = q + 1;
-            last_r = r;
-            last_e = e;
-            if (isA) {
-                const double f = -a / p;
-                s_hist[q * SX_TILE + t] = f;
-                if (liveA) {
-                    F[(size_t)li * SX_KMAX + q] = f;
-                    if (row0 + li == r) {
-                        b = b / p;
-                        bits |= 1u << q;
-                        const u64 w = PM[li];
-                        PM[li] = (((unsigned)(w >> 32) == B) ? w : ((u64)B << 32)) | (1ull << q);
-                    } else {
-                        b = fma(f, br, b);
-                    }
-                }
-                if (bid == 0 && t == 0) {  // every rank keeps the whole basis and the records
-                    recs[q].r = r;                // (base[r] = e, solver.cu:105: at the end of the batch)
-                    recs[q].e = e;
-                    recs[q].p = p;
-                    U[(size_t)q * ld] = br;
-                }
-            } else {
-                u = hist_row(u, q, r, s_hist, s_fr, s_p, s_r);
-                s_hist[q * SX_TILE + t] = u;
-                if (liveB && 1 + ia < c.Ns)
-                    for (int k = 0; k < W; ++k) st_sys(pv.U[k] + (size_t)q * ld + mj, u);
-                const double fd = -dmin / p;  // updateCostsVector, solver.cu:48-56
-                if (tb == 0 && t == 0) d0 = fma(fd, br, d0);
+                const double p = s_p[q], br = s_br;
                 double v = DBL_MAX;
                 int i = -1;
-                if (liveB) {
-                    dj = fma(fd, u, dj);
-                    if (cmp_eps(dj, v) < 0) {
-                        v = dj;
-                        i = ia;
+                if (ost == SX_NOT_ENDED) {
+                    cnt = q + 1;
+                    u = hist_row(u, q, r, s_hist, s_fr, s_p, s_r);
+                    s_hist[q * SX_TILE + t] = u;
+                    if (liveB && 1 + ia < c.Ns)
+                        for (int k = 0; k < W; ++k) st_sys(pv.U[k] + (size_t)q * ld + mj, u);
+                    const double fd = -dmin / p;  // updateCostsVector, solver.cu:48-56
+                    if (tb == 0 && t == 0) d0 = fma(fd, br, d0);
+                    if (liveB) {
+                        dj = fma(fd, u, dj);
+                        if (cmp_eps(dj, v) < 0) {
+                            v = dj;
+                            i = ia;
+                        }
                     }
                 }
                 half_argmin(v, i);
@@ -1781,78 +1819,50 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                     wv = __longlong_as_double(((long long)__builtin_amdgcn_readfirstlane((int)(vb >> 32)) << 32) |
                                               (long long)(unsigned)__builtin_amdgcn_readfirstlane((int)vb));
                     const int win = wi >= 0 ? wi - tb * SX_TILE : 0;
-                    // the record (v, pad, U[s <= q][winner]) into every rank's copy
                     const unsigned pl = wi >= 0 ? (unsigned)win : SX_NOIDX;
-                    const int nG = 4 + 2 * (q + 1);
+                    const int nG = kOU + 2 * (q + 1);
                     for (int idx = t; idx < W * nG; idx += 64) {
                         const int rk = idx / nG, k = idx - rk * nG;
-                        if (k == 2 || k == 3) continue;
-                        const double val = k < 2 ? wv : s_hist[((k - 4) >> 1) * SX_TILE + win];
-                        const unsigned long long bits64 = (unsigned long long)__double_as_longlong(val);
-                        put_g_sys(pv.gb[rk] + (size_t)tb * SX_GB_STRIDE + k,
-                                  (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64, k < 2 ? (tag | pl) : tag);
+                        unsigned data;
+                        if (k == kOR) {
+                            data = (unsigned)r;
+                        } else if (k == kOS) {
+                            data = (unsigned)ost;
+                        } else {
+                            const double val = k < kOP ? wv : k < kOB ? p : k < kOR ? br
+                                                                            : s_hist[((k - kOU) >> 1) * SX_TILE + win];
+                            const u64 bits64 = (u64)__double_as_longlong(val);
+                            data = (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64;
+                        }
+                        put_g_sys(pv.gb[rk] + (size_t)tb * SX_GB_STRIDE + k, data, k < kOP ? (tag | pl) : tag);
                     }
+                }
+                if (ost != SX_NOT_ENDED) {
+                    status = ost;
+                    break;
                 }
             }
-            // ---- entering variable of pivot q + 1: pass 2 over every objective tile (wave 0)
-            if (2 * NBg <= 64 * SX_GATHER_PER_LANE) {
-                if (t < 64) {
-                    const int ok = poll_wave<decltype(gather_b), true>(gb, 2 * NBg, gather_b, tag, s_g, &ch->abort_w,
-                                                                       timeout, s_pay);
-                    double ev = DBL_MAX;
-                    int ei = -1, any = 0;
-                    if (ok) wave_pass2(s_g, s_pay, NBg, s_v, s_i, ev, ei, any);
-                    if (t == 0) {
-                        s_ent_ok = ok;
-                        s_ent_e = ei;
-                        s_ent_v = ev;
-                    }
-                }
-                __syncthreads();
-                if (!s_ent_ok) {
-                    aborted = true;
-                    break;
-                }
-            } else {
-                if (!gather_tagged<decltype(gather_b), true>(gb, 2 * NBg, gather_b, tag, s_g, &ch->abort_w, &s_ok,
-                                                             timeout, s_pay)) {
-                    aborted = true;
-                    break;
-                }
+        }
+        // a batch that ended without a decision of the ratio side: the objective tiles learn the
+        // next entering variable from the last objective records (k_batch)
+        if (!isA && !aborted && (status == SX_NOT_ENDED || status == SX_PIVOT_CAP) && cnt > 0) {
+            const unsigned tag = make_tag(B, cnt - 1);
+            if (t < 64) {
+                const int ok = poll_wave<decltype(gather_b), true>(gb, 2 * NBg, gather_b, tag, s_g, &ch->abort_w,
+                                                                   timeout, s_pay);
                 double ev = DBL_MAX;
-                int ei = -1;
-                if (t < NBg) {
-                    const double cv = gd(s_g[2 * t], s_g[2 * t + 1]);
-                    const unsigned pl = s_pay[t] & SX_NOIDX;
-                    if (cmp_eps(cv, ev) < 0) {
-                        ev = cv;
-                        ei = pl == SX_NOIDX ? -1 : t * SX_TILE + (int)pl;
-                    }
-                }
-                block_argmin512(ev, ei, s_v, s_i);
+                int ei = -1, any = 0;
+                if (ok) wave_pass2(s_g, s_pay, NBg, s_v, s_i, ev, ei, any);
                 if (t == 0) {
+                    s_ent_ok = ok;
                     s_ent_e = ei;
                     s_ent_v = ev;
                 }
-                __syncthreads();
             }
+            __syncthreads();
+            if (!s_ent_ok) aborted = true;
             e = s_ent_e;
             dmin = s_ent_v;
-            if (liveA) a_pre = T[tl.idx(li, c.map(1 + (e >= 0 ? e : 0)))];
-            if (isA && q + 1 < K && e >= 0 && cmp_eps(dmin, 0.0) < 0) {
-                if (t < 64) {  // (wave 0 reads them into LDS)
-                    const int ok = poll_wave<decltype(ident), true>(gb + (size_t)(e / SX_TILE) * SX_GB_STRIDE + 4,
-                                                                    2 * (q + 1), ident, tag, s_g, &ch->abort_w, timeout,
-                                                                    (unsigned *)nullptr);
-                    if (ok && t <= q) s_ue[t] = gd(s_g[2 * t], s_g[2 * t + 1]);
-                    if (t == 0) s_ue_ok = ok;
-                }
-                __syncthreads();
-                if (!s_ue_ok) {
-                    aborted = true;
-                    break;
-                }
-            }
         }
     }
     // this rank's slice of the objective row (its objective tiles' columns; d[0] with tile 0): between
@@ -1900,8 +1910,8 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
     st->status = status;
     st->pivots = piv0 + cnt;
     if (cnt > 0) {
-        st->r = last_r;
-        st->e = last_e;
+        st->r = s_r[cnt - 1];
+        st->e = s_e[cnt - 1];
         st->batch_tag = B;
         st->batch_count = cnt;
     }
