@@ -90,9 +90,9 @@ void simplex_set_regions(int mode);
 /* virtual shards with the peer-memory batch: every rank's batch in one launch (1, default) or one
  * launch per rank on its own stream (0; needs as many hardware queues running at once) */
 void simplex_set_mr_single_launch(int on);
-/* several shards: keep d and U in uncached memory (1) or plain memory (0, default; uncached
- * was measured to corrupt results after earlier allocations were freed -- diagnostic only) */
-void simplex_set_uncached_exchange(int on);
+/* several shards, diagnostic: allocate the exchanged buffers uncached -- bit 0 d, bit 1 U (3 = both,
+ * 0 = plain memory, the default) -- see DESIGN.md §5 for what uncached exchange buffers did */
+void simplex_set_uncached_exchange(int mode);
 
 /* ---- fault handling and test hooks ---- */
 /* a fused batch whose in-kernel hand-off wait times out (SIMPLEX_HANG, never expected) is

@@ -658,15 +658,17 @@ class Engine {
         // the oracle in 3 of 3 runs (1126 / 1124 / 1181 phase-1 pivots instead of 1318), and
         // never with plain memory (tools/_bisect_seq.py) -- dirty L2 lines of a
         // page's earlier cached use written back over the uncached data is the likely cause.
-        if (xchg && g_cfg.uncached_xchg) {
+        // (diagnostic bisect: bit 0 = d uncached, bit 1 = U uncached)
+        if (xchg && (g_cfg.uncached_xchg & 1))
             SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&x.d), round_up((size_t)N1, 16) * sizeof(double),
                                          hipDeviceMallocUncached));
+        else
+            x.d = dalloc<double>(round_up((size_t)N1, 16));
+        if (xchg && (g_cfg.uncached_xchg & 2))
             SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&x.U), (size_t)SX_KMAX * ld * sizeof(double),
                                          hipDeviceMallocUncached));
-        } else {
-            x.d = dalloc<double>(round_up((size_t)N1, 16));
+        else
             x.U = dalloc<double>((size_t)SX_KMAX * ld);
-        }
         x.d_save = dalloc<double>(round_up((size_t)N1, 16));
         x.colE = dalloc<double>(rows_alloc);
         x.prow = dalloc<double>(ld);
@@ -1693,7 +1695,7 @@ void simplex_last_phase_seconds(double *out) {
     out[1] = g_phase_seconds[1];
 }
 void simplex_set_update_waves(double waves) { sx_set_update_waves((float)waves); }
-void simplex_set_uncached_exchange(int on) { g_cfg.uncached_xchg = on ? 1 : 0; }
+void simplex_set_uncached_exchange(int mode) { g_cfg.uncached_xchg = mode < 0 ? 0 : mode & 3; }
 void simplex_set_exchange_mode(int mode) { g_cfg.exchange_mode = (mode >= 0 && mode <= 2) ? mode : 0; }
 void simplex_set_timer_dir(const char *dir) { g_cfg.timer_dir = dir ? dir : ""; }
 

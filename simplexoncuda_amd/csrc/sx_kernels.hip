@@ -1282,6 +1282,10 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     break;
                 }
                 // ---- this pivot's factor column and the rows' new RHS (solver.cu:34-46)
+                // the next entering column's stored value of this row: its load first (HBM latency),
+                // then this pivot's updates while it is in flight
+                const int enext = s_ent_e;
+                if (liveA) a_pre = T[tl.idx(li, c.map(1 + (enext >= 0 ? enext : 0)))];
                 const int r = s_ent_r;
                 const double p = s_ent_p, br = s_br;
                 if (t == 0) {
@@ -1309,9 +1313,8 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     recs[q].p = p;
                     U[(size_t)q * ld] = br;  // the pivot row's RHS entry, for the sweep
                 }
-                e = s_ent_e;
+                e = enext;
                 dmin = s_ent_v;
-                if (liveA) a_pre = T[tl.idx(li, c.map(1 + (e >= 0 ? e : 0)))];
                 __syncthreads();  // (s_p / s_ue of this step are read by the next pivot's chain)
             } else {
                 // ---- selection: pass 2 over the ratio tiles (wave 0 polls and runs the tree)
@@ -1689,6 +1692,8 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                     status = s_ent_st;
                     break;
                 }
+                const int enext = s_ent_e;
+                if (liveA) a_pre = T[tl.idx(li, c.map(1 + (enext >= 0 ? enext : 0)))];
                 const int r = s_ent_r;
                 const double p = s_ent_p, br = s_br;
                 if (t == 0) {
@@ -1716,9 +1721,8 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                     recs[q].p = p;
                     U[(size_t)q * ld] = br;
                 }
-                e = s_ent_e;
+                e = enext;
                 dmin = s_ent_v;
-                if (liveA) a_pre = T[tl.idx(li, c.map(1 + (e >= 0 ? e : 0)))];
                 __syncthreads();
             } else {
                 // ---- selection: pass 2 over every rank's ratio tiles (wave 0 polls and reduces)

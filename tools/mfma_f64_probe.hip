@@ -13,17 +13,18 @@
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
 
-// assumed operand layout (checked below against a plain product):
+// operand layout (checked below against a plain product; a first run with C/D row 4 (l / 16) + v
+// matched only the 64 elements where the two formulas agree):
 //   A 16x4: lane l holds A[l % 16][l / 16];  B 4x16: lane l holds B[l / 16][l % 16];
-//   C/D 16x16: lane l, register v holds [4 (l / 16) + v][l % 16]
+//   C/D 16x16: lane l, register v holds [l / 16 + 4 v][l % 16]
 __global__ void k_mfma(const double *A, const double *B, const double *C, double *D, int reps) {
     const int l = threadIdx.x;
     const double a = A[(l % 16) * 4 + l / 16];
     const double b = B[(l / 16) * 16 + l % 16];
     double4_t c;
-    for (int v = 0; v < 4; ++v) c[v] = C[(4 * (l / 16) + v) * 16 + l % 16];
+    for (int v = 0; v < 4; ++v) c[v] = C[(l / 16 + 4 * v) * 16 + l % 16];
     for (int r = 0; r < reps; ++r) c = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-    for (int v = 0; v < 4; ++v) D[(4 * (l / 16) + v) * 16 + l % 16] = c[v];
+    for (int v = 0; v < 4; ++v) D[(l / 16 + 4 * v) * 16 + l % 16] = c[v];
 }
 
 // the sequential chain in the order k = 0..3 (order 0) or 3..0 (order 1)
