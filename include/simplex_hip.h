@@ -24,7 +24,9 @@ extern "C" {
 int simplex_version(void);
 void simplex_set_verbose(int on);            /* reference progress lines on stdout */
 void simplex_set_update_rows(int rb);        /* rows per sweep step: 1, 2, 4; 0 = auto */
-void simplex_set_store_sc1(int mode);        /* write-through tableau stores: -1 auto, 0, 1 */
+/* the sweep's cache policy: -1 auto; 0 nt loads + plain stores, 1 nt loads + write-through (sc1)
+ * stores, 2 default loads + sc1 stores, 3 default loads + plain stores, 4 nt loads + nt stores */
+void simplex_set_store_sc1(int mode);
 /* pivots per tableau sweep (1..32, default 32): the pivots of a batch are selected on the
  * current values (pending pivots applied on the fly) and then applied to the tableau in one
  * sweep -- the same IEEE operations in the same order as one sweep per pivot */

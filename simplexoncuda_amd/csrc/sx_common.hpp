@@ -148,7 +148,9 @@ struct TLay {
 struct SweepCfg {
     int batch;           // pivots per sweep (1..SX_KMAX): register slots of the sweep
     int rows_per_block;  // 1, 2 or 4 rows per step
-    int sc1;             // write-through (sc1) tableau stores
+    int sc1;             // cache policy of the tableau traffic: 0 nt loads + plain stores, 1 nt loads +
+                         // write-through (sc1) stores (default), 2 default loads + sc1 stores,
+                         // 3 default loads + plain stores, 4 nt loads + nt stores (32-slot sweeps)
 };
 
 int sx_enter_blocks(int L);

@@ -1033,7 +1033,7 @@ class Engine {
         c.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : 1;
         // peer ranks read leaving rows straight from this tableau (system-scope loads over
         // xGMI): its stores must write through to memory, not stay dirty in an L2 of this device
-        if (p2p && rccl) c.sc1 = 1;
+        if (p2p && (rccl || multidev) && c.sc1 != 1 && c.sc1 != 2) c.sc1 = 1;
         return c;
     }
 
@@ -1659,7 +1659,7 @@ extern "C" {
 int simplex_version(void) { return 1; }
 void simplex_set_verbose(int on) { g_cfg.verbose = on; }
 void simplex_set_update_rows(int rb) { g_cfg.update_rows = (rb == 1 || rb == 2 || rb == 4 || rb == 8) ? rb : 0; }
-void simplex_set_store_sc1(int mode) { g_cfg.sc1 = mode < 0 ? -1 : (mode ? 1 : 0); }
+void simplex_set_store_sc1(int mode) { g_cfg.sc1 = mode < 0 ? -1 : (mode <= 4 ? mode : 1); }
 void simplex_set_batch(int pivots) { g_cfg.batch = pivots > 0 ? std::min(pivots, SX_KMAX) : 32; }
 void simplex_set_device(int device) {
     g_cfg.device = device;

@@ -1995,7 +1995,10 @@ __device__ __forceinline__ void sweep_record(int *rec, const DevState *st, const
     }
 }
 
-template <int KT, int RB, bool SC1>
+// POL: cache policy of the tableau traffic -- 0 nt loads + plain stores, 1 nt loads + write-through
+// (sc1) stores (default), 2 default-policy loads + sc1 stores, 3 default loads + plain stores,
+// 4 nt loads + nt stores (sweep-policy A/B, SweepCfg.sc1)
+template <int KT, int RB, int POL>
 __global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, TLay tl, int Ns,
                                                const int *__restrict__ nact, int s0,
                                                const double *__restrict__ F, const double *__restrict__ U,
@@ -2034,13 +2037,14 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, T
         double2 x[RB];
         // non-temporal loads (cache policy nt): each element is read once per sweep; measured
         // 1.5 % faster at config 5, neutral at config 3 (profiles/r01_v13_sweep_load_policy.txt)
+        constexpr int LAUX = (POL == 2 || POL == 3) ? 0 : 2;
 #pragma unroll
         for (int k = 0; k < RB; ++k) {
             const int i = i0 + k < rows ? i0 + k : i0;
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                 Tr + (size_t)i * ldr, 0, oob, 0x00020000);
             x[k] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, i0 + k < rows ? jr * 8 : oob,
-                                                                                      0, 2));
+                                                                                      0, LAUX));
         }
 #pragma unroll
         for (int k = 0; k < RB; ++k) {
@@ -2090,7 +2094,8 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, T
             }
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc(Tr + (size_t)i * ldr, 0, oob, 0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, jr * 8, 0, SC1 ? 16 : 0);
+            constexpr int SAUX = (POL == 1 || POL == 2) ? 16 : POL == 4 ? 2 : 0;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, jr * 8, 0, SAUX);
         }
     }
 }
@@ -2415,27 +2420,34 @@ static int row_slots(int capacity, int col_blocks, int rows, int rb) {
     return (int)g;
 }
 
-template <int KT, int RB, bool SC1>
+template <int KT, int RB, int POL>
 static void launch_sweep_t(double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0, const Pending &pd,
                            const DevState *st, int rev, hipStream_t s) {
     const int cb = (Ns + 511) / 512;
-    dim3 grid(cb, row_slots(sweep_capacity(k_sweep<KT, RB, SC1>), cb, rows, RB));
-    k_sweep<KT, RB, SC1><<<grid, 256, 0, s>>>(T, rows, ld, tl, Ns, nact, s0, pd.F, pd.U,
-                                              pd.recs, pd.PM, st, pd.batch,
-                                              rev, g_sweep_rec);
+    dim3 grid(cb, row_slots(sweep_capacity(k_sweep<KT, RB, POL>), cb, rows, RB));
+    k_sweep<KT, RB, POL><<<grid, 256, 0, s>>>(T, rows, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st, pd.batch, rev,
+                                              g_sweep_rec);
 }
 
-template <int KT>
-static void launch_sweep_k(int rb, bool sc1, double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0,
-                           const Pending &pd, const DevState *st, int rev, hipStream_t s) {
+template <int KT, int POL>
+static void launch_sweep_rb(int rb, double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0,
+                            const Pending &pd, const DevState *st, int rev, hipStream_t s) {
     switch (rb) {
-    case 1: sc1 ? launch_sweep_t<KT, 1, true>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s)
-                : launch_sweep_t<KT, 1, false>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s); break;
-    case 2: sc1 ? launch_sweep_t<KT, 2, true>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s)
-                : launch_sweep_t<KT, 2, false>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s); break;
-    default: sc1 ? launch_sweep_t<KT, 4, true>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s)
-                 : launch_sweep_t<KT, 4, false>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s); break;
+    case 1: launch_sweep_t<KT, 1, POL>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s); break;
+    case 2: launch_sweep_t<KT, 2, POL>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s); break;
+    default: launch_sweep_t<KT, 4, POL>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s); break;
     }
+}
+
+// (the cache-policy variants 2..4 exist for full 32-slot sweeps only; smaller batches take 0 / 1)
+template <int KT>
+static void launch_sweep_k(int rb, int pol, double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0,
+                           const Pending &pd, const DevState *st, int rev, hipStream_t s) {
+    if (KT == SX_KMAX && pol == 2) return launch_sweep_rb<KT, 2>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+    if (KT == SX_KMAX && pol == 3) return launch_sweep_rb<KT, 3>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+    if (KT == SX_KMAX && pol == 4) return launch_sweep_rb<KT, 4>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+    if (pol == 0) return launch_sweep_rb<KT, 0>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+    launch_sweep_rb<KT, 1>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
 }
 
 void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, int m, double *T, int rows, int row0,
@@ -2448,15 +2460,15 @@ void sx_launch_sweep(double *T, int rows, size_t ld, TLay tl, int Ns, const int 
     if (rows <= 0) return;
     const int k = cfg.batch;  // pivots the sweep may have to apply (register slots)
     if (k <= 1)
-        launch_sweep_k<1>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+        launch_sweep_k<1>(cfg.rows_per_block, cfg.sc1, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else if (k <= 4)
-        launch_sweep_k<4>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+        launch_sweep_k<4>(cfg.rows_per_block, cfg.sc1, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else if (k <= 8)
-        launch_sweep_k<8>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+        launch_sweep_k<8>(cfg.rows_per_block, cfg.sc1, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else if (k <= 16)
-        launch_sweep_k<16>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+        launch_sweep_k<16>(cfg.rows_per_block, cfg.sc1, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else if (k <= SX_KMAX)
-        launch_sweep_k<SX_KMAX>(cfg.rows_per_block, cfg.sc1 != 0, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+        launch_sweep_k<SX_KMAX>(cfg.rows_per_block, cfg.sc1, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else
         SX_FATAL("batch larger than SX_KMAX");
 }

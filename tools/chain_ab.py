@@ -5,7 +5,8 @@ W untimed + K timed phase-1 pivots; per pivot: wall time, sweep time (HIP events
 usage: python tools/chain_ab.py <setting>=<v1>,<v2> [config=config5,config3] [rounds=2]
   settings: regions (simplex_set_regions: 0 plain rows, 1 two-region layout),
             rows (simplex_set_update_rows: rows per sweep step, 0 = auto),
-            waves (simplex_set_update_waves: the sweep's grid as a multiple of the resident blocks)"""
+            waves (simplex_set_update_waves: the sweep's grid as a multiple of the resident blocks),
+            policy (simplex_set_store_sc1: the sweep's cache policy 0..4, -1 = default)"""
 import os
 import sys
 
@@ -43,8 +44,9 @@ def main():
     (name, vals), = args.items()
     setter = {"regions": lambda v: lib.simplex_set_regions(int(v)),
               "rows": lambda v: lib.simplex_set_update_rows(int(v)),
-              "waves": lambda v: lib.simplex_set_update_waves(float(v))}[name]
-    reset = {"regions": 1, "rows": 0, "waves": 0}[name]
+              "waves": lambda v: lib.simplex_set_update_waves(float(v)),
+              "policy": lambda v: lib.simplex_set_store_sc1(int(v))}[name]
+    reset = {"regions": 1, "rows": 0, "waves": 0, "policy": -1}[name]
     print("stamps (us): ratio compute | ratio argmin+publish | -> selection seen | pass2 + row details |"
           " row compute | obj argmin+publish | -> entering seen | entering history | pivot")
     for r in range(rounds):
