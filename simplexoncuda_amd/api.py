@@ -380,6 +380,11 @@ def set_store_sc1(mode):
     _lib.load().simplex_set_store_sc1(int(mode))
 
 
+def set_sweep_mfma(mode):
+    """The tableau sweep on the matrix cores (1), the vector sweep (0) or auto (-1)."""
+    _lib.load().simplex_set_sweep_mfma(int(mode))
+
+
 def set_batch(p):
     """Pivots per tableau sweep (1..32; <= 0: default 32)."""
     _lib.load().simplex_set_batch(int(p))

@@ -52,6 +52,10 @@ struct __attribute__((aligned(16))) DevState {
 
 // Deferred pivots: at most SX_KMAX pivots between two sweeps of the tableau.
 #define SX_KMAX 32
+// Position of slot s in a row of F: slot 4 k + g at g * (SX_KMAX / 4) + k, so the 4 slots one
+// matrix-core step applies (k_msweep: lane group g takes slot 4 k + g) are SX_KMAX / 4 doubles
+// apart and the SX_KMAX / 4 slots one lane needs are contiguous (16-byte loads).
+__host__ __device__ constexpr int sx_fslot(int s) { return (s & 3) * (SX_KMAX / 4) + (s >> 2); }
 // Batch ids run 1 .. SX_BATCH_IDS - 1: the fused kernels' granule tags keep 15 bits of the id
 // (sx_kernels.hip make_tag).  When the ids wrap, the engine clears every id-tagged word (the
 // PM pending-leaving masks and the granule records) first, so no stale tag can match.
@@ -68,7 +72,7 @@ struct __attribute__((aligned(16))) PivRec {
 // being enqueued (kernel arguments).
 struct Pending {
     double *U;               // [SX_KMAX][ld] pivot rows (current leaving-row values, before /p)
-    double *F;               // [rows][SX_KMAX] row factors -(a_ie / p)
+    double *F;               // [rows][SX_KMAX] row factors -(a_ie / p), slot s at sx_fslot(s)
     PivRec *recs;            // [SX_KMAX]
     unsigned long long *PM;  // [rows] (batch id << 32) | slots where the row left the basis
     unsigned batch;          // id of the current batch (never 0)
@@ -151,6 +155,7 @@ struct SweepCfg {
     int sc1;             // cache policy of the tableau traffic: 0 nt loads + plain stores, 1 nt loads +
                          // write-through (sc1) stores (default), 2 default loads + sc1 stores,
                          // 3 default loads + plain stores, 4 nt loads + nt stores (32-slot sweeps)
+    int mfma;            // 1: the matrix-core sweep (k_msweep), 0: the vector sweep (k_sweep)
 };
 
 int sx_enter_blocks(int L);
@@ -166,8 +171,21 @@ void sx_launch_pivot_row(const double *T, int rows, int row0, size_t ld, TLay tl
                          size_t prow_stride, const double *colE, DevState *st, const Pending &pd,
                          TilePart *enter_parts, hipStream_t s);
 // nact (device, or null): sweep only the columns [0, s0 + *nact) (slack compaction)
-void sx_launch_sweep(double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0, const Pending &pd,
-                     const DevState *st, int rev, SweepCfg cfg, hipStream_t s);
+void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, const int *nact, int s0,
+                     const Pending &pd, const DevState *st, int rev, SweepCfg cfg, hipStream_t s);
+// What a batch's last block records for its (pipelined) sweep: the batch id, its pivots and the
+// swept slack columns after its activation.
+struct SweepMeta {
+    unsigned tag;
+    int count;
+    int nact;  // < 0: read *nact
+    int pad;
+};
+// the matrix-core sweep out of place (Tsrc -> Tdst; every swept element written); grid_cap > 0
+// caps the resident blocks (room for a concurrent batch)
+void sx_launch_msweep_oop(const double *Tsrc, double *Tdst, int rows, int row0, size_t ld, TLay tl, int Ns,
+                          const int *nact, int s0, const Pending &pd, const DevState *st, const SweepMeta *meta, int rev,
+                          int grid_cap, hipStream_t s);
 // slack compaction, after a batch's selections and before its sweep: move the slack column
 // of every row that left the basis for the first time into the swept block
 void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, int m, double *T, int rows, int row0,

@@ -55,6 +55,8 @@ struct Config {
     int verbose = 0;
     int update_rows = 0;  // 0: auto (by tableau size)
     int sc1 = -1;         // write-through tableau stores: -1 auto, 0, 1
+    int sweep_mfma = -1;  // the matrix-core sweep: -1 auto, 0 off, 1 on
+    int shadow_sweep = 0;  // diagnostic (bench sessions): 0 off, -1 / cap > 0: a concurrent shadow sweep
     int batch = 32;          // pivots per tableau sweep (deferred updates), 1..SX_KMAX
     int device = -1;
     int virtual_ranks = 1;
@@ -1031,6 +1033,7 @@ class Engine {
         c.batch = batch;
         c.rows_per_block = g_cfg.update_rows > 0 ? std::min(g_cfg.update_rows, 4) : (batch > 16 ? 4 : 2);
         c.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : 1;
+        c.mfma = g_cfg.sweep_mfma >= 0 ? g_cfg.sweep_mfma : 0;
         // peer ranks read leaving rows straight from this tableau (system-scope loads over
         // xGMI): its stores must write through to memory, not stay dirty in an L2 of this device
         if (p2p && (rccl || multidev) && c.sc1 != 1 && c.sc1 != 2) c.sc1 = 1;
@@ -1206,7 +1209,7 @@ class Engine {
         if (ev0) SX_HIP(hipEventRecord(ev0, s));
         for (auto &x : sh) {
             DevGuard g(x.dev);
-            sx_launch_sweep(x.T, x.rows, ld, tl, cols(N).Ns, compact ? x.nact : nullptr, 1 + n, pending(x), x.st, rev, cfg,
+            sx_launch_sweep(x.T, x.rows, x.row0, ld, tl, cols(N).Ns, compact ? x.nact : nullptr, 1 + n, pending(x), x.st, rev, cfg,
                             x.s);
             if (rec_shard0) sx_set_sweep_record(nullptr);  // (only shard 0's sweep records)
         }
@@ -1659,6 +1662,8 @@ extern "C" {
 int simplex_version(void) { return 1; }
 void simplex_set_verbose(int on) { g_cfg.verbose = on; }
 void simplex_set_update_rows(int rb) { g_cfg.update_rows = (rb == 1 || rb == 2 || rb == 4 || rb == 8) ? rb : 0; }
+void simplex_set_shadow_sweep(int mode) { g_cfg.shadow_sweep = mode; }
+void simplex_set_sweep_mfma(int mode) { g_cfg.sweep_mfma = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_store_sc1(int mode) { g_cfg.sc1 = mode < 0 ? -1 : (mode <= 4 ? mode : 1); }
 void simplex_set_batch(int pivots) { g_cfg.batch = pivots > 0 ? std::min(pivots, SX_KMAX) : 32; }
 void simplex_set_device(int device) {
@@ -1906,11 +1911,40 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
         }
         ++nsw;
     };
+    // diagnostic: a shadow sweep (a full 32-pivot matrix-core sweep of the tableau into a scratch
+    // buffer) on a second stream, concurrent with every batch -- what a pipelined sweep would
+    // cost the chain and get from the device while the batch runs
+    const bool shadow = g_cfg.shadow_sweep != 0 && fused && E.sh.size() == 1;
+    double *Tsh = nullptr;
+    SweepMeta *meta_dev = nullptr;
+    hipStream_t s2 = nullptr;
+    hipEvent_t sh_a = nullptr, sh_b = nullptr;
+    if (shadow) {
+        Shard &x = E.sh[0];
+        Tsh = dalloc<double>(E.t_doubles(x.rows > 0 ? (size_t)x.rows : 1));
+        meta_dev = dalloc<SweepMeta>(1);
+        SweepMeta mh{1u, SX_KMAX, -1, 0};
+        SX_HIP(hipMemcpy(meta_dev, &mh, sizeof(mh), hipMemcpyHostToDevice));
+        SX_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+        SX_HIP(hipEventCreateWithFlags(&sh_a, hipEventDisableTiming));
+        SX_HIP(hipEventCreateWithFlags(&sh_b, hipEventDisableTiming));
+    }
     SX_HIP(hipEventRecord(w0, E.s));
     for (long long i = 0; i < k;) {
         if (fused) {
             const int kb = (int)std::min<long long>(K, k - i);
+            if (shadow) {
+                Shard &x = E.sh[0];
+                SX_HIP(hipEventRecord(sh_a, E.s));
+                SX_HIP(hipStreamWaitEvent(s2, sh_a, 0));
+                Pending pd = E.pending(x);
+                pd.batch = 1u;
+                sx_launch_msweep_oop(x.T, Tsh, x.rows, x.row0, E.ld, E.tl, E.cols(E.N).Ns, E.compact ? x.nact : nullptr, 1 + E.n,
+                                     pd, x.st, meta_dev, 0, g_cfg.shadow_sweep > 0 ? g_cfg.shadow_sweep : 0, s2);
+                SX_HIP(hipEventRecord(sh_b, s2));
+            }
             E.enqueue_batch(kb);
+            if (shadow) SX_HIP(hipStreamWaitEvent(E.s, sh_b, 0));
             i += kb;
         } else {
             E.enqueue_pivot();
@@ -1962,6 +1996,13 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
     for (auto &e : evs) (void)hipEventDestroy(e);
     (void)hipEventDestroy(w0);
     (void)hipEventDestroy(w1);
+    if (shadow) {
+        (void)hipFree(Tsh);
+        (void)hipFree(meta_dev);
+        (void)hipStreamDestroy(s2);
+        (void)hipEventDestroy(sh_a);
+        (void)hipEventDestroy(sh_b);
+    }
     S->total = f.pivots;
     E.gather_d();  // (outside the timed region: the whole objective row on every shard)
     E.sync_all();
@@ -2136,8 +2177,9 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     cfg.batch = pivots;
     cfg.rows_per_block = g_cfg.update_rows > 0 ? std::min(g_cfg.update_rows, 4) : (pivots > 16 ? 4 : 2);
     cfg.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : 1;  // (as sweep_cfg: write-through at every size)
+    cfg.mfma = g_cfg.sweep_mfma >= 0 ? g_cfg.sweep_mfma : 0;
     long long sweeps = 0;
-    auto one = [&]() { sx_launch_sweep(T, rows, ld, btl, cols, nullptr, 0, pd, st, (int)(sweeps & 1), cfg, s); };
+    auto one = [&]() { sx_launch_sweep(T, rows, 0, ld, btl, cols, nullptr, 0, pd, st, (int)(sweeps & 1), cfg, s); };
     for (int w = 0; w < warmup; ++w, ++sweeps) one();
     hipEvent_t e0, e1;
     SX_HIP(hipEventCreate(&e0));

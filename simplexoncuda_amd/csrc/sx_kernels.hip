@@ -246,7 +246,7 @@ __device__ __forceinline__ unsigned stage_row(const double *__restrict__ F, cons
                                               double *sf, double *sp) {
     const int t = threadIdx.x;
     if (t < q) {
-        sf[t] = F[(size_t)rl * SX_KMAX + t];
+        sf[t] = F[(size_t)rl * SX_KMAX + sx_fslot(t)];
         sp[t] = recs[t].p;
     }
     __syncthreads();
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
         for (int s0 = 0; s0 < q; s0 += 8) {
             double f[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) f[k] = Fr[s0 + k];  // s0 + k < SX_KMAX
+            for (int k = 0; k < 8; ++k) f[k] = Fr[sx_fslot(s0 + k)];  // s0 + k < SX_KMAX
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const int s = s0 + k;
@@ -564,7 +564,7 @@ __global__ __launch_bounds__(256) void k_pivot_row(const double *__restrict__ T,
     const double p = x[0], u0 = x[1], ua = x[2], ub = x[3];
     if ((int)blockIdx.x >= B1) {
         const int i = ((int)blockIdx.x - B1) * 256 + (int)threadIdx.x;
-        if (i < rows) F[(size_t)i * SX_KMAX + q] = -colE[i] / p;
+        if (i < rows) F[(size_t)i * SX_KMAX + sx_fslot(q)] = -colE[i] / p;
         if (i == rl) {
             const unsigned long long w = PM[rl];
             PM[rl] = (((unsigned)(w >> 32) == B) ? w : ((unsigned long long)B << 32)) | (1ull << q);
@@ -1297,7 +1297,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 const double f = -a / p;
                 s_hist[q * SX_TILE + t] = f;
                 if (liveA) {
-                    F[(size_t)li * SX_KMAX + q] = f;
+                    F[(size_t)li * SX_KMAX + sx_fslot(q)] = f;
                     if (li == r) {
                         b = b / p;
                         bits |= 1u << q;
@@ -1705,7 +1705,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 const double f = -a / p;
                 s_hist[q * SX_TILE + t] = f;
                 if (liveA) {
-                    F[(size_t)li * SX_KMAX + q] = f;
+                    F[(size_t)li * SX_KMAX + sx_fslot(q)] = f;
                     if (row0 + li == r) {
                         b = b / p;
                         bits |= 1u << q;
@@ -1983,6 +1983,8 @@ __global__ __launch_bounds__(512) void k_batch_mr_multi(MrRanks R, int nloc, int
 // Infinity Cache).  The sweep runs whatever the phase status: a batch cut short by the end
 // of the phase is still materialised.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef double d4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // (batch tag, batch count, swept slack columns) of this sweep into rec[0..2] (bench sessions'
 // timed sweeps; null otherwise) -- written by the sweep itself instead of two device copies
@@ -2060,7 +2062,7 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, T
             const double *Fr = F + (size_t)i * SX_KMAX;
             double f[KT];
 #pragma unroll
-            for (int s = 0; s < KT; ++s) f[s] = Fr[s];
+            for (int s = 0; s < KT; ++s) f[s] = Fr[sx_fslot(s)];
             const unsigned bits = pend_bits(PM, i, B, mask);
             double2 y = x[k];
             if (bits == 0u && cnt == KT) {  // a full batch, no leaving row: no per-slot branch
@@ -2097,6 +2099,187 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, T
             constexpr int SAUX = (POL == 1 || POL == 2) ? 16 : POL == 4 ? 2 : 0;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, jr * 8, 0, SAUX);
         }
+    }
+}
+
+// K5': the same sweep on the matrix cores.  v_mfma_f64_16x16x4f64 computes a 16x16 tile's
+// D = A B + C as the slot-ordered chain of fused multiply-adds, bit for bit
+// (tools/mfma_f64_probe.hip: every element equals fma(a3, b3, fma(a2, b2, fma(a1, b1,
+// fma(a0, b0, c)))) on MI355X), so SX_KMAX / 4 MFMAs per tile are the batch's updates in the
+// reference's order (solver.cu:34-46).  Operands of step k (slots 4k .. 4k+3):
+//   A (16 rows x 4 slots)     lane l = F[r0 + l % 16][4k + l / 16]   (sx_fslot: 8 contiguous per lane)
+//   B (4 slots x 16 columns)  lane l = U[4k + l / 16][col(l % 16)]
+//   C / D                     lane l, register v = T[r0 + l / 16 + 4v][col(l % 16)]
+// Two tiles share each lane's 16-byte access (tile X the even column 2c, tile Y the odd 2c + 1),
+// so every tableau access is one 16-byte load or store per lane.  A wave owns 64 columns (two
+// pairs of tiles) and walks 16-row strips; its U fragments stay in registers for the whole
+// sweep, the strip's F fragments are loaded per strip; a strip's tableau accesses go through
+// one wave-uniform buffer resource.  A partial batch pads slots >= cnt with f = -0.0, u = +0.0
+// (fma(-0, +0, x) == x for every x) and skips the 4-slot steps past cnt.
+// The rows that left the basis in this batch (x / p at their slot instead of the fma; at most
+// SX_KMAX of the shard's rows) are not stored by the strips: each is recomputed after the strip
+// loop, by the waves of the row slot s % G, from its stored values with the vector chain (one
+// column per lane).  The strips never write those rows, so the values read are the originals.
+// Grid, column order, regions, compaction and cache policy as k_sweep (POL 1), with 256-column
+// tiles.  Out of place (Tdst != Tsrc, the pipelined sweep): every swept element is written, also
+// when the batch selected no pivot (a copy).  meta (or null: the count from st): the batch's
+// count and swept slacks as its last block recorded them.
+__global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *Tdst, int rows, int row0, size_t ld,
+                                                   TLay tl, int Ns, const int *__restrict__ nact, int s0,
+                                                   const double *__restrict__ F, const double *__restrict__ U,
+                                                   const PivRec *__restrict__ recs,
+                                                   const unsigned long long *__restrict__ PM,
+                                                   const DevState *__restrict__ st,
+                                                   const SweepMeta *__restrict__ meta, unsigned B, int rev,
+                                                   int *__restrict__ rec) {
+    constexpr int NKB = SX_KMAX / 4;
+    sweep_record(rec, st, nact);
+    const int cnt = meta ? (meta->tag == B ? meta->count : 0) : (st->batch_tag == B ? st->batch_count : 0);
+    if (cnt <= 0 && Tdst == Tsrc) return;
+    if (nact) {
+        const int na = meta && meta->nact >= 0 ? meta->nact : *nact;
+        if (s0 + na < Ns) Ns = s0 + na;
+    }
+    const int cb = (Ns + 255) / 256;
+    const int lin = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    const int G = (int)(gridDim.x * gridDim.y) / cb;
+    const int tile = lin % cb, gy = lin / cb;
+    if (gy >= G) return;
+    const int bx = rev ? cb - 1 - tile : tile;
+    const int l = (int)threadIdx.x & 63, jl = l & 15, rg = l >> 4;
+    const int c0 = (bx * 4 + ((int)threadIdx.x >> 6)) * 64;  // the wave's first column
+    if (c0 >= Ns) return;
+    // this tile's storage region (jB is a multiple of 512: a 256-column tile lies in one region)
+    const bool inB = bx * 256 >= tl.jB;
+    const double *const Tr = inB ? Tsrc + tl.offB : Tsrc;
+    double *const Tw = inB ? Tdst + tl.offB : Tdst;
+    const size_t ldr = inB ? tl.ldB : tl.ldA;
+    const int cr = inB ? c0 - tl.jB : c0;
+    const unsigned mask = cnt > 0 ? slot_mask(cnt) : 0u;
+    const int nkb = (cnt + 3) >> 2;
+    const int OOB = 0x7fffffff;
+    {
+        // the lane's columns: c0 + 32p + 2jl and the next, p = 0, 1 (an odd last column's neighbour
+        // is an untouched column: not written)
+        double2 uf[NKB][2];
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const int sl = 4 * kb + rg, j = c0 + 32 * p + 2 * jl;
+                uf[kb][p] = (sl < cnt && j < Ns) ? *reinterpret_cast<const double2 *>(U + (size_t)sl * ld + j)
+                                                 : make_double2(0.0, 0.0);
+            }
+        const int nstrip = (rows + 15) >> 4;
+        for (int g = gy; g < nstrip; g += G) {
+            const int r0 = (rev ? nstrip - 1 - g : g) * 16;
+            const int fr = r0 + jl;  // the A-operand row of this lane
+            double ff[NKB];
+            {
+                const double *Fr = F + (size_t)(fr < rows ? fr : r0) * SX_KMAX + rg * NKB;
+#pragma unroll
+                for (int kb = 0; kb < NKB; kb += 2) {
+                    const double2 v = *reinterpret_cast<const double2 *>(Fr + kb);
+                    ff[kb] = v.x;
+                    ff[kb + 1] = v.y;
+                }
+#pragma unroll
+                for (int kb = 0; kb < NKB; ++kb)
+                    if (4 * kb + rg >= cnt) ff[kb] = -0.0;
+            }
+            // row fr's slots as a leaving row (read with the tableau; which strips hold a leaving
+            // row is decided after the first pair's matrix steps, so this load overlaps them)
+            const unsigned lb = fr < rows ? pend_bits(PM, fr, B, mask) : 0u;
+            bool fix = false;
+            unsigned skip = 0u;  // bit v: row r0 + rg + 4v is a leaving row (not stored here)
+            // one buffer resource per strip (wave-uniform), holding the strip's valid rows; rows
+            // past the end read 0 and drop their stores
+            const int nr = rows - r0 < 16 ? rows - r0 : 16;
+            const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<double *>(Tr) + (size_t)r0 * ldr, 0, (int)((size_t)nr * ldr * 8), 0x00020000);
+            const __amdgpu_buffer_rsrc_t rss =
+                __builtin_amdgcn_make_buffer_rsrc(Tw + (size_t)r0 * ldr, 0, (int)((size_t)nr * ldr * 8), 0x00020000);
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const int j = c0 + 32 * p + 2 * jl, jr = cr + 32 * p + 2 * jl;
+                double2 cx[4];
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int off = (int)(((size_t)(rg + 4 * v) * ldr + jr) * 8);
+                    cx[v] = __builtin_bit_cast(double2,
+                                               __builtin_amdgcn_raw_buffer_load_b128(rsl, j < Ns ? off : OOB, 0, 2));
+                }
+                d4_t ax = {cx[0].x, cx[1].x, cx[2].x, cx[3].x};
+                d4_t ay = {cx[0].y, cx[1].y, cx[2].y, cx[3].y};
+                if (nkb == NKB) {
+#pragma unroll
+                    for (int kb = 0; kb < NKB; ++kb) {
+                        ax = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].x, ax, 0, 0, 0);
+                        ay = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].y, ay, 0, 0, 0);
+                    }
+                } else {
+#pragma unroll
+                    for (int kb = 0; kb < NKB; ++kb)
+                        if (kb < nkb) {
+                            ax = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].x, ax, 0, 0, 0);
+                            ay = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].y, ay, 0, 0, 0);
+                        }
+                }
+                if (p == 0) {
+                    fix = __ballot(lb != 0u) != 0ull;
+                    if (fix)
+#pragma unroll
+                        for (int v = 0; v < 4; ++v)
+                            if (__shfl(lb, rg + 4 * v) != 0u) skip |= 1u << v;  // (lane rg + 4v: that row's bits)
+                }
+                const bool pair = j + 1 < Ns;
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int off = (int)(((size_t)(rg + 4 * v) * ldr + jr) * 8);
+                    const bool keep = j < Ns && !((skip >> v) & 1u);
+                    if (pair) {
+                        const double2 y = make_double2(ax[v], ay[v]);
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rss, keep ? off : OOB, 0,
+                                                               16);
+                    } else {
+                        // (built from the 64-bit integer: a bit_cast of ax[v] straight to u32x2 compiled
+                        // to a store of ax[0] for every v -- ROCm 7.2 clang, checked in the ISA)
+                        const unsigned long long xb = (unsigned long long)__double_as_longlong(ax[v]);
+                        const u32x2 w = {(unsigned)xb, (unsigned)(xb >> 32)};
+                        __builtin_amdgcn_raw_buffer_store_b64(w, rss, keep ? off : OOB, 0, 16);
+                    }
+                }
+            }
+        }
+    }
+    // the leaving rows: row r_s (first slot s where it left) by the row slot s % G, one column
+    // per lane, the guarded chain from its stored values (the strips left them unwritten)
+    if (cnt <= 0) return;
+    const int j = c0 + l;
+    double u[SX_KMAX];
+#pragma unroll
+    for (int sl = 0; sl < SX_KMAX; ++sl) u[sl] = (sl < cnt && j < Ns) ? U[(size_t)sl * ld + j] : 0.0;
+    for (int s = gy; s < cnt; s += G) {
+        const int r = recs[s].r - row0;
+        if (r < 0 || r >= rows) continue;
+        const unsigned bits = pend_bits(PM, r, B, mask);
+        if (bits == 0u || (int)__builtin_ctz(bits) != s) continue;  // (not its first slot)
+        const double *Fr = F + (size_t)r * SX_KMAX;
+        double x = j < Ns ? Tr[(size_t)r * ldr + cr + l] : 0.0;
+#pragma unroll
+        for (int sl = 0; sl < SX_KMAX; ++sl) {
+            if (sl < cnt) {
+                if ((bits >> sl) & 1u)
+                    x = x / recs[sl].p;
+                else
+                    x = fma(Fr[sx_fslot(sl)], u[sl], x);
+            }
+        }
+        const __amdgpu_buffer_rsrc_t rsr =
+            __builtin_amdgcn_make_buffer_rsrc(Tw + (size_t)r * ldr, 0, (int)(ldr * 8), 0x00020000);
+        const unsigned long long xb = (unsigned long long)__double_as_longlong(x);
+        const u32x2 w = {(unsigned)xb, (unsigned)(xb >> 32)};
+        __builtin_amdgcn_raw_buffer_store_b64(w, rsr, j < Ns ? (cr + l) * 8 : OOB, 0, 16);  // (write-through, as the strips)
     }
 }
 
@@ -2455,9 +2638,18 @@ void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, in
     k_activate<<<1, 256, 0, s>>>(perm, iperm, act, nact, m, T, rows, row0, ld, tl, s0, pd.U, pd.recs, st, pd.batch);
 }
 
-void sx_launch_sweep(double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0, const Pending &pd,
-                     const DevState *st, int rev, SweepCfg cfg, hipStream_t s) {
+void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, const int *nact, int s0,
+                     const Pending &pd, const DevState *st, int rev, SweepCfg cfg, hipStream_t s) {
     if (rows <= 0) return;
+    if (cfg.mfma) {
+        if (ld % 2 != 0 || tl.ldA % 2 != 0 || (tl.jB < Ns && (tl.jB % 256 != 0 || tl.ldB % 2 != 0 || tl.offB % 2 != 0)))
+            SX_FATAL("matrix-core sweep: 16-byte rows and 256-aligned regions required");
+        const int cb = (Ns + 255) / 256;
+        dim3 grid(cb, row_slots(sweep_capacity(k_msweep), cb, rows, 16));
+        k_msweep<<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st, nullptr,
+                                      pd.batch, rev, g_sweep_rec);
+        return;
+    }
     const int k = cfg.batch;  // pivots the sweep may have to apply (register slots)
     if (k <= 1)
         launch_sweep_k<1>(cfg.rows_per_block, cfg.sc1, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
@@ -2471,6 +2663,19 @@ void sx_launch_sweep(double *T, int rows, size_t ld, TLay tl, int Ns, const int 
         launch_sweep_k<SX_KMAX>(cfg.rows_per_block, cfg.sc1, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else
         SX_FATAL("batch larger than SX_KMAX");
+}
+
+void sx_launch_msweep_oop(const double *Tsrc, double *Tdst, int rows, int row0, size_t ld, TLay tl, int Ns,
+                          const int *nact, int s0, const Pending &pd, const DevState *st, const SweepMeta *meta, int rev,
+                          int grid_cap, hipStream_t s) {
+    if (rows <= 0) return;
+    if (ld % 2 != 0 || tl.ldA % 2 != 0 || (tl.jB < Ns && (tl.jB % 256 != 0 || tl.ldB % 2 != 0 || tl.offB % 2 != 0)))
+        SX_FATAL("matrix-core sweep: 16-byte rows and 256-aligned regions required");
+    const int cb = (Ns + 255) / 256;
+    const int cap = grid_cap > 0 ? std::min(grid_cap, sweep_capacity(k_msweep)) : sweep_capacity(k_msweep);
+    dim3 grid(cb, row_slots(cap, cb, rows, 16));
+    k_msweep<<<grid, 256, 0, s>>>(Tsrc, Tdst, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st, meta,
+                                  pd.batch, rev, nullptr);
 }
 
 static size_t batch_lds(int k) { return (size_t)k * SX_TILE * sizeof(double); }

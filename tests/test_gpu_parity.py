@@ -205,7 +205,8 @@ def _pivots_with(cfg, T, d, base, k):
     Tg, dg, bg = T.copy(), d.copy(), base.copy()
     setters = {"batch": (sx.set_batch, 0), "rb": (sx.set_update_rows, 0), "sc1": (sx.set_store_sc1, -1),
                "fused": (sx.set_fused, -1), "p2p": (sx.set_p2p, -1),
-               "waves": (sx.set_update_waves, 0), "W": (sx.set_virtual_ranks, 1)}
+               "waves": (sx.set_update_waves, 0), "W": (sx.set_virtual_ranks, 1),
+               "mfma": (sx.set_sweep_mfma, -1)}
     try:
         for key, val in cfg.items():
             setters[key][0](val)
@@ -241,6 +242,31 @@ def test_large_batch_sweeps_bit_exact(gpu, batch, rb, sc1):
     Tg, dg, bg, st, done = _pivots_with({"batch": batch, "rb": rb, "sc1": sc1}, T, d, base, 70)
     oracle.solve(T, d, base, max_pivots=70)
     assert done == 70
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+@pytest.mark.parametrize("mfma", [1, 0])
+@pytest.mark.parametrize("fused", [-1, 0])
+@pytest.mark.parametrize("batch", [1, 3, 5, 16, 31, 32])
+def test_matrix_core_sweep_bit_exact(gpu, batch, fused, mfma):
+    """the sweep on the matrix cores (k_msweep: 4 slots per v_mfma_f64_16x16x4f64, partial
+    batches padded, leaving rows recomputed on the vector units) against the vector sweep and the
+    oracle: the same bits, 333 rows (a partial 16-row strip), partial last batches"""
+    T, d, base = _phase1_state(333, 1025, 7)
+    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "fused": fused, "mfma": mfma}, T, d, base, 75)
+    oracle.solve(T, d, base, max_pivots=75)
+    assert done == 75
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+@pytest.mark.parametrize("W", [2, 4])
+def test_matrix_core_sweep_virtual_ranks(gpu, W):
+    """the matrix-core sweep on each virtual shard's rows (peer-memory batches, objective tiles
+    split across ranks): bit-exact"""
+    T, d, base = _phase1_state(300, 1100, 11)
+    Tg, dg, bg, st, done = _pivots_with({"batch": 32, "W": W, "p2p": 1, "mfma": 1}, T, d, base, 150)
+    st_o, done_o = oracle.solve(T, d, base, max_pivots=150)
+    assert done == done_o
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 
@@ -531,16 +557,19 @@ def test_two_region_layout_bit_exact(gpu, n, m, k, fused, W, p2p, cap):
 @pytest.mark.parametrize("W,p2p", [(1, -1), (2, 1), (3, 0)])
 @pytest.mark.parametrize("n,m,seed,lo,hi", [(300, 1100, 41100, 1, 100), (64, 128, 6528, 1, 100),
                                             (129, 1513, 77, -100, 100)])
-def test_two_region_two_phase(gpu, n, m, seed, lo, hi, W, p2p):
+@pytest.mark.parametrize("mfma", [0, 1])
+def test_two_region_two_phase(gpu, n, m, seed, lo, hi, W, p2p, mfma):
     """whole two-phase solves (GEMV, phase switch, solution) on the two-region layout with a
-    region A of 16 slack positions, on 1-3 shards"""
+    region A of 16 slack positions, on 1-3 shards, swept on the vector units or the matrix cores"""
     p = sx.generateRandomProblem(n, m, seed, lo, hi)
     try:
         sx.set_regions(16)
         sx.set_virtual_ranks(W)
         sx.set_p2p(p2p)
+        sx.set_sweep_mfma(mfma)
         _check_two_phase(p)
     finally:
+        sx.set_sweep_mfma(-1)
         sx.set_p2p(-1)
         sx.set_virtual_ranks(1)
         sx.set_regions(1)

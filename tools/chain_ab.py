@@ -6,7 +6,9 @@ usage: python tools/chain_ab.py <setting>=<v1>,<v2> [config=config5,config3] [ro
   settings: regions (simplex_set_regions: 0 plain rows, 1 two-region layout),
             rows (simplex_set_update_rows: rows per sweep step, 0 = auto),
             waves (simplex_set_update_waves: the sweep's grid as a multiple of the resident blocks),
-            policy (simplex_set_store_sc1: the sweep's cache policy 0..4, -1 = default)"""
+            policy (simplex_set_store_sc1: the sweep's cache policy 0..4, -1 = default),
+            mfma (simplex_set_sweep_mfma: 0 vector sweep, 1 matrix-core sweep, -1 auto),
+            shadow (simplex_set_shadow_sweep: 0 off, -1 / cap: a concurrent shadow sweep per batch)"""
 import os
 import sys
 
@@ -45,8 +47,10 @@ def main():
     setter = {"regions": lambda v: lib.simplex_set_regions(int(v)),
               "rows": lambda v: lib.simplex_set_update_rows(int(v)),
               "waves": lambda v: lib.simplex_set_update_waves(float(v)),
-              "policy": lambda v: lib.simplex_set_store_sc1(int(v))}[name]
-    reset = {"regions": 1, "rows": 0, "waves": 0, "policy": -1}[name]
+              "policy": lambda v: lib.simplex_set_store_sc1(int(v)),
+              "mfma": lambda v: lib.simplex_set_sweep_mfma(int(v)),
+              "shadow": lambda v: lib.simplex_set_shadow_sweep(int(v))}[name]
+    reset = {"regions": 1, "rows": 0, "waves": 0, "policy": -1, "mfma": -1, "shadow": 0}[name]
     print("stamps (us): ratio compute | ratio argmin+publish | -> selection seen | pass2 + row details |"
           " row compute | obj argmin+publish | -> entering seen | entering history | pivot")
     for r in range(rounds):

@@ -135,6 +135,53 @@ __global__ __launch_bounds__(256, 2) void k_msweep2(double *T, int rows, int col
     }
 }
 
+// the same with one wave-uniform buffer resource per strip (the per-lane row bases above compile
+// to waterfall loops), as the engine's k_msweep
+template <int K>
+__global__ __launch_bounds__(256, 2) void k_msweep3(double *T, int rows, int cols, size_t ld,
+                                                    const double *__restrict__ Ft, const double *__restrict__ U, int G) {
+    const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c0 = (blockIdx.x * 4 + w) * 64;
+    if (c0 >= cols) return;
+    const int jl = l & 15, rg = l >> 4;
+    double2 uf[K / 4][2];
+#pragma unroll
+    for (int kb = 0; kb < K / 4; ++kb)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+            uf[kb][p] = *reinterpret_cast<const double2 *>(U + (size_t)(4 * kb + rg) * ld + c0 + 32 * p + 2 * jl);
+    const int nstrip = rows / 16;
+    for (int g = blockIdx.y; g < nstrip; g += G) {
+        const int r0 = g * 16;
+        double ff[K / 4];
+#pragma unroll
+        for (int kb = 0; kb < K / 4; ++kb) ff[kb] = Ft[(size_t)(4 * kb + rg) * rows + r0 + jl];
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(T + (size_t)r0 * ld, 0, (int)(16 * ld * 8), 0x00020000);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            double2 cx[4];
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+                cx[v] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(
+                                                        rs, (int)(((rg + 4 * v) * ld + c0 + 32 * p + 2 * jl) * 8), 0, 2));
+            d4 ax = {cx[0].x, cx[1].x, cx[2].x, cx[3].x};
+            d4 ay = {cx[0].y, cx[1].y, cx[2].y, cx[3].y};
+#pragma unroll
+            for (int kb = 0; kb < K / 4; ++kb) {
+                ax = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].x, ax, 0, 0, 0);
+                ay = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].y, ay, 0, 0, 0);
+            }
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const double2 y = make_double2(ax[v], ay[v]);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs,
+                                                       (int)(((rg + 4 * v) * ld + c0 + 32 * p + 2 * jl) * 8), 0, 16);
+            }
+        }
+    }
+}
+
 // reference: the VALU chain, one element per thread
 template <int K>
 __global__ void k_ref(double *T, int rows, int cols, size_t ld, const double *Ft, const double *U) {
@@ -165,9 +212,9 @@ __global__ void k_init(double *p, size_t n, unsigned seed, double lo, double hi)
 }
 
 template <int K, int VAR>
-void run(int rows, int cols) {
-    auto kern = VAR ? k_msweep2<K> : k_msweep<K>;
-    const size_t ld = cols;
+void run(int rows, int cols, size_t ld_pad = 0) {
+    auto kern = VAR == 2 ? k_msweep3<K> : VAR ? k_msweep2<K> : k_msweep<K>;
+    const size_t ld = ld_pad ? ld_pad : cols;
     double *T, *T2, *Ft, *U;
     CK(hipMalloc(&T, (size_t)rows * ld * 8));
     CK(hipMalloc(&T2, (size_t)rows * ld * 8));
@@ -225,14 +272,14 @@ void run(int rows, int cols) {
 
 int main() {
     for (int rep = 0; rep < 2; ++rep) {
-        run<32, 0>(4096, 8192);
-        run<32, 1>(4096, 8192);
-        run<64, 0>(4096, 8192);
-        run<64, 1>(4096, 8192);
-        run<32, 0>(32768, 9216);
-        run<32, 1>(32768, 9216);
-        run<64, 0>(32768, 9216);
-        run<64, 1>(32768, 9216);
+        run<32, 2>(4096, 8192);
+        run<64, 2>(4096, 8192);
+        run<32, 2>(4096, 11008, 12304);
+        run<64, 2>(4096, 11008, 12304);
+        run<32, 2>(32768, 9216);
+        run<64, 2>(32768, 9216);
+        run<32, 2>(32768, 9216, 12288);
+        run<64, 2>(32768, 9216, 12288);
     }
     return 0;
 }
