@@ -4,12 +4,13 @@ Workload (BASELINE.json configs[4], the m=32768 problem north_star's scaling tar
 quoted on): generateRandomProblem(n=8192, m=32768, seed=851968, [1,100]) -- seed n*100+m as
 the reference's -t sweep (main.cu:56-64) -- phase-1 tableau 32768 x 73729 fp64, synthesised
 in HBM (10.7 GB stored: artificial columns aliased to their slack columns).
-A "step" is one pass of the hot path over the tableau: one batch of 32 simplex pivots
-(entering argmin, ratio test, pivot row and objective row of each) followed by
-one sweep that applies their rank-1 updates to every stored tableau element.  W untimed
-steps, then K timed steps: by default pivots 64..2080 of phase 1 (the scaling
-curve is the first 2000 phase-1 pivots).  Every timed step is a full batch, so the timed
-window runs exactly the kernels the warmup ran.
+A "step" is one pass of the hot path over the tableau: one batch of simplex pivots (64 on one
+GPU: two stages of 32; 32 per batch on several) -- entering argmin, ratio test,
+pivot row and objective row of each -- followed by one sweep that applies their rank-1 updates
+to every stored tableau element.  W untimed steps, then K timed steps: by default about the
+first 2000 phase-1 pivots after the warmup (the scaling curve is the first 2000
+phase-1 pivots).  Every timed step is a full batch, so the timed window runs exactly the kernels
+the warmup ran.
 
 N GPUs: the constraint rows are split into N contiguous 512-aligned blocks, each GPU sweeps only
 its rows; per pivot the shards exchange the tile winners and the pivot row (peer memory over
@@ -109,12 +110,13 @@ def cpu_baseline(n, m, seed, pivots, sx):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=63,
-                    help="timed steps; a step = one batch of --batch pivots + one tableau sweep")
+    ap.add_argument("--steps", type=int, default=0,
+                    help="timed steps; a step = one batch of pivots + one tableau sweep (0 = about 2016 pivots)")
     ap.add_argument("--warmup", type=int, default=2, help="untimed steps before timing")
     ap.add_argument("--config", default="config5", choices=sorted(CONFIGS))
     ap.add_argument("--update-rows", type=int, default=0, help="rows per sweep step (0 = auto)")
-    ap.add_argument("--batch", type=int, default=0, help="pivots per tableau sweep (0 = library default, 32)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="pivots per tableau sweep (0 = library default: 64 on one GPU, 32 on several)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--update-events", type=int, default=1,
                     help="bracket every k-th sweep launch with HIP events (0 = none)")
@@ -122,7 +124,8 @@ def main():
                     help="directory of pmc_sweep_<config>.json: per-launch HBM bytes of the sweep (rocprofv3 --pmc)")
     ap.add_argument("--secondary", default="config3",
                     help="second workload timed in the same run ('' to skip): the roofline-target tableau")
-    ap.add_argument("--secondary-steps", type=int, default=278, help="config 3: 278 steps = pivots 64..8960 of 8981")
+    ap.add_argument("--secondary-steps", type=int, default=0,
+                    help="config 3 (0 = up to pivot 8960 of its 8981 phase-1 pivots)")
     ap.add_argument("--secondary-warmup", type=int, default=2)
     ap.add_argument("--full-solves", default="config3,config4,config5",
                     help="instances solved end to end by twoPhaseMethod at N=1 ('' to skip)")
@@ -166,16 +169,18 @@ def main():
         if world > 1:
             dist.barrier()
 
-    K = args.batch if args.batch > 0 else 32  # pivots per step (the library clamps to 1..32)
-
-    def measure(config, steps, warmup, events):
-        """W untimed + K timed steps (batches of K pivots + one sweep) of `config`'s phase 1."""
+    def measure(config, steps, warmup, events, last_pivot=2016 + 64):
+        """W untimed + `steps` timed steps (batches of K pivots + one sweep) of `config`'s phase 1;
+        steps = 0: up to pivot `last_pivot`."""
         n, m, seed = CONFIGS[config]
         t_setup = time.perf_counter()
         # generateRandomProblem(n, m, seed, 1, 100) synthesised directly in HBM, each rank its rows
         sess = sx.Session(generated=(n, m, seed, 1, 100))
         torch.cuda.synchronize()
         t_setup = time.perf_counter() - t_setup
+        K = sess.batch()  # pivots per step: the library's batch on this engine
+        if steps <= 0:
+            steps = max(1, (last_pivot - warmup * K) // K)
         if warmup > 0:
             sess.pivots(warmup * K)
         barrier()
@@ -206,7 +211,7 @@ def main():
         achieved = tim.swept_bytes / (tim.update_ms / 1e3) / 1e9 if tim.update_launches else None
         return {"n": n, "m": m, "seed": seed, "tim": tim, "elapsed": elapsed, "pivots": tim.pivots,
                 "avg_update_s": avg_update_s, "achieved": achieved, "setup_s": t_setup,
-                "steps": steps, "warmup": warmup, "per_rank": per_rank}
+                "steps": steps, "warmup": warmup, "per_rank": per_rank, "K": K}
 
     def roofline(cfg, r):
         tim, achieved = r["tim"], r["achieved"]
@@ -227,7 +232,9 @@ def main():
             "frac": achieved / HBM_PEAK_GBS if achieved else None,
             "traffic": traffic,
             "traffic_source": source,
-            "kernel": "k_sweep (rank-1 pivot updates of a batch applied to the tableau, rank 0)",
+            "kernel": ("k_msweep<16> (the batch's 64 rank-1 pivot updates applied to the tableau on the matrix "
+                       "cores, rank 0)" if r["K"] > 32 else
+                       "k_sweep (the batch's rank-1 pivot updates applied to the tableau, rank 0)"),
             "bytes_definition": "16 * rows * (1 + n + touched slack columns) per sweep: every stored tableau "
                                 "element the sweep moves, read and written once (SURVEY.md §8d 16(m+1)N over the "
                                 "swept columns; artificial columns alias their slacks and untouched slack columns "
@@ -255,14 +262,15 @@ def main():
 
     r = measure(args.config, args.steps, args.warmup, args.update_events)
     n, m, seed, tim, elapsed, pivots = r["n"], r["m"], r["seed"], r["tim"], r["elapsed"], r["pivots"]
+    K, steps = r["K"], r["steps"]
     out = {
         "metric": "simplex pivots/sec + HBM GB/s on gaussian update, dense m×n tableau",
         "value": pivots / elapsed,
         "unit": "pivots/s",
         "n_gpus": n_gpus,
-        "steps": args.steps,
+        "steps": steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed * 1e3 / max(args.steps, 1),
+        "ms_per_step": elapsed * 1e3 / max(steps, 1),
         "ms_per_pivot": elapsed * 1e3 / max(pivots, 1),
         "higher_is_better": True,
         "scaling": "strong",
@@ -288,34 +296,41 @@ def main():
         "cpu_baseline": None,
     }
     if args.secondary and args.secondary != args.config:
-        r2 = measure(args.secondary, args.secondary_steps, args.secondary_warmup, args.update_events)
+        r2 = measure(args.secondary, args.secondary_steps, args.secondary_warmup, args.update_events, last_pivot=8960)
         out["secondary"] = {
             "workload": workload(args.secondary, r2),
             "value": r2["pivots"] / r2["elapsed"], "unit": "pivots/s",
             "vs_baseline": (r2["pivots"] / r2["elapsed"]) / REF_PIVOTS_PER_S[args.secondary]
             if args.secondary in REF_PIVOTS_PER_S else None,
-            "ms_per_step": r2["elapsed"] * 1e3 / max(args.secondary_steps, 1),
-            "steps": args.secondary_steps, "warmup": args.secondary_warmup, "pivots_timed": r2["pivots"],
-            "first_timed_pivot": args.secondary_warmup * K,
+            "ms_per_step": r2["elapsed"] * 1e3 / max(r2["steps"], 1), "pivots_per_step": r2["K"],
+            "steps": r2["steps"], "warmup": args.secondary_warmup, "pivots_timed": r2["pivots"],
+            "first_timed_pivot": args.secondary_warmup * r2["K"],
             "status_after": r2["tim"].status, "rows_per_gpu_rank0": r2["tim"].local_rows, "setup_s": r2["setup_s"],
             "roofline": roofline(args.secondary, r2),
         }
     if n_gpus == 1 and not args.no_update_bench:
         # SURVEY.md §8d config 3': the sweep kernel alone on a synthetic 4096 x 8192 fp64 matrix
-        # (uniform [1,100], seed 823296) with 32 random pending pivots
+        # (uniform [1,100], seed 823296) with K random pending pivots, K = the pivot loop's batch
         # (three runs of 10 untimed + 50 timed sweeps each; the median run is reported -- the
-        # first run on a box is often 5-10 % slower, tools/sweep_bench_ab.py)
-        runs = [sx.bench_sweep(4096, 8192, 823296, 1, 100, 32, warmup=10, iters=50) for _ in range(3)]
-        us, nbytes = sorted(runs)[1]
-        gbs = nbytes / (us * 1e-6) / 1e9
-        out["update_bench"] = {
-            "workload": "config3': k_sweep on a synthetic 4096x8192 fp64 matrix (uniform [1,100], seed 823296), "
-                        "32 random pending pivots per sweep, median of 3 runs of 50 timed sweeps (HIP events)",
-            "runs_us": [r[0] for r in runs],
-            "avg_launch_us": us, "bytes_per_launch": nbytes, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": gbs / HBM_PEAK_GBS, "per_pivot_equivalent_us": us / 32,
-            "note": "the matrix (268 MB) is about the size of the 256 MB Infinity Cache, so sweeps partly hit it",
-        }
+        # first run on a box is often 5-10 % slower); the one-stage variants alongside
+        def sweep_bench(pivots, mfma):
+            sx.set_sweep_mfma(mfma)
+            runs = [sx.bench_sweep(4096, 8192, 823296, 1, 100, pivots, warmup=10, iters=50) for _ in range(3)]
+            sx.set_sweep_mfma(-1)
+            us, nbytes = sorted(runs)[1]
+            gbs = nbytes / (us * 1e-6) / 1e9
+            return {"pivots_per_sweep": pivots,
+                    "kernel": ("k_msweep<%d> (matrix cores)" % (pivots // 4 if pivots > 32 else 8)) if mfma or pivots > 32
+                    else "k_sweep<32,4,1> (vector units)",
+                    "runs_us": [x[0] for x in runs], "avg_launch_us": us, "bytes_per_launch": nbytes, "achieved": gbs,
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "us_per_pivot": us / pivots}
+        prod = sweep_bench(K, -1)
+        out["update_bench"] = dict(prod, workload=(
+            "config3': the pivot loop's sweep kernel on a synthetic 4096x8192 fp64 matrix (uniform [1,100], seed "
+            "823296), %d random pending pivots per sweep (the loop's batch), median of 3 runs of 50 timed sweeps "
+            "(HIP events)" % K),
+            note="the matrix (268 MB) is about the size of the 256 MB Infinity Cache, so sweeps partly hit it")
+        out["update_bench"]["one_stage_variants"] = [sweep_bench(32, 0), sweep_bench(32, 1)]
     if args.full_solves:
         # the whole drop-in call, as main.cu -t times it: build + both phases + solution (problem
         # synthesised on the GPU and copied to the host first, outside the clock)

@@ -30,7 +30,9 @@ void simplex_set_store_sc1(int mode);
 /* the sweep on the matrix cores (v_mfma_f64_16x16x4f64, bit-identical to the vector chain):
  * -1 auto, 0 vector sweep, 1 matrix-core sweep */
 void simplex_set_sweep_mfma(int mode);
-/* pivots per tableau sweep (1..32, default 32): the pivots of a batch are selected on the
+/* pivots per tableau sweep (1..64; 0 = default: 64 in one shard's fused batch of a tableau with
+ * >= 8192 rows -- two stages of 32, applied by the matrix-core sweep -- else 32; more than 32
+ * only in one shard's fused batch): the pivots of a batch are selected on the
  * current values (pending pivots applied on the fly) and then applied to the tableau in one
  * sweep -- the same IEEE operations in the same order as one sweep per pivot */
 void simplex_set_batch(int pivots);
@@ -166,6 +168,8 @@ long long simplex_session_tableau(simplex_session *s, double *T, long long ld, d
 /* slack columns the sweeps currently move (m without slack compaction) */
 long long simplex_session_active_slacks(simplex_session *s);
 long long simplex_session_total_pivots(simplex_session *s);
+/* pivots per batch (and per sweep) of simplex_session_pivots on this session */
+int simplex_session_batch(simplex_session *s);
 /* per timed sweep of the last simplex_session_pivots call: pivots it applied and its
  * duration in microseconds; returns the number of sweeps logged (at most cap are copied) */
 long long simplex_session_launch_log(simplex_session *s, long long *rows, double *update_us, long long cap);

@@ -133,6 +133,7 @@ SIGNATURES = {
                                                     ctypes.POINTER(ctypes.c_int)]),
     "simplex_session_active_slacks": (ctypes.c_longlong, [ctypes.c_void_p]),
     "simplex_session_total_pivots": (ctypes.c_longlong, [ctypes.c_void_p]),
+    "simplex_session_batch": (ctypes.c_int, [ctypes.c_void_p]),
     "simplex_session_launch_log": (ctypes.c_longlong, [ctypes.c_void_p, c_ll_p, c_double_p, ctypes.c_longlong]),
     "simplex_session_close": (None, [ctypes.c_void_p]),
     "simplex_session_stamps": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_ulonglong)]),

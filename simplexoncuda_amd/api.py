@@ -228,6 +228,10 @@ class Session:
     def total_pivots(self):
         return self._lib.simplex_session_total_pivots(self._h)
 
+    def batch(self):
+        """Pivots per batch (and per sweep) of pivots() on this session."""
+        return self._lib.simplex_session_batch(self._h)
+
     def close(self):
         if self._h:
             self._lib.simplex_session_close(self._h)

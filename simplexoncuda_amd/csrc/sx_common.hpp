@@ -50,11 +50,15 @@ struct __attribute__((aligned(16))) DevState {
 // TilePart.elig: bit 0 = "some entry >= eps" of the tile (the unbounded test)
 #define SX_ELIG(x) ((x) & 1)
 
-// Deferred pivots: at most SX_KMAX pivots between two sweeps of the tableau.
-#define SX_KMAX 32
+// Deferred pivots: at most SX_KMAX pivots between two sweeps of the tableau.  A batch runs in
+// stages of SX_HMAX slots (the on-chip history of the fused batch, the hand-off records, the
+// per-pivot kernels, the vector sweep and the multi-rank batch hold one stage); the one-shard
+// fused batch runs two stages, whose 64 pivots the matrix-core sweep applies at once.
+#define SX_KMAX 64
+#define SX_HMAX 32
 // Position of slot s in a row of F: slot 4 k + g at g * (SX_KMAX / 4) + k, so the 4 slots one
 // matrix-core step applies (k_msweep: lane group g takes slot 4 k + g) are SX_KMAX / 4 doubles
-// apart and the SX_KMAX / 4 slots one lane needs are contiguous (16-byte loads).
+// apart and the slots one lane needs are contiguous (16-byte loads).
 __host__ __device__ constexpr int sx_fslot(int s) { return (s & 3) * (SX_KMAX / 4) + (s >> 2); }
 // Batch ids run 1 .. SX_BATCH_IDS - 1: the fused kernels' granule tags keep 15 bits of the id
 // (sx_kernels.hip make_tag).  When the ids wrap, the engine clears every id-tagged word (the
@@ -74,7 +78,8 @@ struct Pending {
     double *U;               // [SX_KMAX][ld] pivot rows (current leaving-row values, before /p)
     double *F;               // [rows][SX_KMAX] row factors -(a_ie / p), slot s at sx_fslot(s)
     PivRec *recs;            // [SX_KMAX]
-    unsigned long long *PM;  // [rows] (batch id << 32) | slots where the row left the basis
+    unsigned long long *PM;  // [rows] (batch id << 32) | slots < SX_HMAX where the row left the basis
+    unsigned long long *PM2; // [rows] the same for slots SX_HMAX + b (bit b): the second stage
     unsigned batch;          // id of the current batch (never 0)
     int q;                   // slot of the pivot being enqueued (pivots pending before it)
 };
@@ -150,7 +155,7 @@ struct TLay {
 
 // ---- kernel launchers (sx_kernels.hip) ----
 struct SweepCfg {
-    int batch;           // pivots per sweep (1..SX_KMAX): register slots of the sweep
+    int batch;           // pivots per sweep (1..SX_KMAX; the vector sweep: up to SX_HMAX)
     int rows_per_block;  // 1, 2 or 4 rows per step
     int sc1;             // cache policy of the tableau traffic: 0 nt loads + plain stores, 1 nt loads +
                          // write-through (sc1) stores (default), 2 default loads + sc1 stores,

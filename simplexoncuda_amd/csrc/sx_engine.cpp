@@ -57,7 +57,7 @@ struct Config {
     int sc1 = -1;         // write-through tableau stores: -1 auto, 0, 1
     int sweep_mfma = -1;  // the matrix-core sweep: -1 auto, 0 off, 1 on
     int shadow_sweep = 0;  // diagnostic (bench sessions): 0 off, -1 / cap > 0: a concurrent shadow sweep
-    int batch = 32;          // pivots per tableau sweep (deferred updates), 1..SX_KMAX
+    int batch = 0;           // pivots per tableau sweep (deferred updates), 1..SX_KMAX; 0 = auto
     int device = -1;
     int virtual_ranks = 1;
     std::vector<int> gpus;   // simplex_set_gpus: one process, one row-block shard per listed device
@@ -256,6 +256,7 @@ struct Shard {
     double *F = nullptr;              // pending row factors [rows][SX_KMAX]
     PivRec *recs = nullptr;           // pending pivot records [SX_KMAX]
     unsigned long long *PM = nullptr; // [rows] pending leaving-row slots (batch-tagged)
+    unsigned long long *PM2 = nullptr; // [rows] the same for the second stage's slots
     double *coef = nullptr;
     double *gemv_local = nullptr;
     double *gemv_all = nullptr;
@@ -690,10 +691,12 @@ class Engine {
         x.F = dalloc<double>(rows_alloc * SX_KMAX);
         x.recs = dalloc<PivRec>(SX_KMAX);
         x.PM = dalloc<unsigned long long>(rows_alloc);
+        x.PM2 = dalloc<unsigned long long>(rows_alloc);
         SX_HIP(hipMemsetAsync(x.U, 0, (size_t)SX_KMAX * ld * sizeof(double), x.s));
         SX_HIP(hipMemsetAsync(x.F, 0, rows_alloc * SX_KMAX * sizeof(double), x.s));
         SX_HIP(hipMemsetAsync(x.recs, 0, SX_KMAX * sizeof(PivRec), x.s));
         SX_HIP(hipMemsetAsync(x.PM, 0, rows_alloc * sizeof(unsigned long long), x.s));
+        SX_HIP(hipMemsetAsync(x.PM2, 0, rows_alloc * sizeof(unsigned long long), x.s));
         x.coef = dalloc<double>(rows_alloc);
         x.rhs_local = dalloc<double>(rpr);
         if (xchg) x.rhs_all = dalloc<double>((size_t)W * rpr);
@@ -741,7 +744,7 @@ class Engine {
             x.urec = -1;
         }
         for (void *p : {(void *)x.T, (void *)x.d, (void *)x.d_save, (void *)x.dx, (void *)x.colE, (void *)x.prow, (void *)x.prow_send,
-                        (void *)x.slot_send, (void *)x.slot_all, (void *)x.U, (void *)x.F, (void *)x.recs, (void *)x.PM,
+                        (void *)x.slot_send, (void *)x.slot_all, (void *)x.U, (void *)x.F, (void *)x.recs, (void *)x.PM, (void *)x.PM2,
                         (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
                         (void *)x.rhs_all, (void *)x.base, (void *)x.enter_parts, (void *)x.tiles_local, (void *)x.chan,
                         (void *)x.ga, (void *)x.gb, (void *)x.gdone, (void *)x.perm, (void *)x.iperm,
@@ -1033,17 +1036,27 @@ class Engine {
         c.batch = batch;
         c.rows_per_block = g_cfg.update_rows > 0 ? std::min(g_cfg.update_rows, 4) : (batch > 16 ? 4 : 2);
         c.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : 1;
-        c.mfma = g_cfg.sweep_mfma >= 0 ? g_cfg.sweep_mfma : 0;
+        // (a two-stage batch: the matrix-core sweep, the only one holding SX_KMAX slots)
+        c.mfma = batch > SX_HMAX ? 1 : (g_cfg.sweep_mfma >= 0 ? g_cfg.sweep_mfma : 0);
         // peer ranks read leaving rows straight from this tableau (system-scope loads over
         // xGMI): its stores must write through to memory, not stay dirty in an L2 of this device
         if (p2p && (rccl || multidev) && c.sc1 != 1 && c.sc1 != 2) c.sc1 = 1;
         return c;
     }
 
-    // pivots per sweep: the configured batch (1 while tracing every pivot)
+    // pivots per sweep: the configured batch (1 while tracing every pivot); two stages (SX_KMAX)
+    // only in one shard's fused batch -- the per-pivot kernels, the vector sweep and the
+    // multi-rank batch hold one stage (run_phase caps it again when the batch is not fused)
+    // Default: two stages when the tableau has >= 8192 rows -- the second stage's longer chains
+    // (+1 to +1.4 us per pivot, the first stage's 32 pending pivots applied on the fly) cost
+    // less than the sweep they save there (config 5: 27.3 -> 16.5 us of sweep per pivot, 24.0k
+    // -> 32.1k pivots/s), not at 4096 rows (config 3: 73.4k vs 72.0k pivots/s;
+    // profiles/r03_two_stage_chain_ab.txt)
     int batch_size() const {
         if (on_pivot) return 1;
-        return std::max(1, std::min(g_cfg.batch, SX_KMAX));
+        const int want = g_cfg.batch > 0 ? g_cfg.batch : (m >= 8192 ? SX_KMAX : SX_HMAX);
+        const int cap = (!xchg && sh.size() == 1 && g_cfg.fused != 0) ? SX_KMAX : SX_HMAX;
+        return std::max(1, std::min(want, cap));
     }
 
     Pending pending(const Shard &x) const {
@@ -1052,6 +1065,7 @@ class Engine {
         p.F = x.F;
         p.recs = x.recs;
         p.PM = x.PM;
+        p.PM2 = x.PM2;
         p.batch = batch_id;
         p.q = q_host;
         return p;
@@ -1229,6 +1243,7 @@ class Engine {
         for (auto &x : sh) {
             DevGuard g(x.dev);
             SX_HIP(hipMemsetAsync(x.PM, 0, sizeof(unsigned long long) * (x.rows > 0 ? (size_t)x.rows : 1), x.s));
+            SX_HIP(hipMemsetAsync(x.PM2, 0, sizeof(unsigned long long) * (x.rows > 0 ? (size_t)x.rows : 1), x.s));
             SX_HIP(hipMemsetAsync(x.ga, 0, sx_batch_granules_a() * sizeof(unsigned long long), x.s));
             SX_HIP(hipMemsetAsync(x.gb, 0, sx_batch_granules_b() * sizeof(unsigned long long), x.s));
             if (x.gdone) SX_HIP(hipMemsetAsync(x.gdone, 0, SX_MAXW * sizeof(unsigned long long), x.s));
@@ -1271,7 +1286,7 @@ class Engine {
         N = width;
         reset_state(max_pivots);
         enqueue_enter_partials();
-        const int K = batch_size();
+        int K = batch_size();
         const bool timed = ch && ch->on();
         std::vector<hipEvent_t> it_ev;  // TIMER CSV: one event pair per loop iteration
         if (on_pivot) {  // DEBUG: one pivot at a time, tableau printed after each
@@ -1285,6 +1300,7 @@ class Engine {
         // batches of K pivots + one sweep; the host polls the status of the batch before the
         // last one, so the device never waits on the host
         bool fused = !timed && fused_ok(K);
+        if (!fused) K = std::min(K, SX_HMAX);
         int hangs = 0;
         long long k = 0;
         for (; !on_pivot; ++k) {
@@ -1315,7 +1331,10 @@ class Engine {
                     // a fused batch's hand-off wait timed out (every rank sees it at the same
                     // batch): restore the state it found, re-run it on the per-pivot path
                     recover_hang(K);
-                    if (++hangs >= 2) fused = false;  // not twice more: stay on the per-pivot path
+                    if (++hangs >= 2) {  // not twice more: stay on the per-pivot path
+                        fused = false;
+                        K = std::min(K, SX_HMAX);
+                    }
                     if (read_state().status != SX_NOT_ENDED) break;
                     k = -1;  // restart the lagged polling
                     continue;
@@ -1354,7 +1373,10 @@ class Engine {
             SX_HIP(hipMemcpyAsync(x.d, x.d_save, sizeof(double) * N, hipMemcpyDeviceToDevice, x.s));
             SX_HIP(hipMemcpyAsync(&x.st->status, &ne, sizeof(int), hipMemcpyHostToDevice, x.s));
         }
-        for (int b = 0; b < K; ++b) enqueue_pivot();  // (the first gathers d)
+        for (int b = 0; b < K; ++b) {  // (the first gathers d; a two-stage batch: two sweeps)
+            enqueue_pivot();
+            if (q_host == SX_HMAX) enqueue_sweep();
+        }
         enqueue_sweep();
         sync_all();
     }
@@ -1665,7 +1687,7 @@ void simplex_set_update_rows(int rb) { g_cfg.update_rows = (rb == 1 || rb == 2 |
 void simplex_set_shadow_sweep(int mode) { g_cfg.shadow_sweep = mode; }
 void simplex_set_sweep_mfma(int mode) { g_cfg.sweep_mfma = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_store_sc1(int mode) { g_cfg.sc1 = mode < 0 ? -1 : (mode <= 4 ? mode : 1); }
-void simplex_set_batch(int pivots) { g_cfg.batch = pivots > 0 ? std::min(pivots, SX_KMAX) : 32; }
+void simplex_set_batch(int pivots) { g_cfg.batch = pivots > 0 ? std::min(pivots, SX_KMAX) : 0; }
 void simplex_set_device(int device) {
     g_cfg.device = device;
     if (device >= 0) SX_HIP(hipSetDevice(device));
@@ -1881,7 +1903,8 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
     // tableau (a call ends with one too, so T is materialised on return).  time_updates =
     // s > 0: bracket every s-th sweep with HIP events and log how many pivots it applied.
     Engine &E = *S->E;
-    const int K = E.batch_size();
+    int K = E.batch_size();
+    if (!E.fused_ok(K)) K = std::min(K, SX_HMAX);
     const long long every = time_updates > 0 ? time_updates : 0;
     const long long max_sweeps = (k + K - 1) / K + 1;
     const long long nt = every ? (max_sweeps + every - 1) / every : 0;
@@ -2022,6 +2045,10 @@ long long simplex_session_tableau(simplex_session *S, double *T, long long ld, d
 
 long long simplex_session_active_slacks(simplex_session *S) { return S->E->active_slacks(); }
 long long simplex_session_total_pivots(simplex_session *S) { return S->E->read_state().pivots; }
+int simplex_session_batch(simplex_session *S) {
+    const int K = S->E->batch_size();
+    return S->E->fused_ok(K) ? K : std::min(K, SX_HMAX);
+}
 
 int simplex_session_stamps(simplex_session *S, int k, unsigned long long *out) {
     // one fused batch of k pivots with in-kernel timestamps (diagnostic); out[k][8]
@@ -2133,6 +2160,7 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     double *F = dalloc<double>((size_t)rows * SX_KMAX);
     PivRec *recs = dalloc<PivRec>(SX_KMAX);
     unsigned long long *PM = dalloc<unsigned long long>(rows);
+    unsigned long long *PM2 = dalloc<unsigned long long>(rows);
     DevState *st = dalloc<DevState>(1);
     SX_HIP(hipMemsetAsync(T, 0, sizeof(double) * (size_t)rows * ld, s));
     // column 0 = b (first CRT seed), columns 1.. = A's rows (third), as generateRandomProblem
@@ -2148,15 +2176,17 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     sx_launch_gen_vector(sd[1] ^ 0x9e3779b9u, 0, rows * SX_KMAX, -1, 1, F, s);
     const unsigned B = 1;
     std::vector<PivRec> rc(SX_KMAX);
-    std::vector<unsigned long long> pm((size_t)rows, 0ull);
+    std::vector<unsigned long long> pm((size_t)rows, 0ull), pm2((size_t)rows, 0ull);
     for (int k = 0; k < SX_KMAX; ++k) {
         rc[k].r = (int)(((long long)k * rows) / pivots % rows);
         rc[k].e = k;
         rc[k].p = 1.0 + (double)(k % 97);
-        if (k < pivots) pm[(size_t)rc[k].r] = ((unsigned long long)B << 32) | (1ull << k);
+        if (k < pivots && k < SX_HMAX) pm[(size_t)rc[k].r] = ((unsigned long long)B << 32) | (1ull << k);
+        if (k < pivots && k >= SX_HMAX) pm2[(size_t)rc[k].r] = ((unsigned long long)B << 32) | (1ull << (k - SX_HMAX));
     }
     SX_HIP(hipMemcpyAsync(recs, rc.data(), sizeof(PivRec) * SX_KMAX, hipMemcpyHostToDevice, s));
     SX_HIP(hipMemcpyAsync(PM, pm.data(), sizeof(unsigned long long) * rows, hipMemcpyHostToDevice, s));
+    SX_HIP(hipMemcpyAsync(PM2, pm2.data(), sizeof(unsigned long long) * rows, hipMemcpyHostToDevice, s));
     DevState init;
     std::memset(&init, 0, sizeof(init));
     init.status = SX_NOT_ENDED;
@@ -2168,6 +2198,7 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     pd.F = F;
     pd.recs = recs;
     pd.PM = PM;
+    pd.PM2 = PM2;
     pd.batch = B;
     pd.q = pivots;
     TLay btl;  // one region: rows of ld doubles
@@ -2177,7 +2208,7 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     cfg.batch = pivots;
     cfg.rows_per_block = g_cfg.update_rows > 0 ? std::min(g_cfg.update_rows, 4) : (pivots > 16 ? 4 : 2);
     cfg.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : 1;  // (as sweep_cfg: write-through at every size)
-    cfg.mfma = g_cfg.sweep_mfma >= 0 ? g_cfg.sweep_mfma : 0;
+    cfg.mfma = pivots > SX_HMAX ? 1 : (g_cfg.sweep_mfma >= 0 ? g_cfg.sweep_mfma : 0);
     long long sweeps = 0;
     auto one = [&]() { sx_launch_sweep(T, rows, 0, ld, btl, cols, nullptr, 0, pd, st, (int)(sweeps & 1), cfg, s); };
     for (int w = 0; w < warmup; ++w, ++sweeps) one();
@@ -2192,7 +2223,7 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     SX_HIP(hipEventElapsedTime(&ms, e0, e1));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    for (void *p : {(void *)T, (void *)U, (void *)F, (void *)recs, (void *)PM, (void *)st}) (void)hipFree(p);
+    for (void *p : {(void *)T, (void *)U, (void *)F, (void *)recs, (void *)PM, (void *)PM2, (void *)st}) (void)hipFree(p);
     (void)hipStreamDestroy(s);
     if (bytes) *bytes = 16.0 * (double)rows * (double)cols;
     return 1e3 * (double)ms / (double)iters;

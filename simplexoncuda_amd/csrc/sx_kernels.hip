@@ -863,54 +863,60 @@ __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, uns
 // granule layout of one tile record
 // (k_batch: the RV..RF / OV..OU layouts below; k_batch_mr: v(2) pad(2) a(2) b(2) F(2 per slot) and
 // v(2) pad(2) U(2 per slot) inside the same strides)
-#define SX_GA_STRIDE (10 + 2 * SX_KMAX)  // ratio tile record, granules
-#define SX_GB_STRIDE (8 + 2 * SX_KMAX)   // objective tile record, granules
+#define SX_GA_STRIDE (10 + 2 * SX_HMAX)  // ratio tile record, granules (one stage of history)
+#define SX_GB_STRIDE (8 + 2 * SX_HMAX)   // objective tile record, granules
 __device__ __forceinline__ int rec2_a(int k) { return (k >> 1) * SX_GA_STRIDE + (k & 1); }
 // granules of all tile records
 __host__ __device__ __forceinline__ size_t sx_ga_size() { return (size_t)SX_TILE * SX_GA_STRIDE; }
 __host__ __device__ __forceinline__ size_t sx_gb_size() { return (size_t)SX_TILE * SX_GB_STRIDE; }
 __device__ __forceinline__ int rec2_b(int k) { return (k >> 1) * SX_GB_STRIDE + (k & 1); }
 
-// The batch's pending pivots s < q applied, in slot order, to a ratio row's entering-column
-// entry `a` (solver.cu:34-46 on that element): a / p_s at the slots in `bits` (the row itself
-// left the basis there), fma(F[row][s], U[s][e], a) at the others.  A wave none of whose rows
-// left the basis in this batch -- nearly always -- runs the plain fma chain: no per-slot
-// exec-mask branch, LDS reads batched 8 slots at a time (the guarded chain cost ~25
-// instructions per slot).
+// The history chains below read the block-uniform values of a slot (the entering column's
+// U[s][e], the leaving row's F[r][s], the pivots) through one register per wave -- lane s holds
+// slot s, read with v_readlane into scalar registers -- instead of an LDS read per slot: with
+// the fused batch's register file nearly full, per-slot LDS reads were issued one at a time
+// and each waited its round trip (ISA of round 3).
+__device__ __forceinline__ double rdlane(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+// The batch's pending pivots s < q of one stage applied, in slot order, to a ratio row's
+// entering-column entry `a` (solver.cu:34-46 on that element): a / p_s at the slots in `bits`
+// (the row itself left the basis there), fma(F[row][s], U[s][e], a) at the others.  A row that
+// left at slots in `bits` has, just before its last such slot sl, exactly the value the pivot
+// row of slot sl held in this column -- U[sl][e], formed by the objective tiles with the same
+// operations in the same order -- so its chain is U[sl][e] / p_sl followed by the fmas of the
+// slots after sl: one division and a select per slot instead of a branch per slot (~25
+// instructions each).  A wave none of whose rows left -- nearly always -- runs the plain chain.
 __device__ __forceinline__ double hist_col(double a, int q, unsigned bits, const double *s_hist, const double *s_ue,
                                            const double *s_p) {
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, lane = t & 63;
+    const double wu = s_ue[lane & (SX_HMAX - 1)];  // lane s: U[s][e]
     if (__ballot(bits != 0u) == 0ull) {
         int s = 0;
         for (; s + 8 <= q; s += 8) {
-            double h[8], ue[8];
+            double h[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                h[k] = s_hist[(s + k) * SX_TILE + t];
-                ue[k] = s_ue[s + k];
-            }
+            for (int k = 0; k < 8; ++k) h[k] = s_hist[(s + k) * SX_TILE + t];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) a = fma(h[k], ue[k], a);
+            for (int k = 0; k < 8; ++k) a = fma(h[k], rdlane(wu, s + k), a);
         }
-        for (; s < q; ++s) a = fma(s_hist[s * SX_TILE + t], s_ue[s], a);
+        for (; s < q; ++s) a = fma(s_hist[s * SX_TILE + t], rdlane(wu, s), a);
         return a;
     }
+    const int sl = bits ? 31 - __builtin_clz(bits) : -1;  // the row's last leaving slot
+    if (bits) a = s_ue[sl] / s_p[sl];
     for (int s0 = 0; s0 < q; s0 += 8) {  // (slots past q read slot s0 and are not used)
-        double h[8], ue[8], pp[8];
+        double h[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int s = s0 + k < q ? s0 + k : s0;
-            h[k] = s_hist[s * SX_TILE + t];
-            ue[k] = s_ue[s];
-            pp[k] = s_p[s];
-        }
+        for (int k = 0; k < 8; ++k) h[k] = s_hist[(s0 + k < q ? s0 + k : s0) * SX_TILE + t];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             if (s0 + k < q) {
-                if ((bits >> (s0 + k)) & 1u)
-                    a = a / pp[k];
-                else
-                    a = fma(h[k], ue[k], a);
+                const double y = fma(h[k], rdlane(wu, s0 + k), a);
+                a = s0 + k > sl ? y : a;
             }
         }
     }
@@ -919,46 +925,74 @@ __device__ __forceinline__ double hist_col(double a, int q, unsigned bits, const
 
 // The same for the pivot row's entry `u` on an objective tile's column: u / p_s at the slots
 // where the leaving row r itself left before (s_r[s] == r), else fma(F[r][s], U[s][j], u).
-// The slots where r left are wave-uniform (one ballot); when there are none the chain is
-// branch-free.
+// The slots where r left are block-uniform: with none the chain is branch-free; else it starts
+// from U[sl][j] / p_sl (this thread's own history of slot sl, the last) and runs the fmas of
+// the slots after sl.
 __device__ __forceinline__ double hist_row(double u, int q, int r, const double *s_hist, const double *s_fr,
                                            const double *s_p, const int *s_r) {
     const int t = threadIdx.x, lane = t & 63;
-    if (__ballot(lane < q && s_r[lane < q ? lane : 0] == r) == 0ull) {
-        int s = 0;
-        for (; s + 8 <= q; s += 8) {
-            double h[8], fr[8];
+    const double wf = s_fr[lane & (SX_HMAX - 1)];  // lane s: F[r][s]
+    const unsigned long long left = __ballot(lane < q && s_r[lane < q ? lane : 0] == r);
+    int s = 0;
+    if (left) {
+        const int sl = 63 - __builtin_clzll(left);
+        u = s_hist[sl * SX_TILE + t] / s_p[sl];
+        s = sl + 1;
+    }
+    for (; s + 8 <= q; s += 8) {
+        double h[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                h[k] = s_hist[(s + k) * SX_TILE + t];
-                fr[k] = s_fr[s + k];
-            }
+        for (int k = 0; k < 8; ++k) h[k] = s_hist[(s + k) * SX_TILE + t];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) u = fma(fr[k], h[k], u);
-        }
-        for (; s < q; ++s) u = fma(s_fr[s], s_hist[s * SX_TILE + t], u);
+        for (int k = 0; k < 8; ++k) u = fma(rdlane(wf, s + k), h[k], u);
+    }
+    for (; s < q; ++s) u = fma(rdlane(wf, s), s_hist[s * SX_TILE + t], u);
+    return u;
+}
+
+// A two-stage batch (k_batch, pivots SX_HMAX .. SX_KMAX - 1): the first stage's SX_HMAX pending
+// pivots, whose history each thread moved from LDS to registers (h[s]: a ratio row's factor F[.][s],
+// an objective column's pivot-row value U[s][.]), applied before the second stage's
+// (hist_col / hist_row on the LDS history): the same operations in slot order, the same
+// leaving-row shortcut.  s_u / s_f: the first stage's U[s][e] (entering column) / F[r][s]
+// (leaving row), block-uniform in LDS.
+__device__ __forceinline__ double stage1_col(double a, const double (&h)[SX_HMAX], unsigned bits, const double *s_u,
+                                             const double *s_p) {
+    const int lane = threadIdx.x & 63;
+    const double wu = s_u[lane & (SX_HMAX - 1)];
+    if (__ballot(bits != 0u) == 0ull) {
+#pragma unroll
+        for (int s = 0; s < SX_HMAX; ++s) a = fma(h[s], rdlane(wu, s), a);
+        return a;
+    }
+    const int sl = bits ? 31 - __builtin_clz(bits) : -1;
+    if (bits) a = s_u[sl] / s_p[sl];
+#pragma unroll
+    for (int s = 0; s < SX_HMAX; ++s) {
+        const double y = fma(h[s], rdlane(wu, s), a);
+        a = s > sl ? y : a;
+    }
+    return a;
+}
+__device__ __forceinline__ double stage1_row(double u, const double (&h)[SX_HMAX], int r, const double *s_f,
+                                             const double *s_p, const int *s_r) {
+    const int lane = threadIdx.x & 63;
+    const double wf = s_f[lane & (SX_HMAX - 1)];
+    const unsigned long long left = __ballot(lane < SX_HMAX && s_r[lane < SX_HMAX ? lane : 0] == r);
+    if (left == 0ull) {
+#pragma unroll
+        for (int s = 0; s < SX_HMAX; ++s) u = fma(rdlane(wf, s), h[s], u);
         return u;
     }
-    for (int s0 = 0; s0 < q; s0 += 8) {
-        double h[8], fr[8], pp[8];
-        int rr[8];
+    const int sl = 63 - __builtin_clzll(left);  // (block-uniform)
+    double hs = 0.0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int s = s0 + k < q ? s0 + k : s0;
-            h[k] = s_hist[s * SX_TILE + t];
-            fr[k] = s_fr[s];
-            pp[k] = s_p[s];
-            rr[k] = s_r[s];
-        }
+    for (int s = 0; s < SX_HMAX; ++s) hs = s == sl ? h[s] : hs;
+    u = hs / s_p[sl];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            if (s0 + k < q) {
-                if (rr[k] == r)
-                    u = u / pp[k];
-                else
-                    u = fma(fr[k], h[k], u);
-            }
-        }
+    for (int s = 0; s < SX_HMAX; ++s) {
+        const double y = fma(rdlane(wf, s), h[s], u);
+        u = s > sl ? y : u;
     }
     return u;
 }
@@ -976,8 +1010,8 @@ __device__ __forceinline__ double hist_row(double u, int q, int r, const double 
 // block call it; s_rr[0..cnt) are the batch's leaving rows (local = global: one shard).
 __device__ void activate_block(int *__restrict__ perm, int *__restrict__ iperm, unsigned char *__restrict__ act,
                                int *__restrict__ nact_p, int m, double *__restrict__ T, int rows, TLay tl, int s0,
-                               double *__restrict__ U, size_t ld, const int *s_rr, int cnt, int *s_pl, int *s_ol,
-                               int *s_cl, int *s_src, int *s_misc, double *s_u) {
+                               double *__restrict__ U, size_t ld, int nU, const int *s_rr, int cnt, int *s_pl,
+                               int *s_ol, int *s_cl, int *s_src, int *s_misc, double *s_u) {
     const int t = threadIdx.x;
     if (t < 64) {
         const int na0 = *nact_p;
@@ -1047,13 +1081,13 @@ __device__ void activate_block(int *__restrict__ perm, int *__restrict__ iperm, 
         s_src[t] = j;
     }
     __syncthreads();
-    for (int k = t; k < cnt * nl; k += blockDim.x) {
+    for (int k = t; k < nU * nl; k += blockDim.x) {
         const int s = k / nl, i = k - s * nl;
         s_u[k] = __longlong_as_double(
             (long long)ld_sc1(reinterpret_cast<const u64 *>(U + (size_t)s * ld + s0 + s_pl[s_src[i]])));
     }
     __syncthreads();
-    for (int k = t; k < cnt * nl; k += blockDim.x) {
+    for (int k = t; k < nU * nl; k += blockDim.x) {
         const int s = k / nl, i = k - s * nl;
         U[(size_t)s * ld + s0 + s_pl[i]] = s_u[k];
     }
@@ -1120,15 +1154,17 @@ constexpr int kOU = 8;
 __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t ld, TLay tl, Cols c,
                                                double *__restrict__ d, double *__restrict__ d_save, int *base,
                                                DevState *st, double *U, double *F, PivRec *recs,
-                                               unsigned long long *PM, unsigned B, int K, int NA, int NB,
+                                               unsigned long long *PM, unsigned long long *PM2, unsigned B, int K,
+                                               int NA, int NB,
                                                BatchChan *ch, u64 *ga, u64 *gb, unsigned long long *stamps,
                                                int *perm, int *iperm, unsigned char *act, int *nact, int m) {
-    extern __shared__ double s_hist[];  // [K][512]: F history (ratio blocks) / U history (objective blocks)
+    extern __shared__ double s_hist[];  // [stage slots][512]: F history (ratio blocks) / U history (objective blocks)
     __shared__ double s_v[16];
     __shared__ int s_i[16];
     __shared__ double s_p[SX_KMAX];                  // pivots of the batch
     __shared__ int s_r[SX_KMAX], s_e[SX_KMAX];       // leaving rows / entering variables of the batch
-    __shared__ double s_ue[SX_KMAX], s_fr[SX_KMAX];  // U[s][e] (entering column) / F[r][s] (leaving row)
+    __shared__ double s_ue[SX_HMAX], s_fr[SX_HMAX];  // U[s][e] (entering column) / F[r][s] (leaving row), this stage
+    __shared__ double s_ue1[SX_HMAX], s_fr1[SX_HMAX];  // the same for the first stage's slots (second stage)
     __shared__ double s_a[SX_TILE], s_b[SX_TILE];    // ratio blocks: entering column, RHS (winner lookup)
     __shared__ unsigned s_g[4 * SX_TILE];            // gathered granules
     __shared__ unsigned s_pay[SX_TILE];              // their payloads (two-granule records)
@@ -1163,7 +1199,12 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
         const bool liveB = !isA && ia < L;
         const int mj = c.map(1 + (liveB ? ia : 0));
         double b = liveA ? T[tl.idx(li, 0)] : 0.0;  // current RHS of the row
-        unsigned bits = 0u;                            // slots where this row left the basis
+        unsigned bits = 0u;                            // slots of this stage where this row left the basis
+        unsigned bits1 = 0u;                           // ... of the first stage (second stage)
+        double h1[SX_HMAX];                            // this thread's first-stage history (second stage)
+#pragma unroll
+        for (int s1 = 0; s1 < SX_HMAX; ++s1) h1[s1] = 0.0;
+        int hb = 0;                                    // first slot of the current stage
         double dj = liveB ? d[1 + ia] : 0.0;
         double d0 = (!isA && tb == 0 && t == 0) ? d[0] : 0.0;
         // the objective row as the batch found it, for the host to restore when the batch is
@@ -1180,11 +1221,32 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 status = SX_PIVOT_CAP;
                 break;
             }
+            if (q == SX_HMAX) {
+                // second stage: this thread's first-stage history to registers, the LDS history
+                // reused.  The block's first-stage F / U stores are written back from its L2
+                // (every thread's stores acknowledged, then one agent-scope release: buffer_wbl2)
+                // before any second-stage record of the block, so a block that reads one of them
+                // with sc1 loads (the leaving row's F, the entering column's U) after that
+                // record sees them
+#pragma unroll
+                for (int s1 = 0; s1 < SX_HMAX; ++s1) h1[s1] = s_hist[s1 * SX_TILE + t];
+                bits1 = bits;
+                bits = 0u;
+                if (t < SX_HMAX) s_ue1[t] = s_ue[t];  // (U[s][e] of pivot SX_HMAX: its objective record)
+                drain();
+                __syncthreads();
+                if (t == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                __syncthreads();
+                hb = SX_HMAX;
+            }
+            const int qq = q - hb;  // slot within the stage
             if (isA) {
                 const bool done = !(cmp_eps(dmin, 0.0) < 0);  // solver.cu:88: optimal
                 // ---- ratio tile: current entering column, ratios, tile winner
                 if (blockIdx.x == 0) SX_STAMP(0);
-                const double a = done ? 0.0 : hist_col(a_pre, q, bits, s_hist, s_ue, s_p);
+                double a1 = a_pre;
+                if (hb && !done) a1 = stage1_col(a1, h1, bits1, s_ue1, s_p);
+                const double a = done ? 0.0 : hist_col(a1, qq, bits, s_hist, s_ue, s_p + hb);
                 double rv = DBL_MAX;
                 int ri = -1, elig = 0;
                 if (liveA && !done) {
@@ -1223,7 +1285,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                         (long long)(unsigned)__builtin_amdgcn_readfirstlane((int)vb));
                     const int wl = wi >= 0 ? wi - (int)blockIdx.x * SX_TILE : 0;
                     const unsigned pl = (wi >= 0 ? (unsigned)wl : SX_NOIDX) | ((unsigned)any << 10);
-                    const int nG = kRF + 2 * q;
+                    const int nG = kRF + 2 * qq;
                     for (int k = t; k < nG; k += 64) {
                         unsigned data;
                         if (k == kRE) {
@@ -1253,12 +1315,18 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     int ei = -1, any = 0;
                     if (ok) wave_pass2(s_g, s_pay, NB, s_v, s_i, ev, ei, any);
                     ei = __builtin_amdgcn_readfirstlane(ei);
+                    // second stage: the next entering column's first-stage pivot-row values U[s][e]
+                    // (write-through, drained at the stage switch), loaded while the record is polled
+                    u64 ue1 = 0ull;
+                    if (hb && ok && ei >= 0 && t < SX_HMAX)
+                        ue1 = ld_sc1(reinterpret_cast<const u64 *>(U + (size_t)t * ld + c.map(1 + ei)));
                     if (ok) {
                         const int wt = ei >= 0 ? ei / SX_TILE : 0;
-                        ok = poll_wave(gb + (size_t)wt * SX_GB_STRIDE + kOP, (kOU - kOP) + 2 * (q + 1),
+                        ok = poll_wave(gb + (size_t)wt * SX_GB_STRIDE + kOP, (kOU - kOP) + 2 * (qq + 1),
                                        [](int k) { return k; }, tag, s_g, &ch->abort_w, 20000000ull, (unsigned *)nullptr);
-                        if (ok && t <= q) s_ue[t] = gd(s_g[kOU - kOP + 2 * t], s_g[kOU - kOP + 1 + 2 * t]);
+                        if (ok && t <= qq) s_ue[t] = gd(s_g[kOU - kOP + 2 * t], s_g[kOU - kOP + 1 + 2 * t]);
                     }
+                    if (hb && t < SX_HMAX) s_ue1[t] = __longlong_as_double((long long)ue1);
                     if (t == 0) {
                         s_ent_ok = ok;
                         s_ent_e = ei;
@@ -1295,14 +1363,15 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 }
                 cnt = q + 1;
                 const double f = -a / p;
-                s_hist[q * SX_TILE + t] = f;
+                s_hist[qq * SX_TILE + t] = f;
                 if (liveA) {
                     F[(size_t)li * SX_KMAX + sx_fslot(q)] = f;
                     if (li == r) {
                         b = b / p;
-                        bits |= 1u << q;
-                        const u64 w = PM[li];
-                        PM[li] = (((unsigned)(w >> 32) == B) ? w : ((u64)B << 32)) | (1ull << q);
+                        bits |= 1u << qq;
+                        unsigned long long *const P = hb ? PM2 : PM;
+                        const u64 w = P[li];
+                        P[li] = (((unsigned)(w >> 32) == B) ? w : ((u64)B << 32)) | (1ull << qq);
                     } else {
                         b = fma(f, br, b);
                     }
@@ -1342,11 +1411,17 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 // e, the ratio side's status and F[r][s < q], read by wave 0 into LDS
                 if (t < 64) {
                     const int wt = r >= 0 ? r / SX_TILE : 0;
-                    const int ok = poll_wave(ga + (size_t)wt * SX_GA_STRIDE + kRD, (kRF - kRD) + 2 * q,
+                    // second stage: the leaving row's first-stage factors F[r][s] (write-through,
+                    // drained at the stage switch), loaded while the record is polled
+                    u64 fr1 = 0ull;
+                    if (hb && t < SX_HMAX)
+                        fr1 = ld_sc1(reinterpret_cast<const u64 *>(F + (size_t)(r >= 0 ? r : 0) * SX_KMAX + sx_fslot(t)));
+                    const int ok = poll_wave(ga + (size_t)wt * SX_GA_STRIDE + kRD, (kRF - kRD) + 2 * qq,
                                              [](int k) { return k; }, tag, s_g, &ch->abort_w, 20000000ull,
                                              (unsigned *)nullptr);
+                    if (hb && t < SX_HMAX) s_fr1[t] = __longlong_as_double((long long)fr1);
                     if (ok) {
-                        if (t < q) s_fr[t] = gd(s_g[kRF - kRD + 2 * t], s_g[kRF - kRD + 1 + 2 * t]);
+                        if (t < qq) s_fr[t] = gd(s_g[kRF - kRD + 2 * t], s_g[kRF - kRD + 1 + 2 * t]);
                         if (t == 0) {
                             s_det_dmin = gd(s_g[0], s_g[1]);
                             s_p[q] = gd(s_g[kRA - kRD], s_g[kRA - kRD + 1]);
@@ -1383,13 +1458,12 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     cnt = q + 1;
                     // ---- objective tile: current pivot row on this column, d, tile winner
                     if (tb == 0) SX_STAMP(6);
-                    u = hist_row(u, q, r, s_hist, s_fr, s_p, s_r);
-                    s_hist[q * SX_TILE + t] = u;
+                    if (hb) u = stage1_row(u, h1, r, s_fr1, s_p, s_r);
+                    u = hist_row(u, qq, r, s_hist, s_fr, s_p + hb, s_r + hb);
+                    s_hist[qq * SX_TILE + t] = u;
                     if (tb == 0) SX_STAMP(7);
-                    // (write-through: the last block reads them back for the column activation)
-                    if (liveB && 1 + ia < c.Ns)
-                        __hip_atomic_store(reinterpret_cast<u64 *>(U + (size_t)q * ld + mj), (u64)__double_as_longlong(u),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    // (plain stores: written back at the stage switch and before the block leaves)
+                    if (liveB && 1 + ia < c.Ns) U[(size_t)q * ld + mj] = u;
                     const double fd = -dmin / p;  // updateCostsVector, solver.cu:48-56
                     if (tb == 0 && t == 0) d0 = fma(fd, br, d0);
                     if (liveB) {
@@ -1418,7 +1492,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                                               (long long)(unsigned)__builtin_amdgcn_readfirstlane((int)vb));
                     const int win = wi >= 0 ? wi - tb * SX_TILE : 0;
                     const unsigned pl = wi >= 0 ? (unsigned)win : SX_NOIDX;
-                    const int nG = kOU + 2 * (q + 1);
+                    const int nG = kOU + 2 * (qq + 1);
                     for (int k = t; k < nG; k += 64) {
                         unsigned data;
                         if (k == kOR) {
@@ -1471,6 +1545,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
     drain();
     __syncthreads();
     if (t == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // (the block's U stores out of its L2)
         const unsigned k = __hip_atomic_fetch_add(&ch->exit_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = k == (unsigned)(NA + NB) - 1;
         if (s_last) __hip_atomic_store(&ch->exit_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1478,10 +1553,18 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
     __syncthreads();
     if (!s_last || status0 != SX_NOT_ENDED) return;
     const bool hang = ld_sc1(&ch->abort_w) != 0u || aborted;
-    if (!hang && perm != nullptr && cnt > 0)
-        activate_block(perm, iperm, act, nact, m, const_cast<double *>(T), rows, tl, c.s0, U, ld, s_r, cnt,
-                       reinterpret_cast<int *>(s_g), reinterpret_cast<int *>(s_g) + 64, reinterpret_cast<int *>(s_g) + 128,
-                       reinterpret_cast<int *>(s_g) + 192, reinterpret_cast<int *>(s_pay), s_hist);
+    if (!hang && perm != nullptr && cnt > 0) {
+        // one stage at a time (a list entry per lane): the exchanges of the first stage's slots,
+        // then of the second's from the state the first left -- the same exchanges in slot order;
+        // each swaps the entries of all the batch's pending rows U[s]
+        for (int s1 = 0; s1 < cnt; s1 += SX_HMAX) {
+            if (s1) __syncthreads();
+            activate_block(perm, iperm, act, nact, m, const_cast<double *>(T), rows, tl, c.s0, U, ld, cnt, s_r + s1,
+                           cnt - s1 < SX_HMAX ? cnt - s1 : SX_HMAX, reinterpret_cast<int *>(s_g),
+                           reinterpret_cast<int *>(s_g) + 64, reinterpret_cast<int *>(s_g) + 128,
+                           reinterpret_cast<int *>(s_g) + 192, reinterpret_cast<int *>(s_pay), s_hist);
+        }
+    }
     if (t != 0) return;
     if (hang) {
         st->status = SX_HANG;
@@ -2124,15 +2207,19 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, T
 // tiles.  Out of place (Tdst != Tsrc, the pipelined sweep): every swept element is written, also
 // when the batch selected no pivot (a copy).  meta (or null: the count from st): the batch's
 // count and swept slacks as its last block recorded them.
+// NKB: 4-slot steps held (SX_HMAX / 4: one stage, 3 waves per SIMD; SX_KMAX / 4: two stages,
+// 2 waves per SIMD).
+template <int NKB>
 __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *Tdst, int rows, int row0, size_t ld,
                                                    TLay tl, int Ns, const int *__restrict__ nact, int s0,
                                                    const double *__restrict__ F, const double *__restrict__ U,
                                                    const PivRec *__restrict__ recs,
                                                    const unsigned long long *__restrict__ PM,
+                                                   const unsigned long long *__restrict__ PM2,
                                                    const DevState *__restrict__ st,
                                                    const SweepMeta *__restrict__ meta, unsigned B, int rev,
                                                    int *__restrict__ rec) {
-    constexpr int NKB = SX_KMAX / 4;
+    constexpr int KS = 4 * NKB;  // slots held
     sweep_record(rec, st, nact);
     const int cnt = meta ? (meta->tag == B ? meta->count : 0) : (st->batch_tag == B ? st->batch_count : 0);
     if (cnt <= 0 && Tdst == Tsrc) return;
@@ -2156,6 +2243,7 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
     const size_t ldr = inB ? tl.ldB : tl.ldA;
     const int cr = inB ? c0 - tl.jB : c0;
     const unsigned mask = cnt > 0 ? slot_mask(cnt) : 0u;
+    const unsigned mask2 = cnt > SX_HMAX ? slot_mask(cnt - SX_HMAX) : 0u;
     const int nkb = (cnt + 3) >> 2;
     const int OOB = 0x7fffffff;
     {
@@ -2176,7 +2264,7 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
             const int fr = r0 + jl;  // the A-operand row of this lane
             double ff[NKB];
             {
-                const double *Fr = F + (size_t)(fr < rows ? fr : r0) * SX_KMAX + rg * NKB;
+                const double *Fr = F + (size_t)(fr < rows ? fr : r0) * SX_KMAX + rg * (SX_KMAX / 4);
 #pragma unroll
                 for (int kb = 0; kb < NKB; kb += 2) {
                     const double2 v = *reinterpret_cast<const double2 *>(Fr + kb);
@@ -2189,7 +2277,8 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
             }
             // row fr's slots as a leaving row (read with the tableau; which strips hold a leaving
             // row is decided after the first pair's matrix steps, so this load overlaps them)
-            const unsigned lb = fr < rows ? pend_bits(PM, fr, B, mask) : 0u;
+            const unsigned lb =
+                fr < rows ? (pend_bits(PM, fr, B, mask) | (mask2 ? pend_bits(PM2, fr, B, mask2) : 0u)) : 0u;
             bool fix = false;
             unsigned skip = 0u;  // bit v: row r0 + rg + 4v is a leaving row (not stored here)
             // one buffer resource per strip (wave-uniform), holding the strip's valid rows; rows
@@ -2256,20 +2345,21 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
     // per lane, the guarded chain from its stored values (the strips left them unwritten)
     if (cnt <= 0) return;
     const int j = c0 + l;
-    double u[SX_KMAX];
+    double u[KS];
 #pragma unroll
-    for (int sl = 0; sl < SX_KMAX; ++sl) u[sl] = (sl < cnt && j < Ns) ? U[(size_t)sl * ld + j] : 0.0;
+    for (int sl = 0; sl < KS; ++sl) u[sl] = (sl < cnt && j < Ns) ? U[(size_t)sl * ld + j] : 0.0;
     for (int s = gy; s < cnt; s += G) {
         const int r = recs[s].r - row0;
         if (r < 0 || r >= rows) continue;
-        const unsigned bits = pend_bits(PM, r, B, mask);
-        if (bits == 0u || (int)__builtin_ctz(bits) != s) continue;  // (not its first slot)
+        const unsigned long long bits = (unsigned long long)pend_bits(PM, r, B, mask) |
+                                        ((unsigned long long)(mask2 ? pend_bits(PM2, r, B, mask2) : 0u) << SX_HMAX);
+        if (bits == 0ull || (int)__builtin_ctzll(bits) != s) continue;  // (not its first slot)
         const double *Fr = F + (size_t)r * SX_KMAX;
         double x = j < Ns ? Tr[(size_t)r * ldr + cr + l] : 0.0;
 #pragma unroll
-        for (int sl = 0; sl < SX_KMAX; ++sl) {
+        for (int sl = 0; sl < KS; ++sl) {
             if (sl < cnt) {
-                if ((bits >> sl) & 1u)
+                if ((bits >> sl) & 1ull)
                     x = x / recs[sl].p;
                 else
                     x = fma(Fr[sx_fslot(sl)], u[sl], x);
@@ -2538,7 +2628,7 @@ void sx_launch_ratio_select(const double *T, int rows, int row0, size_t ld, TLay
     int g = (rows + SX_TILE - 1) / SX_TILE;
     if (g < 1) g = 1;  // a shard without rows still decides optimality for its own state
     if (select && g > SX_TILE) SX_FATAL("too many ratio tiles for the 512-thread pass 2");
-    if (pd.q < 0 || pd.q >= SX_KMAX) SX_FATAL("pending slot out of range");
+    if (pd.q < 0 || pd.q >= SX_HMAX) SX_FATAL("pending slot out of range");
     k_ratio_select<<<g, SX_TILE, 0, s>>>(T, rows, row0, ld, tl, tiles_local, colE, st, base, select ? 1 : 0, slots,
                                          slot_stride, c, pd.F, pd.U, pd.recs, pd.PM, pd.batch, pd.q);
 }
@@ -2626,9 +2716,9 @@ static void launch_sweep_rb(int rb, double *T, int rows, size_t ld, TLay tl, int
 template <int KT>
 static void launch_sweep_k(int rb, int pol, double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0,
                            const Pending &pd, const DevState *st, int rev, hipStream_t s) {
-    if (KT == SX_KMAX && pol == 2) return launch_sweep_rb<KT, 2>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
-    if (KT == SX_KMAX && pol == 3) return launch_sweep_rb<KT, 3>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
-    if (KT == SX_KMAX && pol == 4) return launch_sweep_rb<KT, 4>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+    if (KT == SX_HMAX && pol == 2) return launch_sweep_rb<KT, 2>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+    if (KT == SX_HMAX && pol == 3) return launch_sweep_rb<KT, 3>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+    if (KT == SX_HMAX && pol == 4) return launch_sweep_rb<KT, 4>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     if (pol == 0) return launch_sweep_rb<KT, 0>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     launch_sweep_rb<KT, 1>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
 }
@@ -2645,9 +2735,15 @@ void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, 
         if (ld % 2 != 0 || tl.ldA % 2 != 0 || (tl.jB < Ns && (tl.jB % 256 != 0 || tl.ldB % 2 != 0 || tl.offB % 2 != 0)))
             SX_FATAL("matrix-core sweep: 16-byte rows and 256-aligned regions required");
         const int cb = (Ns + 255) / 256;
-        dim3 grid(cb, row_slots(sweep_capacity(k_msweep), cb, rows, 16));
-        k_msweep<<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st, nullptr,
-                                      pd.batch, rev, g_sweep_rec);
+        if (cfg.batch > SX_HMAX) {
+            dim3 grid(cb, row_slots(sweep_capacity(k_msweep<SX_KMAX / 4>), cb, rows, 16));
+            k_msweep<SX_KMAX / 4><<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM,
+                                                       pd.PM2, st, nullptr, pd.batch, rev, g_sweep_rec);
+        } else {
+            dim3 grid(cb, row_slots(sweep_capacity(k_msweep<SX_HMAX / 4>), cb, rows, 16));
+            k_msweep<SX_HMAX / 4><<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM,
+                                                       pd.PM2, st, nullptr, pd.batch, rev, g_sweep_rec);
+        }
         return;
     }
     const int k = cfg.batch;  // pivots the sweep may have to apply (register slots)
@@ -2659,10 +2755,10 @@ void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, 
         launch_sweep_k<8>(cfg.rows_per_block, cfg.sc1, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else if (k <= 16)
         launch_sweep_k<16>(cfg.rows_per_block, cfg.sc1, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
-    else if (k <= SX_KMAX)
-        launch_sweep_k<SX_KMAX>(cfg.rows_per_block, cfg.sc1, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+    else if (k <= SX_HMAX)
+        launch_sweep_k<SX_HMAX>(cfg.rows_per_block, cfg.sc1, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else
-        SX_FATAL("batch larger than SX_KMAX");
+        SX_FATAL("the vector sweep holds at most SX_HMAX slots");
 }
 
 void sx_launch_msweep_oop(const double *Tsrc, double *Tdst, int rows, int row0, size_t ld, TLay tl, int Ns,
@@ -2672,13 +2768,15 @@ void sx_launch_msweep_oop(const double *Tsrc, double *Tdst, int rows, int row0, 
     if (ld % 2 != 0 || tl.ldA % 2 != 0 || (tl.jB < Ns && (tl.jB % 256 != 0 || tl.ldB % 2 != 0 || tl.offB % 2 != 0)))
         SX_FATAL("matrix-core sweep: 16-byte rows and 256-aligned regions required");
     const int cb = (Ns + 255) / 256;
-    const int cap = grid_cap > 0 ? std::min(grid_cap, sweep_capacity(k_msweep)) : sweep_capacity(k_msweep);
+    auto kern = k_msweep<SX_KMAX / 4>;
+    const int cap = grid_cap > 0 ? std::min(grid_cap, sweep_capacity(kern)) : sweep_capacity(kern);
     dim3 grid(cb, row_slots(cap, cb, rows, 16));
-    k_msweep<<<grid, 256, 0, s>>>(Tsrc, Tdst, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st, meta,
-                                  pd.batch, rev, nullptr);
+    kern<<<grid, 256, 0, s>>>(Tsrc, Tdst, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, pd.PM2, st, meta,
+                              pd.batch, rev, nullptr);
 }
 
-static size_t batch_lds(int k) { return (size_t)k * SX_TILE * sizeof(double); }
+// LDS history of a fused batch of k pivots: one stage
+static size_t batch_lds(int k) { return (size_t)(k < SX_HMAX ? k : SX_HMAX) * SX_TILE * sizeof(double); }
 
 size_t sx_batch_granules_a() { return sx_ga_size(); }
 size_t sx_batch_granules_b() { return sx_gb_size(); }
@@ -2710,11 +2808,12 @@ void sx_launch_batch(const double *T, int rows, size_t ld, TLay tl, Cols c, doub
     if (!sx_batch_fits(rows, c, k)) SX_FATAL("fused batch grid does not fit the device");
     const int NA = (rows + SX_TILE - 1) / SX_TILE, NB = (c.N - 1 + SX_TILE - 1) / SX_TILE;
     k_batch<<<NA + NB, SX_TILE, batch_lds(k), s>>>(T, rows, ld, tl, c, d, d_save, base, st, pd.U, pd.F, pd.recs, pd.PM,
-                                                   pd.batch, k, NA, NB, chan, ga, gb, stamps, perm, iperm, act, nact, m);
+                                                   pd.PM2, pd.batch, k, NA, NB, chan, ga, gb, stamps, perm, iperm, act,
+                                                   nact, m);
 }
 
 bool sx_batch_mr_fits(int slots, int nb_local, int k, int grids) {
-    if (k < 1 || k > SX_KMAX || slots < 1 || slots > SX_TILE) return false;
+    if (k < 1 || k > SX_HMAX || slots < 1 || slots > SX_TILE) return false;  // (one stage)
     static int per_cu[SX_KMAX + 1] = {0};
     static int cus = 0;
     if (per_cu[k] == 0) {

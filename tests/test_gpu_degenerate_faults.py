@@ -90,17 +90,21 @@ def test_degenerate_public_entry(gpu):
 
 
 # ------------------------------------------------------------------ fused-batch aborts
-@pytest.mark.parametrize("inject", [0, 3, 40])
-def test_hang_recovery_bit_exact(gpu, inject):
+@pytest.mark.parametrize("batch", [0, 64])
+@pytest.mark.parametrize("inject", [0, 3, 30])
+def test_hang_recovery_bit_exact(gpu, inject, batch):
     """config 2's instance (2003 + 69 pivots, published): the inject-th fused batch of the
-    solve aborts; it is undone and re-run, and the whole solve stays bit-exact"""
+    solve aborts; it is undone and re-run (a two-stage batch: two per-pivot stages), and the
+    whole solve stays bit-exact"""
     lib = sx.load()
     p = sx.generateRandomProblem(2048, 1024, 205824, 1, 100)
     r0 = lib.simplex_hang_recoveries()
     lib.simplex_set_hang_inject(inject)
+    sx.set_batch(batch)
     try:
         got = solve_both(*p.arrays())
     finally:
+        sx.set_batch(0)
         lib.simplex_set_hang_inject(-1)
         p.close()
     assert lib.simplex_hang_recoveries() == r0 + 1

@@ -184,21 +184,46 @@ def test_virtual_ranks_two_phase(gpu, W):
 # ------------------------------------------------------------------ bench session
 def test_session_pivots(gpu):
     p = sx.generateRandomProblem(2048, 1024, 205824, 1, 100)
-    s = sx.Session(p)
-    t = s.pivots(50, time_updates=True)
-    # 50 pivots = one full batch of 32 + one of 18, each ending with a sweep
-    assert t.pivots == 50 and t.status == sx.NOT_ENDED and t.update_launches == 2 and t.swept_pivots == 50
-    assert t.update_ms > 0 and t.wall_ms >= t.update_ms
-    assert t.stored_width == 1 + 2048 + 1024 and t.width == 1 + 2048 + 2 * 1024
-    # slack compaction: a sweep moves 1+n columns plus the slacks of rows that have left
-    assert 16.0 * 1024 * (1 + 2048) < t.update_bytes <= 16.0 * 1024 * (1 + 2048 + 50)
-    assert t.swept_bytes == 2 * t.update_bytes
-    applied, us = s.launch_log()
-    assert list(applied) == [32, 18] and (us > 0).all()
-    t2 = s.pivots(10000, time_updates=1)
-    assert s.total_pivots() == 2003 and t2.status == sx.FEASIBLE
-    assert t2.swept_pivots == 2003 - 50  # no-op sweeps after the phase ended are not counted
-    s.close()
+    sx.set_batch(32)  # (the library reads it at every call)
+    try:
+        s = sx.Session(p)
+        assert s.batch() == 32
+        t = s.pivots(50, time_updates=True)
+        # 50 pivots = one full batch of 32 + one of 18, each ending with a sweep
+        assert t.pivots == 50 and t.status == sx.NOT_ENDED and t.update_launches == 2 and t.swept_pivots == 50
+        assert t.update_ms > 0 and t.wall_ms >= t.update_ms
+        assert t.stored_width == 1 + 2048 + 1024 and t.width == 1 + 2048 + 2 * 1024
+        # slack compaction: a sweep moves 1+n columns plus the slacks of rows that have left
+        assert 16.0 * 1024 * (1 + 2048) < t.update_bytes <= 16.0 * 1024 * (1 + 2048 + 50)
+        assert t.swept_bytes == 2 * t.update_bytes
+        applied, us = s.launch_log()
+        assert list(applied) == [32, 18] and (us > 0).all()
+        t2 = s.pivots(10000, time_updates=1)
+        assert s.total_pivots() == 2003 and t2.status == sx.FEASIBLE
+        assert t2.swept_pivots == 2003 - 50  # no-op sweeps after the phase ended are not counted
+        s.close()
+    finally:
+        sx.set_batch(0)
+
+
+def test_session_two_stage_batches(gpu):
+    """64-pivot batches on one shard (the default from 8192 rows): one sweep per batch"""
+    p = sx.generateRandomProblem(2048, 1024, 205824, 1, 100)
+    sx.set_batch(64)
+    try:
+        s = sx.Session(p)
+        assert s.batch() == 64
+        t = s.pivots(150, time_updates=True)
+        applied, us = s.launch_log()
+        assert t.pivots == 150 and list(applied) == [64, 64, 22] and (us > 0).all()
+        t2 = s.pivots(10000)
+        assert s.total_pivots() == 2003 and t2.status == sx.FEASIBLE
+        s.close()
+    finally:
+        sx.set_batch(0)
+    s2 = sx.Session(generated=(512, 8192, 512 * 100 + 8192, 1, 100))
+    assert s2.batch() == 64
+    s2.close()
 
 
 def _pivots_with(cfg, T, d, base, k):
@@ -257,6 +282,32 @@ def test_matrix_core_sweep_bit_exact(gpu, batch, fused, mfma):
     oracle.solve(T, d, base, max_pivots=75)
     assert done == 75
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+@pytest.mark.parametrize("batch", [33, 40, 63, 64])
+@pytest.mark.parametrize("inst", [(333, 1025, 7), (300, 1100, 11)])
+def test_two_stage_batch_bit_exact(gpu, batch, inst):
+    """batches of more than 32 pivots on one shard: the fused batch's second stage (the first
+    stage's history in registers, its U / F read back write-through) and the 64-slot matrix-core
+    sweep (slots past 32 in PM2), partial last batches: the oracle's bits"""
+    T, d, base = _phase1_state(*inst)
+    Tg, dg, bg, st, done = _pivots_with({"batch": batch}, T, d, base, 150)
+    oracle.solve(T, d, base, max_pivots=150)
+    assert done == 150
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+@pytest.mark.parametrize("n,m,seed,lo,hi", [(64, 128, 6528, 1, 100), (300, 1100, 41100, 1, 100),
+                                            (129, 1513, 77, -100, 100), (40, 700, 4070, 1, 100)])
+def test_two_stage_batch_whole_phase(gpu, n, m, seed, lo, hi):
+    """whole two-phase solves with the default 64-pivot batches (phase ends inside either stage,
+    rows leaving in both stages of one batch, slack compaction over two activation passes)"""
+    p = sx.generateRandomProblem(n, m, seed, lo, hi)
+    sx.set_batch(64)
+    try:
+        _check_two_phase(p)
+    finally:
+        sx.set_batch(0)
 
 
 @pytest.mark.parametrize("W", [2, 4])
@@ -592,10 +643,12 @@ def test_slack_compaction_generated_session_width(gpu):
     """device-built tableau: the timed sweeps move 1+n+(touched slacks) columns"""
     n, m = 512, 2048
     s = sx.Session(generated=(n, m, n * 100 + m, 1, 100))
+    K = s.batch()
+    assert K == 32  # (the default below 8192 rows)
     t = s.pivots(96, time_updates=1)
     active = s.active_slacks()
     s.close()
     assert 0 < active <= 96
-    assert t.update_launches == 3 and t.swept_pivots == 96
+    assert t.update_launches == (96 + K - 1) // K and t.swept_pivots == 96
     assert t.update_bytes <= 16.0 * m * (1 + n + active) + 1e-6
     assert t.update_bytes < 16.0 * m * t.stored_width

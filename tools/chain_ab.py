@@ -8,7 +8,8 @@ usage: python tools/chain_ab.py <setting>=<v1>,<v2> [config=config5,config3] [ro
             waves (simplex_set_update_waves: the sweep's grid as a multiple of the resident blocks),
             policy (simplex_set_store_sc1: the sweep's cache policy 0..4, -1 = default),
             mfma (simplex_set_sweep_mfma: 0 vector sweep, 1 matrix-core sweep, -1 auto),
-            shadow (simplex_set_shadow_sweep: 0 off, -1 / cap: a concurrent shadow sweep per batch)"""
+            shadow (simplex_set_shadow_sweep: 0 off, -1 / cap: a concurrent shadow sweep per batch),
+            batch (simplex_set_batch: pivots per batch and sweep, 0 = default)"""
 import os
 import sys
 
@@ -49,8 +50,9 @@ def main():
               "waves": lambda v: lib.simplex_set_update_waves(float(v)),
               "policy": lambda v: lib.simplex_set_store_sc1(int(v)),
               "mfma": lambda v: lib.simplex_set_sweep_mfma(int(v)),
-              "shadow": lambda v: lib.simplex_set_shadow_sweep(int(v))}[name]
-    reset = {"regions": 1, "rows": 0, "waves": 0, "policy": -1, "mfma": -1, "shadow": 0}[name]
+              "shadow": lambda v: lib.simplex_set_shadow_sweep(int(v)),
+              "batch": lambda v: lib.simplex_set_batch(int(v))}[name]
+    reset = {"regions": 1, "rows": 0, "waves": 0, "policy": -1, "mfma": -1, "shadow": 0, "batch": 0}[name]
     print("stamps (us): ratio compute | ratio argmin+publish | -> selection seen | pass2 + row details |"
           " row compute | obj argmin+publish | -> entering seen | entering history | pivot")
     for r in range(rounds):
@@ -59,8 +61,8 @@ def main():
             for v in vals.split(","):
                 setter(v)
                 s = sx.Session(generated=(n, m, seed, 1, 100))
-                s.pivots(64)
-                tim = s.pivots(PIVOTS[cfg], time_updates=1)
+                s.pivots(128)
+                tim = s.pivots(PIVOTS[cfg] // s.batch() * s.batch(), time_updates=1)
                 st = stamps_summary(s)
                 s.close()
                 per = tim.wall_ms * 1e3 / tim.pivots
