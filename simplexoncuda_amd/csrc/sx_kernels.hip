@@ -2262,6 +2262,26 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
         for (int g = gy; g < nstrip; g += G) {
             const int r0 = (rev ? nstrip - 1 - g : g) * 16;
             const int fr = r0 + jl;  // the A-operand row of this lane
+            // one buffer resource per strip (wave-uniform), holding the strip's valid rows; rows
+            // past the end read 0 and drop their stores
+            const int nr = rows - r0 < 16 ? rows - r0 : 16;
+            const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<double *>(Tr) + (size_t)r0 * ldr, 0, (int)((size_t)nr * ldr * 8), 0x00020000);
+            const __amdgpu_buffer_rsrc_t rss =
+                __builtin_amdgcn_make_buffer_rsrc(Tw + (size_t)r0 * ldr, 0, (int)((size_t)nr * ldr * 8), 0x00020000);
+            // issue order: both pairs' tableau tiles, the strip's factors, its leaving-row bits --
+            // one memory round trip per strip (the bits are only needed after the first pair's
+            // matrix steps, and the counter waits are in issue order)
+            double2 cx[2][4];
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int j = c0 + 32 * p + 2 * jl;
+                    const int off = (int)(((size_t)(rg + 4 * v) * ldr + cr + 32 * p + 2 * jl) * 8);
+                    cx[p][v] = __builtin_bit_cast(
+                        double2, __builtin_amdgcn_raw_buffer_load_b128(rsl, j < Ns ? off : OOB, 0, 2));
+                }
             double ff[NKB];
             {
                 const double *Fr = F + (size_t)(fr < rows ? fr : r0) * SX_KMAX + rg * (SX_KMAX / 4);
@@ -2271,35 +2291,19 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
                     ff[kb] = v.x;
                     ff[kb + 1] = v.y;
                 }
-#pragma unroll
-                for (int kb = 0; kb < NKB; ++kb)
-                    if (4 * kb + rg >= cnt) ff[kb] = -0.0;
             }
-            // row fr's slots as a leaving row (read with the tableau; which strips hold a leaving
-            // row is decided after the first pair's matrix steps, so this load overlaps them)
-            const unsigned lb =
-                fr < rows ? (pend_bits(PM, fr, B, mask) | (mask2 ? pend_bits(PM2, fr, B, mask2) : 0u)) : 0u;
+            const int frc = fr < rows ? fr : r0;
+            const unsigned long long pm1 = PM[frc], pm2 = PM2[frc];
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+                if (4 * kb + rg >= cnt) ff[kb] = -0.0;
             bool fix = false;
             unsigned skip = 0u;  // bit v: row r0 + rg + 4v is a leaving row (not stored here)
-            // one buffer resource per strip (wave-uniform), holding the strip's valid rows; rows
-            // past the end read 0 and drop their stores
-            const int nr = rows - r0 < 16 ? rows - r0 : 16;
-            const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<double *>(Tr) + (size_t)r0 * ldr, 0, (int)((size_t)nr * ldr * 8), 0x00020000);
-            const __amdgpu_buffer_rsrc_t rss =
-                __builtin_amdgcn_make_buffer_rsrc(Tw + (size_t)r0 * ldr, 0, (int)((size_t)nr * ldr * 8), 0x00020000);
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
                 const int j = c0 + 32 * p + 2 * jl, jr = cr + 32 * p + 2 * jl;
-                double2 cx[4];
-#pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    const int off = (int)(((size_t)(rg + 4 * v) * ldr + jr) * 8);
-                    cx[v] = __builtin_bit_cast(double2,
-                                               __builtin_amdgcn_raw_buffer_load_b128(rsl, j < Ns ? off : OOB, 0, 2));
-                }
-                d4_t ax = {cx[0].x, cx[1].x, cx[2].x, cx[3].x};
-                d4_t ay = {cx[0].y, cx[1].y, cx[2].y, cx[3].y};
+                d4_t ax = {cx[p][0].x, cx[p][1].x, cx[p][2].x, cx[p][3].x};
+                d4_t ay = {cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
                 if (nkb == NKB) {
 #pragma unroll
                     for (int kb = 0; kb < NKB; ++kb) {
@@ -2315,6 +2319,10 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
                         }
                 }
                 if (p == 0) {
+                    // row fr's slots as a leaving row (both stages)
+                    const unsigned lb = fr < rows ? ((((unsigned)(pm1 >> 32) == B) ? ((unsigned)pm1 & mask) : 0u) |
+                                                     (((unsigned)(pm2 >> 32) == B) ? ((unsigned)pm2 & mask2) : 0u))
+                                                  : 0u;
                     fix = __ballot(lb != 0u) != 0ull;
                     if (fix)
 #pragma unroll
@@ -2345,9 +2353,6 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
     // per lane, the guarded chain from its stored values (the strips left them unwritten)
     if (cnt <= 0) return;
     const int j = c0 + l;
-    double u[KS];
-#pragma unroll
-    for (int sl = 0; sl < KS; ++sl) u[sl] = (sl < cnt && j < Ns) ? U[(size_t)sl * ld + j] : 0.0;
     for (int s = gy; s < cnt; s += G) {
         const int r = recs[s].r - row0;
         if (r < 0 || r >= rows) continue;
@@ -2356,13 +2361,20 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
         if (bits == 0ull || (int)__builtin_ctzll(bits) != s) continue;  // (not its first slot)
         const double *Fr = F + (size_t)r * SX_KMAX;
         double x = j < Ns ? Tr[(size_t)r * ldr + cr + l] : 0.0;
+        // (the column's pivot-row values 16 slots at a time: few registers, loads only here)
+        for (int c1 = 0; c1 < cnt; c1 += 16) {
+            double uu[16];
 #pragma unroll
-        for (int sl = 0; sl < KS; ++sl) {
-            if (sl < cnt) {
-                if ((bits >> sl) & 1ull)
-                    x = x / recs[sl].p;
-                else
-                    x = fma(Fr[sx_fslot(sl)], u[sl], x);
+            for (int k = 0; k < 16; ++k) uu[k] = (c1 + k < cnt && j < Ns) ? U[(size_t)(c1 + k) * ld + j] : 0.0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int sl = c1 + k;
+                if (sl < cnt) {
+                    if ((bits >> sl) & 1ull)
+                        x = x / recs[sl].p;
+                    else
+                        x = fma(Fr[sx_fslot(sl)], uu[k], x);
+                }
             }
         }
         const __amdgpu_buffer_rsrc_t rsr =
