@@ -56,10 +56,13 @@ struct __attribute__((aligned(16))) DevState {
 // fused batch runs two stages, whose 64 pivots the matrix-core sweep applies at once.
 #define SX_KMAX 64
 #define SX_HMAX 32
-// Position of slot s in a row of F: slot 4 k + g at g * (SX_KMAX / 4) + k, so the 4 slots one
-// matrix-core step applies (k_msweep: lane group g takes slot 4 k + g) are SX_KMAX / 4 doubles
-// apart and the slots one lane needs are contiguous (16-byte loads).
-__host__ __device__ constexpr int sx_fslot(int s) { return (s & 3) * (SX_KMAX / 4) + (s >> 2); }
+// Position of row i's factor of slot s in F: rows in strips of 16, each strip slot-major
+// ([strip][slot][16 rows]).  The matrix-core sweep's A operand for 4 slots of a 16-row strip is
+// then 64 consecutive doubles (one coalesced load per 4-slot step), and a batch's per-pivot
+// factor column is written 16 consecutive doubles per strip.  F holds round_up(rows, 16) rows.
+__host__ __device__ constexpr size_t sx_fidx(long long i, int s) {
+    return (size_t)(i >> 4) * (16 * SX_KMAX) + (size_t)s * 16 + (size_t)(i & 15);
+}
 // Batch ids run 1 .. SX_BATCH_IDS - 1: the fused kernels' granule tags keep 15 bits of the id
 // (sx_kernels.hip make_tag).  When the ids wrap, the engine clears every id-tagged word (the
 // PM pending-leaving masks and the granule records) first, so no stale tag can match.
@@ -76,7 +79,7 @@ struct __attribute__((aligned(16))) PivRec {
 // being enqueued (kernel arguments).
 struct Pending {
     double *U;               // [SX_KMAX][ld] pivot rows (current leaving-row values, before /p)
-    double *F;               // [rows][SX_KMAX] row factors -(a_ie / p), slot s at sx_fslot(s)
+    double *F;               // row factors -(a_ie / p), F[sx_fidx(i, s)]
     PivRec *recs;            // [SX_KMAX]
     unsigned long long *PM;  // [rows] (batch id << 32) | slots < SX_HMAX where the row left the basis
     unsigned long long *PM2; // [rows] the same for slots SX_HMAX + b (bit b): the second stage

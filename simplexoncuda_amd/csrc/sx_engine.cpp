@@ -688,12 +688,12 @@ class Engine {
             }
             SX_HIP(hipMemcpy(x.slot_send, init.data(), sizeof(double) * init.size(), hipMemcpyHostToDevice));
         }
-        x.F = dalloc<double>(rows_alloc * SX_KMAX);
+        x.F = dalloc<double>(round_up(rows_alloc, 16) * SX_KMAX);  // (sx_fidx: whole 16-row strips)
         x.recs = dalloc<PivRec>(SX_KMAX);
         x.PM = dalloc<unsigned long long>(rows_alloc);
         x.PM2 = dalloc<unsigned long long>(rows_alloc);
         SX_HIP(hipMemsetAsync(x.U, 0, (size_t)SX_KMAX * ld * sizeof(double), x.s));
-        SX_HIP(hipMemsetAsync(x.F, 0, rows_alloc * SX_KMAX * sizeof(double), x.s));
+        SX_HIP(hipMemsetAsync(x.F, 0, round_up(rows_alloc, 16) * SX_KMAX * sizeof(double), x.s));
         SX_HIP(hipMemsetAsync(x.recs, 0, SX_KMAX * sizeof(PivRec), x.s));
         SX_HIP(hipMemsetAsync(x.PM, 0, rows_alloc * sizeof(unsigned long long), x.s));
         SX_HIP(hipMemsetAsync(x.PM2, 0, rows_alloc * sizeof(unsigned long long), x.s));
@@ -1036,8 +1036,11 @@ class Engine {
         c.batch = batch;
         c.rows_per_block = g_cfg.update_rows > 0 ? std::min(g_cfg.update_rows, 4) : (batch > 16 ? 4 : 2);
         c.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : 1;
-        // (a two-stage batch: the matrix-core sweep, the only one holding SX_KMAX slots)
-        c.mfma = batch > SX_HMAX ? 1 : (g_cfg.sweep_mfma >= 0 ? g_cfg.sweep_mfma : 0);
+        // (a two-stage batch: the matrix-core sweep, the only one holding SX_KMAX slots; one stage:
+        // the matrix cores too by default -- with the strip-major factors the vector sweep's
+        // per-row factor loads are scalar loads 128 B apart, config 2/3/5 no faster on the vector
+        // units, profiles/r03_onestage_mfma_ab.txt)
+        c.mfma = batch > SX_HMAX ? 1 : (g_cfg.sweep_mfma >= 0 ? g_cfg.sweep_mfma : 1);
         // peer ranks read leaving rows straight from this tableau (system-scope loads over
         // xGMI): its stores must write through to memory, not stay dirty in an L2 of this device
         if (p2p && (rccl || multidev) && c.sc1 != 1 && c.sc1 != 2) c.sc1 = 1;
@@ -1047,14 +1050,13 @@ class Engine {
     // pivots per sweep: the configured batch (1 while tracing every pivot); two stages (SX_KMAX)
     // only in one shard's fused batch -- the per-pivot kernels, the vector sweep and the
     // multi-rank batch hold one stage (run_phase caps it again when the batch is not fused)
-    // Default: two stages when the tableau has >= 8192 rows -- the second stage's longer chains
-    // (+1 to +1.4 us per pivot, the first stage's 32 pending pivots applied on the fly) cost
-    // less than the sweep they save there (config 5: 27.3 -> 16.5 us of sweep per pivot, 24.0k
-    // -> 32.1k pivots/s), not at 4096 rows (config 3: 73.4k vs 72.0k pivots/s;
-    // profiles/r03_two_stage_chain_ab.txt)
+    // Default: two stages when the tableau has >= 4096 rows -- the second stage's longer chains
+    // (+0.7 to +1.4 us per pivot, the first stage's 32 pending pivots applied on the fly) cost
+    // less than the sweep they save there (config 5: 27.6 -> 15.4 us of sweep per pivot, 23.7k
+    // -> 33.4k pivots/s; config 3: 71.6k -> 72.9k; profiles/r03_flayout_ab.txt)
     int batch_size() const {
         if (on_pivot) return 1;
-        const int want = g_cfg.batch > 0 ? g_cfg.batch : (m >= 8192 ? SX_KMAX : SX_HMAX);
+        const int want = g_cfg.batch > 0 ? g_cfg.batch : (m >= 4096 ? SX_KMAX : SX_HMAX);
         const int cap = (!xchg && sh.size() == 1 && g_cfg.fused != 0) ? SX_KMAX : SX_HMAX;
         return std::max(1, std::min(want, cap));
     }
@@ -2157,7 +2159,7 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     sx_crt_seeds(seed, 0, sd);
     double *T = dalloc<double>((size_t)rows * ld);
     double *U = dalloc<double>((size_t)SX_KMAX * ld);
-    double *F = dalloc<double>((size_t)rows * SX_KMAX);
+    double *F = dalloc<double>(round_up((size_t)rows, 16) * SX_KMAX);
     PivRec *recs = dalloc<PivRec>(SX_KMAX);
     unsigned long long *PM = dalloc<unsigned long long>(rows);
     unsigned long long *PM2 = dalloc<unsigned long long>(rows);
@@ -2173,7 +2175,7 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     (void)hipFree(b_dev);
     SX_HIP(hipMemsetAsync(U, 0, sizeof(double) * SX_KMAX * ld, s));
     for (int k = 0; k < pivots; ++k) sx_launch_gen_vector(sd[1] + 7919u * (unsigned)k, 0, cols, lo, hi, U + k * ld, s);
-    sx_launch_gen_vector(sd[1] ^ 0x9e3779b9u, 0, rows * SX_KMAX, -1, 1, F, s);
+    sx_launch_gen_vector(sd[1] ^ 0x9e3779b9u, 0, (int)(round_up((size_t)rows, 16) * SX_KMAX), -1, 1, F, s);
     const unsigned B = 1;
     std::vector<PivRec> rc(SX_KMAX);
     std::vector<unsigned long long> pm((size_t)rows, 0ull), pm2((size_t)rows, 0ull);
@@ -2208,7 +2210,7 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     cfg.batch = pivots;
     cfg.rows_per_block = g_cfg.update_rows > 0 ? std::min(g_cfg.update_rows, 4) : (pivots > 16 ? 4 : 2);
     cfg.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : 1;  // (as sweep_cfg: write-through at every size)
-    cfg.mfma = pivots > SX_HMAX ? 1 : (g_cfg.sweep_mfma >= 0 ? g_cfg.sweep_mfma : 0);
+    cfg.mfma = pivots > SX_HMAX ? 1 : (g_cfg.sweep_mfma >= 0 ? g_cfg.sweep_mfma : 1);
     long long sweeps = 0;
     auto one = [&]() { sx_launch_sweep(T, rows, 0, ld, btl, cols, nullptr, 0, pd, st, (int)(sweeps & 1), cfg, s); };
     for (int w = 0; w < warmup; ++w, ++sweeps) one();

@@ -246,7 +246,7 @@ __device__ __forceinline__ unsigned stage_row(const double *__restrict__ F, cons
                                               double *sf, double *sp) {
     const int t = threadIdx.x;
     if (t < q) {
-        sf[t] = F[(size_t)rl * SX_KMAX + sx_fslot(t)];
+        sf[t] = F[sx_fidx(rl, t)];
         sp[t] = recs[t].p;
     }
     __syncthreads();
@@ -328,11 +328,10 @@ __global__ __launch_bounds__(512) void k_ratio_select(const double *__restrict__
     }
     __syncthreads();
     if (li < rows) {
-        const double *Fr = F + (size_t)li * SX_KMAX;
         for (int s0 = 0; s0 < q; s0 += 8) {
             double f[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) f[k] = Fr[sx_fslot(s0 + k)];  // s0 + k < SX_KMAX
+            for (int k = 0; k < 8; ++k) f[k] = F[sx_fidx(li, s0 + k)];  // s0 + k < SX_KMAX
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const int s = s0 + k;
@@ -564,7 +563,7 @@ __global__ __launch_bounds__(256) void k_pivot_row(const double *__restrict__ T,
     const double p = x[0], u0 = x[1], ua = x[2], ub = x[3];
     if ((int)blockIdx.x >= B1) {
         const int i = ((int)blockIdx.x - B1) * 256 + (int)threadIdx.x;
-        if (i < rows) F[(size_t)i * SX_KMAX + sx_fslot(q)] = -colE[i] / p;
+        if (i < rows) F[sx_fidx(i, q)] = -colE[i] / p;
         if (i == rl) {
             const unsigned long long w = PM[rl];
             PM[rl] = (((unsigned)(w >> 32) == B) ? w : ((unsigned long long)B << 32)) | (1ull << q);
@@ -1365,7 +1364,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 const double f = -a / p;
                 s_hist[qq * SX_TILE + t] = f;
                 if (liveA) {
-                    F[(size_t)li * SX_KMAX + sx_fslot(q)] = f;
+                    F[sx_fidx(li, q)] = f;
                     if (li == r) {
                         b = b / p;
                         bits |= 1u << qq;
@@ -1415,7 +1414,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     // drained at the stage switch), loaded while the record is polled
                     u64 fr1 = 0ull;
                     if (hb && t < SX_HMAX)
-                        fr1 = ld_sc1(reinterpret_cast<const u64 *>(F + (size_t)(r >= 0 ? r : 0) * SX_KMAX + sx_fslot(t)));
+                        fr1 = ld_sc1(reinterpret_cast<const u64 *>(F + sx_fidx(r >= 0 ? r : 0, t)));
                     const int ok = poll_wave(ga + (size_t)wt * SX_GA_STRIDE + kRD, (kRF - kRD) + 2 * qq,
                                              [](int k) { return k; }, tag, s_g, &ch->abort_w, 20000000ull,
                                              (unsigned *)nullptr);
@@ -1788,7 +1787,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 const double f = -a / p;
                 s_hist[q * SX_TILE + t] = f;
                 if (liveA) {
-                    F[(size_t)li * SX_KMAX + sx_fslot(q)] = f;
+                    F[sx_fidx(li, q)] = f;
                     if (row0 + li == r) {
                         b = b / p;
                         bits |= 1u << q;
@@ -2142,10 +2141,9 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, T
             // (1668 vs 851 us at config 5 with 20-pivot batches, profiles/r02_sweep_partial_batch.txt).
             // Padding slots >= cnt with f = -0.0 (fma(-0, +0, y) = y exactly) instead cost every
             // full sweep 40 % (1218 vs 851 us): 32 scalar selects per row behind spilled masks.
-            const double *Fr = F + (size_t)i * SX_KMAX;
             double f[KT];
 #pragma unroll
-            for (int s = 0; s < KT; ++s) f[s] = Fr[sx_fslot(s)];
+            for (int s = 0; s < KT; ++s) f[s] = F[sx_fidx(i, s)];
             const unsigned bits = pend_bits(PM, i, B, mask);
             double2 y = x[k];
             if (bits == 0u && cnt == KT) {  // a full batch, no leaving row: no per-slot branch
@@ -2190,7 +2188,7 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, T
 // (tools/mfma_f64_probe.hip: every element equals fma(a3, b3, fma(a2, b2, fma(a1, b1,
 // fma(a0, b0, c)))) on MI355X), so SX_KMAX / 4 MFMAs per tile are the batch's updates in the
 // reference's order (solver.cu:34-46).  Operands of step k (slots 4k .. 4k+3):
-//   A (16 rows x 4 slots)     lane l = F[r0 + l % 16][4k + l / 16]   (sx_fslot: 8 contiguous per lane)
+//   A (16 rows x 4 slots)     lane l = F[r0 + l % 16][4k + l / 16]   (sx_fidx: 64 consecutive doubles)
 //   B (4 slots x 16 columns)  lane l = U[4k + l / 16][col(l % 16)]
 //   C / D                     lane l, register v = T[r0 + l / 16 + 4v][col(l % 16)]
 // Two tiles share each lane's 16-byte access (tile X the even column 2c, tile Y the odd 2c + 1),
@@ -2284,13 +2282,11 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
                 }
             double ff[NKB];
             {
-                const double *Fr = F + (size_t)(fr < rows ? fr : r0) * SX_KMAX + rg * (SX_KMAX / 4);
+                // (lane l of step kb: F[sx_fidx(r0 + l % 16, 4 kb + l / 16)] = strip base + 64 kb + l;
+                // the strip's rows past the end hold stale factors of rows that are not stored)
+                const double *Fs = F + sx_fidx(r0, 0) + l;
 #pragma unroll
-                for (int kb = 0; kb < NKB; kb += 2) {
-                    const double2 v = *reinterpret_cast<const double2 *>(Fr + kb);
-                    ff[kb] = v.x;
-                    ff[kb + 1] = v.y;
-                }
+                for (int kb = 0; kb < NKB; ++kb) ff[kb] = Fs[64 * kb];
             }
             const int frc = fr < rows ? fr : r0;
             const unsigned long long pm1 = PM[frc], pm2 = PM2[frc];
@@ -2359,7 +2355,6 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
         const unsigned long long bits = (unsigned long long)pend_bits(PM, r, B, mask) |
                                         ((unsigned long long)(mask2 ? pend_bits(PM2, r, B, mask2) : 0u) << SX_HMAX);
         if (bits == 0ull || (int)__builtin_ctzll(bits) != s) continue;  // (not its first slot)
-        const double *Fr = F + (size_t)r * SX_KMAX;
         double x = j < Ns ? Tr[(size_t)r * ldr + cr + l] : 0.0;
         // (the column's pivot-row values 16 slots at a time: few registers, loads only here)
         for (int c1 = 0; c1 < cnt; c1 += 16) {
@@ -2373,7 +2368,7 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
                     if ((bits >> sl) & 1ull)
                         x = x / recs[sl].p;
                     else
-                        x = fma(Fr[sx_fslot(sl)], uu[k], x);
+                        x = fma(F[sx_fidx(r, sl)], uu[k], x);
                 }
             }
         }

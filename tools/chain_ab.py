@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
-PIVOTS = {"config5": 640, "config4": 1280, "config3": 3200, "config2": 1600}
+PIVOTS = {"config5": 640, "config4": 1280, "config3": 3200, "config2": 1600}  # (timed, after 128)
 
 
 def stamps_summary(s, k=32, nb=6):
