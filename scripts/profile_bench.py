@@ -1,7 +1,7 @@
 """Summarise a scripts/profile.sh run of the driver's bench command into profiles/.
 
-The bench runs its primary workload first: `warmup` + `steps` steps, one sweep (k_sweep)
-each, so the first warmup+steps k_sweep dispatches of the trace are the primary workload's
+The bench runs its primary workload first: `warmup` + `steps` steps, one sweep (k_msweep or
+k_sweep) each, so the first warmup+steps k_sweep dispatches of the trace are the primary workload's
 and the last `steps` of those are its timed sweeps -- the ones the bench line's roofline
 averages with HIP events.  Outputs:
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary of the command
@@ -22,12 +22,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def sweep_rows(path, counter=None):
-    """k_sweep dispatches in dispatch order: (dispatch id, name, value) -- value = duration
+    """sweep dispatches (k_msweep / k_sweep) in dispatch order: (dispatch id, name, value) -- value = duration
     in ns (trace) or the counter's value (PMC)."""
     out = []
     with open(path) as f:
         for r in csv.DictReader(f):
-            if "k_sweep" not in r["Kernel_Name"]:
+            if "k_sweep" not in r["Kernel_Name"] and "k_msweep" not in r["Kernel_Name"]:
                 continue
             if counter is None:
                 v = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
@@ -59,7 +59,7 @@ def main():
            "avg_ns": sum(v for _, _, v in timed) / max(len(timed), 1),
            "min_ns": min((v for _, _, v in timed), default=None),
            "max_ns": max((v for _, _, v in timed), default=None),
-           "selection": f"k_sweep dispatches {warmup}..{warmup + steps - 1} in dispatch order: the primary "
+           "selection": f"sweep dispatches {warmup}..{warmup + steps - 1} in dispatch order: the primary "
                         "workload's timed sweeps"}
     pmc = {}
     for c in ("FETCH_SIZE", "WRITE_SIZE"):

@@ -12,10 +12,11 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 
-def run(sx, n, m, seed, k, W, p2p, force=0):
+def run(sx, n, m, seed, k, W, p2p, force=0, batch=0):
     sx.set_virtual_ranks(W)
     sx.set_p2p(p2p)
     sx.set_force_exchange(force)
+    sx.set_batch(batch)
     try:
         s = sx.Session(generated=(n, m, seed, 1, 100))
         s.pivots(64)
@@ -25,6 +26,7 @@ def run(sx, n, m, seed, k, W, p2p, force=0):
         sx.set_virtual_ranks(1)
         sx.set_p2p(-1)
         sx.set_force_exchange(0)
+        sx.set_batch(0)
     return t
 
 
@@ -35,11 +37,15 @@ def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "config3"
     k = int(sys.argv[2]) if len(sys.argv) > 2 else 640
     n, m, seed = bench.CONFIGS[cfg]
-    for W, p2p, force in [(1, -1, 0), (1, 1, 1), (2, 0, 0), (2, 1, 0), (3, 1, 0), (4, 1, 0), (8, 1, 0)]:
-        t = run(sx, n, m, seed, k, W, p2p, force)
-        print(f"{cfg} W={W} p2p={p2p} force_exchange={force}: {t.pivots / t.wall_ms * 1e3:9.1f} pivots/s "
-              f"({t.wall_ms * 1e3 / max(t.pivots, 1):7.2f} us/pivot, sweep {t.update_ms * 1e3 / max(t.update_launches, 1):8.1f} us)"
-              f" status {t.status}", flush=True)
+    for W, p2p, force, batch in [(1, -1, 0, 0), (1, -1, 0, 32), (1, 1, 1, 32), (2, 0, 0, 0), (2, 1, 0, 0),
+                                 (3, 1, 0, 0), (4, 1, 0, 0), (8, 1, 0, 0)]:
+        t = run(sx, n, m, seed, k, W, p2p, force, batch)
+        per = t.wall_ms * 1e3 / max(t.pivots, 1)
+        sw = t.update_ms * 1e3 / max(t.pivots, 1)  # (shard 0's sweeps)
+        print(f"{cfg} W={W} p2p={p2p} force_exchange={force} batch={batch or 'default'}: "
+              f"{t.pivots / t.wall_ms * 1e3:9.1f} pivots/s ({per:7.2f} us/pivot = shard-0 sweep {sw:6.2f} + rest "
+              f"{per - sw:6.2f}; sweep {t.update_ms * 1e3 / max(t.update_launches, 1):8.1f} us) status {t.status}",
+              flush=True)
 
 
 if __name__ == "__main__":
