@@ -31,7 +31,7 @@ void simplex_set_store_sc1(int mode);
  * -1 auto (matrix cores), 0 vector sweep (batches of at most 32), 1 matrix-core sweep */
 void simplex_set_sweep_mfma(int mode);
 /* pivots per tableau sweep (1..64; 0 = default: 64 in one shard's fused batch of a tableau with
- * >= 8192 rows -- two stages of 32, applied by the matrix-core sweep -- else 32; more than 32
+ * >= 4096 rows -- two stages of 32, applied by the matrix-core sweep -- else 32; more than 32
  * only in one shard's fused batch): the pivots of a batch are selected on the
  * current values (pending pivots applied on the fly) and then applied to the tableau in one
  * sweep -- the same IEEE operations in the same order as one sweep per pivot */

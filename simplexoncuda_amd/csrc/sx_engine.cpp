@@ -1050,15 +1050,13 @@ class Engine {
     // pivots per sweep: the configured batch (1 while tracing every pivot); two stages (SX_KMAX)
     // only in one shard's fused batch -- the per-pivot kernels, the vector sweep and the
     // multi-rank batch hold one stage (run_phase caps it again when the batch is not fused)
-    // Default: two stages when the tableau has >= 8192 rows -- the second stage's longer chains
+    // Default: two stages when the tableau has >= 4096 rows -- the second stage's longer chains
     // (+0.7 to +1.4 us per pivot, the first stage's 32 pending pivots applied on the fly) cost
-    // less than the sweep they save there (config 5: 27.6 -> 15.4 us of sweep per pivot, 23.7k
-    // -> 33.4k pivots/s).  At 4096 rows the gain is within box-to-box noise (config 3: 71.6k ->
-    // 72.9k, one box) while the 64-slot sweep moves its 4096 rows at half the one-stage sweep's
-    // rate (profiles/r03_flayout_ab.txt, r03_sweep_kernels_ab_flayout.txt)
+    // less than the sweep they save (same box: config 5 27.6 -> 15.4 us of sweep per pivot,
+    // 23.7k -> 33.4k pivots/s; config 3 3.80 -> 2.88 us, 71.6k -> 72.9k; profiles/r03_flayout_ab.txt)
     int batch_size() const {
         if (on_pivot) return 1;
-        const int want = g_cfg.batch > 0 ? g_cfg.batch : (m >= 8192 ? SX_KMAX : SX_HMAX);
+        const int want = g_cfg.batch > 0 ? g_cfg.batch : (m >= 4096 ? SX_KMAX : SX_HMAX);
         const int cap = (!xchg && sh.size() == 1 && g_cfg.fused != 0) ? SX_KMAX : SX_HMAX;
         return std::max(1, std::min(want, cap));
     }

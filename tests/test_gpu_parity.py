@@ -207,7 +207,7 @@ def test_session_pivots(gpu):
 
 
 def test_session_two_stage_batches(gpu):
-    """64-pivot batches on one shard (the default from 8192 rows): one sweep per batch"""
+    """64-pivot batches on one shard (the default from 4096 rows): one sweep per batch"""
     p = sx.generateRandomProblem(2048, 1024, 205824, 1, 100)
     sx.set_batch(64)
     try:
@@ -221,7 +221,7 @@ def test_session_two_stage_batches(gpu):
         s.close()
     finally:
         sx.set_batch(0)
-    s2 = sx.Session(generated=(256, 8192, 256 * 100 + 8192, 1, 100))
+    s2 = sx.Session(generated=(256, 4096, 256 * 100 + 4096, 1, 100))
     assert s2.batch() == 64
     s2.close()
 
@@ -644,7 +644,7 @@ def test_slack_compaction_generated_session_width(gpu):
     n, m = 512, 2048
     s = sx.Session(generated=(n, m, n * 100 + m, 1, 100))
     K = s.batch()
-    assert K == 32  # (the default below 8192 rows)
+    assert K == 32  # (the default below 4096 rows)
     t = s.pivots(96, time_updates=1)
     active = s.active_slacks()
     s.close()
