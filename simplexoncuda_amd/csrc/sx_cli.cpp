@@ -9,6 +9,11 @@
 // Messages, status handling and the solution file format follow main.cu:14-115.  Paths: the
 // solution goes to $SIMPLEX_SOLUTION (default "solution.txt"), seed files and TIMER CSVs to
 // $SIMPLEX_DATA_DIR (default "."); -t enables the TIMER CSV (benchmark_<n>_<m>.txt) there.
+// Extension options before the mode:
+//   --gpus N              N GPUs (devices 0..N-1) for the solve, as SIMPLEX_GPUS=N
+//   --pivot-budget K      at most K pivots per phase (twoPhaseMethodEx; off = parity mode)
+//   --rand msvc|glibc     the CRT rand() of the generator's seeds (default msvc: the published
+//                         pivot counts were produced by MSVC builds)
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -27,9 +32,27 @@ static std::string data_dir() {
     return e ? e : ".";
 }
 
+static int g_rand_kind = 0;             // --rand: 0 MSVC, 1 glibc
+static long long g_pivot_budget = -1;   // --pivot-budget
+
+static problem_t *generate(int vars, int constraints, unsigned seed, int lo, int hi) {
+    return g_rand_kind ? simplex_generate_problem_ex(vars, constraints, seed, lo, hi, g_rand_kind)
+                       : generateRandomProblem(vars, constraints, seed, lo, hi);
+}
+
 static problem_t *random_input(int vars, int constraints, int seed) {
     printf("Generating random problem with %d variables, %d contraints with seed: %d\n", vars, constraints, seed);
-    return generateRandomProblem(vars, constraints, (unsigned)seed, MIN_V, MAX_V);
+    return generate(vars, constraints, (unsigned)seed, MIN_V, MAX_V);
+}
+
+// twoPhaseMethod, or twoPhaseMethodEx under a pivot budget
+static int solve_problem(problem_t *p, double *solution, double *optimalValue) {
+    if (g_pivot_budget < 0) return twoPhaseMethod(p, solution, optimalValue);
+    long long piv[2] = {0, 0};
+    const int st = twoPhaseMethodEx(p, solution, optimalValue, nullptr, piv, g_pivot_budget);
+    if (st == SIMPLEX_PIVOT_CAP) printf("\nPivot budget of %lld reached (phase pivots %lld + %lld)\n", g_pivot_budget,
+                                        piv[0], piv[1]);
+    return st;
 }
 
 static void save_random_input(int vars, int constraints, int seed) {
@@ -44,6 +67,35 @@ static void save_random_input(int vars, int constraints, int seed) {
 
 int main(int argc, const char *argv[]) {
     printf("Starting...\n");
+    // extension options, then the reference's arguments
+    while (argc > 2 && strncmp(argv[1], "--", 2) == 0) {
+        if (strcmp(argv[1], "--gpus") == 0) {
+            const int n = atoi(argv[2]);
+            if (n < 1 || n > 64) {
+                fprintf(stderr, "--gpus: expected 1..64\n");
+                exit(-1);
+            }
+            int devs[64];
+            for (int k = 0; k < n; ++k) devs[k] = k;
+            simplex_set_gpus(devs, n);
+        } else if (strcmp(argv[1], "--pivot-budget") == 0) {
+            g_pivot_budget = atoll(argv[2]);
+        } else if (strcmp(argv[1], "--rand") == 0) {
+            if (strcmp(argv[2], "msvc") == 0) {
+                g_rand_kind = 0;
+            } else if (strcmp(argv[2], "glibc") == 0) {
+                g_rand_kind = 1;
+            } else {
+                fprintf(stderr, "--rand: expected msvc or glibc\n");
+                exit(-1);
+            }
+        } else {
+            fprintf(stderr, "Unknown option %s\n", argv[1]);
+            exit(-1);
+        }
+        argc -= 2;
+        argv += 2;
+    }
     if (argc < 2) {
         fprintf(stderr, "Not enough arguments!\n");
         exit(-1);
@@ -64,7 +116,12 @@ int main(int argc, const char *argv[]) {
     } else if (strcmp(argv[1], "-rf") == 0 && argc > 2) {
         printf("Reading seed from file\n");
         FILE *file = openFile(argv[2], "r");
-        problem = readRandomProblemFromFile(file);
+        if (g_rand_kind) {  // (the seed file "n m seed min max", problem.cu:128-139, under --rand glibc)
+            int n = 0, m = 0, seed = 0, lo = 0, hi = 0;
+            if (fscanf(file, "%d %d %d %d %d", &n, &m, &seed, &lo, &hi) == 5) problem = generate(n, m, (unsigned)seed, lo, hi);
+        } else {
+            problem = readRandomProblemFromFile(file);
+        }
         fclose(file);
     } else if (strcmp(argv[1], "-t") == 0) {
         enableBenchmarkMode();
@@ -76,10 +133,10 @@ int main(int argc, const char *argv[]) {
             for (int vars = 256; vars <= max_side; vars *= 2) {
                 fprintf(stdout, "\nCurrent matrix: %d*%d\n\n", vars, constraints);
                 const int seed = vars * 100 + constraints + (vars == 1024 && constraints == 8192 ? 1 : 0);
-                problem_t *p = generateRandomProblem(vars, constraints, (unsigned)seed, +1, +100);
+                problem_t *p = generate(vars, constraints, (unsigned)seed, +1, +100);
                 double *solution = (double *)malloc(sizeof(double) * p->vars);
                 double optimalValue = 0;
-                twoPhaseMethod(p, solution, &optimalValue);
+                solve_problem(p, solution, &optimalValue);
                 freeProblem(p);
                 free(p);
                 free(solution);
@@ -101,7 +158,7 @@ int main(int argc, const char *argv[]) {
     const char *sol_path = getenv("SIMPLEX_SOLUTION") ? getenv("SIMPLEX_SOLUTION") : "solution.txt";
     FILE *fileSolution = openFile(sol_path, "w");
     printf("Resolving....\n");
-    switch (twoPhaseMethod(problem, solution, &optimalValue)) {
+    switch (solve_problem(problem, solution, &optimalValue)) {
     case INFEASIBLE:
         printf("\nProblem INFEASIBLE!\n");
         break;
@@ -110,6 +167,8 @@ int main(int argc, const char *argv[]) {
         break;
     case DEGENERATE:
         printf("\nProblem DEGENERATE!\n");
+        break;
+    case SIMPLEX_PIVOT_CAP:
         break;
     default:
         printf("\nProblem solved!\n");

@@ -83,3 +83,41 @@ def test_debug_trace(gpu, tmp_path):
     assert "Tableu nella situazione iniziale" in out and "Tableu dopo seconda esecuzione del solver" in out
     last = out[out.rindex("Tableu dopo seconda esecuzione del solver"):]
     assert "|\t 64.00000000000" in last and "Base\n3\t0\t" in last
+
+
+def test_cli_rejects_bad_options(tmp_path):
+    r = run(["--rand", "bsd", "-r", "3", "3", "1"], tmp_path)
+    assert r.returncode == 255 and "--rand: expected msvc or glibc" in r.stderr
+    r = run(["--frobnicate", "1", "-r", "3", "3", "1"], tmp_path)
+    assert r.returncode == 255 and "Unknown option --frobnicate" in r.stderr
+    r = run(["--gpus", "0", "-r", "3", "3", "1"], tmp_path)
+    assert r.returncode == 255 and "--gpus: expected 1..64" in r.stderr
+
+
+@pytest.mark.gpu
+def test_cli_pivot_budget(gpu, tmp_path):
+    """--pivot-budget K: twoPhaseMethodEx's per-phase cap (SIMPLEX_PIVOT_CAP), no solution written"""
+    r = run(["--pivot-budget", "3", "-r", "300", "200", "5"], tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Pivot budget of 3 reached (phase pivots 3 + 0)" in r.stdout
+    assert "Problem solved!" not in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["msvc", "glibc"])
+def test_cli_rand_and_gpus(gpu, tmp_path, kind):
+    """--rand picks the generator's rand(); --gpus 1 is the default device set. The CLI's
+    objective equals the library's on the same generated instance"""
+    import simplexoncuda_amd as sx
+    r = run(["--gpus", "1", "--rand", kind, "-r", "60", "40", "99"], tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr
+    p = sx.generateRandomProblem(60, 40, 99, -100, 100, rand_kind=sx.RAND_GLIBC if kind == "glibc" else sx.RAND_MSVC)
+    try:
+        st, _, opt = sx.twoPhaseMethod(p)
+    finally:
+        p.close()
+    if st == sx.FEASIBLE:
+        assert "Problem solved!" in r.stdout
+        assert (tmp_path / "solution.txt").read_text().endswith("Optimal value: %f\n" % opt)
+    else:
+        assert "Problem solved!" not in r.stdout

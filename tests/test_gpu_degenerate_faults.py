@@ -148,14 +148,17 @@ def test_hang_recovery_multirank(gpu, W):
 
 
 # ------------------------------------------------------------------ batch ids wrap
-@pytest.mark.parametrize("mode", ["fused", "unfused", "p2p2"])
+@pytest.mark.parametrize("mode", ["fused", "fused64", "unfused", "p2p2"])
 def test_batch_id_wrap(gpu, mode):
-    """the solve starts 20 batch ids before the wrap (ids 1..32767) and crosses it"""
+    """the solve starts 20 batch ids before the wrap (ids 1..32767) and crosses it (fused64:
+    two-stage batches, whose second-stage leaving slots live in PM2)"""
     lib = sx.load()
     p = sx.generateRandomProblem(2048, 1024, 205824, 1, 100)
     lib.simplex_set_first_batch_id(32767 - 20)
     if mode == "unfused":
         sx.set_fused(0)
+    if mode == "fused64":
+        sx.set_batch(64)
     if mode == "p2p2":
         sx.set_virtual_ranks(2)
         sx.set_p2p(1)
@@ -163,6 +166,7 @@ def test_batch_id_wrap(gpu, mode):
         got = solve_both(*p.arrays())
     finally:
         lib.simplex_set_first_batch_id(1)
+        sx.set_batch(0)
         sx.set_fused(-1)
         sx.set_p2p(-1)
         sx.set_virtual_ranks(1)

@@ -244,14 +244,25 @@ def _pivots_with(cfg, T, d, base, k):
 
 @pytest.mark.parametrize("fused", [-1, 0])
 @pytest.mark.parametrize("batch", [1, 2, 3, 7, 16, 17, 32])
-@pytest.mark.parametrize("rb", [1, 2, 4])
-def test_batched_sweep_bit_exact(gpu, batch, rb, fused):
+def test_batched_sweep_bit_exact(gpu, batch, fused):
     """k pivots with the tableau swept every `batch` pivots (pending pivots applied on the fly
     to the columns and rows the decisions read): the same bits as the oracle's pivot-by-pivot
-    updates, for every register-slot variant of the sweep and a partial last batch; each batch
-    as one resident launch (fused) or as two launches per pivot"""
+    updates, with a partial last batch; each batch as one resident launch (fused) or as two
+    launches per pivot (the default sweep: the matrix cores)"""
     T, d, base = _phase1_state(333, 1025, 7)
-    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "rb": rb, "fused": fused}, T, d, base, 45)
+    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "fused": fused}, T, d, base, 45)
+    oracle.solve(T, d, base, max_pivots=45)
+    assert done == 45
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+@pytest.mark.parametrize("batch", [1, 3, 7, 16, 17])
+@pytest.mark.parametrize("rb", [1, 4])
+def test_vector_sweep_slots_bit_exact(gpu, batch, rb):
+    """the vector sweep (simplex_set_sweep_mfma(0)) at every register-slot variant (1, 4, 8, 16,
+    32 slots) and row step, with a partial last batch"""
+    T, d, base = _phase1_state(333, 1025, 7)
+    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "rb": rb, "mfma": 0}, T, d, base, 45)
     oracle.solve(T, d, base, max_pivots=45)
     assert done == 45
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
@@ -261,10 +272,10 @@ def test_batched_sweep_bit_exact(gpu, batch, rb, fused):
 @pytest.mark.parametrize("rb", [1, 2, 4])
 @pytest.mark.parametrize("sc1", [0, 1])
 def test_large_batch_sweeps_bit_exact(gpu, batch, rb, sc1):
-    """batches above 16 pivots (32 register slots per column in the sweep), every row step and
-    store flavour, with a partial last batch"""
+    """the vector sweep's 32-slot variant (batches above 16 pivots), every row step and store
+    flavour, with a partial last batch"""
     T, d, base = _phase1_state(333, 1025, 7)
-    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "rb": rb, "sc1": sc1}, T, d, base, 70)
+    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "rb": rb, "sc1": sc1, "mfma": 0}, T, d, base, 70)
     oracle.solve(T, d, base, max_pivots=70)
     assert done == 70
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
@@ -272,7 +283,7 @@ def test_large_batch_sweeps_bit_exact(gpu, batch, rb, sc1):
 
 @pytest.mark.parametrize("mfma", [1, 0])
 @pytest.mark.parametrize("fused", [-1, 0])
-@pytest.mark.parametrize("batch", [1, 3, 5, 16, 31, 32])
+@pytest.mark.parametrize("batch", [5, 31])
 def test_matrix_core_sweep_bit_exact(gpu, batch, fused, mfma):
     """the sweep on the matrix cores (k_msweep: 4 slots per v_mfma_f64_16x16x4f64, partial
     batches padded, leaving rows recomputed on the vector units) against the vector sweep and the
