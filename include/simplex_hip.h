@@ -179,6 +179,11 @@ long long simplex_session_launch_log(simplex_session *s, long long *rows, double
  * 7 its pivot-row values, 4 its tile published, 5 ratio block 0 knows the next entering
  * variable; -1 when the fused path is not in use */
 int simplex_session_stamps(simplex_session *s, int k, unsigned long long *out);
+/* the same with every block's own stamps, blk[k][blocks][4] (ratio blocks first: starts the pivot,
+ * tile published, knows the next entering variable; objective blocks: knows the selection, has
+ * the details, tile published), copied when cap >= k * blocks * 4; returns the blocks (-1 as above) */
+int simplex_session_block_stamps(simplex_session *s, int k, unsigned long long *out, unsigned long long *blk,
+                                 long long cap);
 void simplex_session_close(simplex_session *s);
 
 /* ---- multi-process peer-memory test mode (no RCCL; e.g. 2 processes on one GPU) ----

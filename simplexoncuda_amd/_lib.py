@@ -137,6 +137,8 @@ SIGNATURES = {
     "simplex_session_launch_log": (ctypes.c_longlong, [ctypes.c_void_p, c_ll_p, c_double_p, ctypes.c_longlong]),
     "simplex_session_close": (None, [ctypes.c_void_p]),
     "simplex_session_stamps": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_ulonglong)]),
+    "simplex_session_block_stamps": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_ulonglong),
+                                                    ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_longlong]),
     "simplex_ipc_handles_size": (ctypes.c_int, []),
     "simplex_ipc_session_open": (ctypes.c_void_p, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_double_p,
                                                    ctypes.c_longlong, c_double_p, c_int_p, ctypes.c_char_p]),

@@ -208,6 +208,19 @@ class Session:
         rc = self._lib.simplex_session_stamps(self._h, k, out.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)))
         return out if rc == 0 else None
 
+    def block_stamps(self, k, blocks):
+        """Diagnostic: stamps(k) plus every block's own, (k, blocks, 4) uint64 (see
+        simplex_session_block_stamps); (None, None) when the fused path is not in use."""
+        out = np.zeros((k, 8), dtype=np.uint64)
+        blk = np.zeros((k, blocks, 4), dtype=np.uint64)
+        P = ctypes.POINTER(ctypes.c_ulonglong)
+        rc = self._lib.simplex_session_block_stamps(self._h, k, out.ctypes.data_as(P), blk.ctypes.data_as(P), blk.size)
+        if rc < 0:
+            return None, None
+        if rc != blocks:
+            raise RuntimeError(f"simplex_session_block_stamps: {rc} blocks, expected {blocks}")
+        return out, blk
+
     def objective(self):
         return self._lib.simplex_session_objective(self._h)
 

@@ -2053,11 +2053,19 @@ int simplex_session_batch(simplex_session *S) {
 }
 
 int simplex_session_stamps(simplex_session *S, int k, unsigned long long *out) {
-    // one fused batch of k pivots with in-kernel timestamps (diagnostic); out[k][8]
+    return simplex_session_block_stamps(S, k, out, nullptr, 0) < 0 ? -1 : 0;
+}
+
+int simplex_session_block_stamps(simplex_session *S, int k, unsigned long long *out, unsigned long long *blk,
+                                 long long cap) {
+    // one fused batch of k pivots with in-kernel timestamps (diagnostic); out[k][8], and
+    // blk[k][blocks][4] when it holds cap >= k * blocks * 4 entries; returns the blocks
     Engine &E = *S->E;
-    if (k < 1 || k > SX_KMAX || !E.fused_ok(k)) return -1;
-    unsigned long long *dev = dalloc<unsigned long long>((size_t)k * 8);
-    SX_HIP(hipMemsetAsync(dev, 0, sizeof(unsigned long long) * k * 8, E.s));
+    if (k < 1 || k > SX_KMAX || !E.fused_ok(k) || E.sh.size() != 1) return -1;
+    const size_t nb = (size_t)((E.sh[0].rows + SX_TILE - 1) / SX_TILE) + (size_t)((E.N - 1 + SX_TILE - 1) / SX_TILE);
+    const size_t total = (size_t)k * 8 + (size_t)k * nb * 4;
+    unsigned long long *dev = dalloc<unsigned long long>(total);
+    SX_HIP(hipMemsetAsync(dev, 0, sizeof(unsigned long long) * total, E.s));
     E.stamps = dev;
     E.enqueue_batch(k);
     E.stamps = nullptr;
@@ -2065,9 +2073,12 @@ int simplex_session_stamps(simplex_session *S, int k, unsigned long long *out) {
     E.gather_d();
     E.sync_all();
     SX_HIP(hipMemcpyAsync(out, dev, sizeof(unsigned long long) * k * 8, hipMemcpyDeviceToHost, E.s));
+    if (blk && cap >= (long long)((size_t)k * nb * 4))
+        SX_HIP(hipMemcpyAsync(blk, dev + (size_t)k * 8, sizeof(unsigned long long) * k * nb * 4, hipMemcpyDeviceToHost,
+                              E.s));
     SX_HIP(hipStreamSynchronize(E.s));
     (void)hipFree(dev);
-    return 0;
+    return (int)nb;
 }
 
 long long simplex_session_launch_log(simplex_session *S, long long *rows, double *update_us, long long cap) {

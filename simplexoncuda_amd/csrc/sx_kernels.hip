@@ -863,7 +863,7 @@ __device__ bool gather_tagged(const u64 *base, int n, OFF off, unsigned tag, uns
 // (k_batch: the RV..RF / OV..OU layouts below; k_batch_mr: v(2) pad(2) a(2) b(2) F(2 per slot) and
 // v(2) pad(2) U(2 per slot) inside the same strides)
 #define SX_GA_STRIDE (10 + 2 * SX_HMAX)  // ratio tile record, granules (one stage of history)
-#define SX_GB_STRIDE (8 + 2 * SX_HMAX)   // objective tile record, granules
+#define SX_GB_STRIDE (9 + 2 * SX_HMAX)   // objective tile record, granules
 __device__ __forceinline__ int rec2_a(int k) { return (k >> 1) * SX_GA_STRIDE + (k & 1); }
 // granules of all tile records
 __host__ __device__ __forceinline__ size_t sx_ga_size() { return (size_t)SX_TILE * SX_GA_STRIDE; }
@@ -1110,7 +1110,7 @@ __device__ void activate_block(int *__restrict__ perm, int *__restrict__ iperm, 
 //                     ratio side (NOT_ENDED, or FEASIBLE: the phase ended) | kRF F[winner][s < q]
 //   objective tile q  kOV v (payload: winner index) | kOP pivot p | kOB the pivot row's RHS | kOR
 //                     leaving row r | kOS status of the objective side (NOT_ENDED, UNBOUNDED,
-//                     NUMERIC_FAIL) | kOU U[s <= q][winner]
+//                     NUMERIC_FAIL) | kOM the winner's stored column (c.map) | kOU U[s <= q][winner]
 [[maybe_unused]] constexpr int kRV = 0;  // (the value granules come first: rec2_a / rec2_b index them)
 constexpr int kRD = 2;
 constexpr int kRA = 4;
@@ -1123,7 +1123,8 @@ constexpr int kOP = 2;
 constexpr int kOB = 4;
 constexpr int kOR = 6;
 constexpr int kOS = 7;
-constexpr int kOU = 8;
+constexpr int kOM = 8;
+constexpr int kOU = 9;  // (odd: a history value's low word at kOU + 2s, its high word after it)
 
 // K6: a whole batch of pivots in ONE resident launch (one shard).  Blocks [0, NA) own the
 // 512-row ratio tiles, blocks [NA, NA + NB) the 512-entry objective-row tiles.  Each block
@@ -1170,7 +1171,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
     __shared__ int s_last;
     // per-step results written by wave 0 before the step's one barrier (each step its own
     // words, so no wave still reading an earlier step's result can see them change)
-    __shared__ int s_sel_ok, s_sel_r, s_sel_any, s_det_ok, s_det_e, s_det_st, s_ent_ok, s_ent_e, s_ent_r, s_ent_st;
+    __shared__ int s_sel_ok, s_sel_r, s_sel_any, s_det_ok, s_det_e, s_det_st, s_ent_ok, s_ent_e, s_ent_r, s_ent_st, s_ent_m;
     __shared__ double s_det_dmin, s_ent_v, s_br, s_ent_p;
     __shared__ int s_welig[SX_TILE / 64];
     const int t = threadIdx.x;
@@ -1180,6 +1181,14 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
 #define SX_STAMP(k)                                                                           \
     do {                                                                                       \
         if (stamps && t == 0) stamps[(size_t)q * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+    // ... and every block's own, after the [K][8] block: [q][block][4] (ratio: compute start,
+    // publish, entering seen; objective: selection seen, details in, publish)
+#define SX_BSTAMP(k)                                                                                    \
+    do {                                                                                                \
+        if (stamps && t == 0)                                                                           \
+            stamps[(size_t)K * 8 + ((size_t)q * (NA + NB) + blockIdx.x) * 4 + (k)] =                    \
+                __builtin_amdgcn_s_memrealtime();                                                       \
     } while (0)
     // state at the start of the batch (written only by the last block to leave)
     const int status0 = st->status;
@@ -1197,6 +1206,8 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
         const int ia = tb * SX_TILE + t;
         const bool liveB = !isA && ia < L;
         const int mj = c.map(1 + (liveB ? ia : 0));
+        // (objective blocks: every column's stored position, for the record of the tile winner)
+        if (!isA) reinterpret_cast<int *>(s_a)[t] = mj;
         double b = liveA ? T[tl.idx(li, 0)] : 0.0;  // current RHS of the row
         unsigned bits = 0u;                            // slots of this stage where this row left the basis
         unsigned bits1 = 0u;                           // ... of the first stage (second stage)
@@ -1213,36 +1224,39 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
         // the entering column's stored value of this row: loaded as soon as the entering
         // variable is known, so the load overlaps the wait for its pending history
         double a_pre = liveA ? T[tl.idx(li, c.map(1 + (e >= 0 ? e : 0)))] : 0.0;
-        for (int q = 0; q < K; ++q) {
-            const unsigned tag = make_tag(B, q);
-            // ---- does the phase end here?  (the same decision in every block)
-            if (cap >= 0 && piv0 + q >= cap) {
-                status = SX_PIVOT_CAP;
-                break;
-            }
-            if (q == SX_HMAX) {
-                // second stage: this thread's first-stage history to registers, the LDS history
-                // reused.  The block's first-stage F / U stores are written back from its L2
-                // (every thread's stores acknowledged, then one agent-scope release: buffer_wbl2)
-                // before any second-stage record of the block, so a block that reads one of them
-                // with sc1 loads (the leaving row's F, the entering column's U) after that
-                // record sees them
+        // the stage switch at slot SX_HMAX: this thread's first-stage history to registers, the
+        // LDS history reused.  The block's first-stage F / U stores are written back from its L2
+        // (every thread's stores acknowledged, then one agent-scope release: buffer_wbl2) before
+        // any second-stage record of the block, so a block that reads one of them with sc1 loads
+        // (the leaving row's F, the entering column's U) after that record sees them
+        auto next_stage = [&]() {
 #pragma unroll
-                for (int s1 = 0; s1 < SX_HMAX; ++s1) h1[s1] = s_hist[s1 * SX_TILE + t];
-                bits1 = bits;
-                bits = 0u;
-                if (t < SX_HMAX) s_ue1[t] = s_ue[t];  // (U[s][e] of pivot SX_HMAX: its objective record)
-                drain();
-                __syncthreads();
-                if (t == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                __syncthreads();
-                hb = SX_HMAX;
-            }
-            const int qq = q - hb;  // slot within the stage
-            if (isA) {
+            for (int s1 = 0; s1 < SX_HMAX; ++s1) h1[s1] = s_hist[s1 * SX_TILE + t];
+            bits1 = bits;
+            bits = 0u;
+            if (t < SX_HMAX) s_ue1[t] = s_ue[t];  // (U[s][e] of pivot SX_HMAX: its objective record)
+            drain();
+            __syncthreads();
+            if (t == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __syncthreads();
+            hb = SX_HMAX;
+        };
+        // The two roles run separate loops (the same steps per pivot), so the compiler's memory
+        // counter waits on one role's path never cover the other role's loads.  Per pivot q: does
+        // the phase end here (the pivot cap: the same decision in every block), the stage switch.
+        if (isA) {
+            for (int q = 0; q < K; ++q) {
+                const unsigned tag = make_tag(B, q);
+                if (cap >= 0 && piv0 + q >= cap) {
+                    status = SX_PIVOT_CAP;
+                    break;
+                }
+                if (q == SX_HMAX) next_stage();
+                const int qq = q - hb;  // slot within the stage
                 const bool done = !(cmp_eps(dmin, 0.0) < 0);  // solver.cu:88: optimal
                 // ---- ratio tile: current entering column, ratios, tile winner
                 if (blockIdx.x == 0) SX_STAMP(0);
+                SX_BSTAMP(0);
                 double a1 = a_pre;
                 if (hb && !done) a1 = stage1_col(a1, h1, bits1, s_ue1, s_p);
                 const double a = done ? 0.0 : hist_col(a1, qq, bits, s_hist, s_ue, s_p + hb);
@@ -1301,6 +1315,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     }
                 }
                 if (blockIdx.x == 0) SX_STAMP(1);
+                SX_BSTAMP(1);
                 if (done) {
                     status = SX_FEASIBLE;
                     break;
@@ -1335,11 +1350,13 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                             s_br = gd(s_g[kOB - kOP], s_g[kOB - kOP + 1]);
                             s_ent_r = (int)s_g[kOR - kOP];
                             s_ent_st = (int)s_g[kOS - kOP];
+                            s_ent_m = (int)s_g[kOM - kOP];
                         }
                     }
                 }
                 __syncthreads();
                 if (blockIdx.x == 0) SX_STAMP(5);
+                SX_BSTAMP(2);
                 if (!s_ent_ok) {
                     aborted = true;
                     break;
@@ -1349,10 +1366,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     break;
                 }
                 // ---- this pivot's factor column and the rows' new RHS (solver.cu:34-46)
-                // the next entering column's stored value of this row: its load first (HBM latency),
-                // then this pivot's updates while it is in flight
                 const int enext = s_ent_e;
-                if (liveA) a_pre = T[tl.idx(li, c.map(1 + (enext >= 0 ? enext : 0)))];
                 const int r = s_ent_r;
                 const double p = s_ent_p, br = s_br;
                 if (t == 0) {
@@ -1368,9 +1382,9 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     if (li == r) {
                         b = b / p;
                         bits |= 1u << qq;
-                        unsigned long long *const P = hb ? PM2 : PM;
-                        const u64 w = P[li];
-                        P[li] = (((unsigned)(w >> 32) == B) ? w : ((u64)B << 32)) | (1ull << qq);
+                        // (the row's slots of this stage are `bits`: the word is written, not
+                        // read-modified, so no load waits behind the entering column's)
+                        (hb ? PM2 : PM)[li] = ((u64)B << 32) | bits;
                     } else {
                         b = fma(f, br, b);
                     }
@@ -1383,8 +1397,21 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 }
                 e = enext;
                 dmin = s_ent_v;
+                // the next entering column's stored value of this row (its stored position from the
+                // winner's record): issued after this pivot's stores, so no wait of the compiler's
+                // for a register reused above covers it; it is waited for in the next chain
+                if (liveA) a_pre = T[tl.idx(li, s_ent_m)];
                 __syncthreads();  // (s_p / s_ue of this step are read by the next pivot's chain)
-            } else {
+            }
+        } else {
+            for (int q = 0; q < K; ++q) {
+                const unsigned tag = make_tag(B, q);
+                if (cap >= 0 && piv0 + q >= cap) {
+                    status = SX_PIVOT_CAP;
+                    break;
+                }
+                if (q == SX_HMAX) next_stage();
+                const int qq = q - hb;  // slot within the stage
                 // ---- selection: pass 2 over the ratio tiles (wave 0 polls and runs the tree)
                 if (t < 64) {
                     const int ok = poll_wave(ga, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
@@ -1399,6 +1426,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 }
                 __syncthreads();
                 if (tb == 0) SX_STAMP(3);
+                SX_BSTAMP(0);
                 if (!s_sel_ok) {
                     aborted = true;
                     break;
@@ -1434,6 +1462,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     if (t == 0) s_det_ok = ok;
                 }
                 __syncthreads();
+                SX_BSTAMP(1);
                 if (!s_det_ok) {
                     aborted = true;
                     break;
@@ -1498,16 +1527,19 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                             data = (unsigned)r;
                         } else if (k == kOS) {
                             data = (unsigned)ost;
+                        } else if (k == kOM) {
+                            data = (unsigned)reinterpret_cast<const int *>(s_a)[win];
                         } else {
                             const double val = k < kOP ? wv : k < kOB ? p : k < kOR ? br
                                                                           : s_hist[((k - kOU) >> 1) * SX_TILE + win];
                             const u64 bits64 = (u64)__double_as_longlong(val);
-                            data = (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64;
+                            data = ((k < kOU ? k : k - kOU) & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64;
                         }
                         put_g(gb + (size_t)tb * SX_GB_STRIDE + k, data, k < kOP ? (tag | pl) : tag);
                     }
                 }
                 if (tb == 0) SX_STAMP(4);
+                SX_BSTAMP(2);
                 if (ost != SX_NOT_ENDED) {
                     status = ost;
                     break;
@@ -1583,6 +1615,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
     st->e_next = e;
     st->dmin_next = dmin;
 #undef SX_STAMP
+#undef SX_BSTAMP
 }
 
 
@@ -1637,7 +1670,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
     __shared__ unsigned s_pay[SX_TILE];
     __shared__ int s_ok, s_flag;
     // per-step results written by wave 0 before the step's one barrier (as in k_batch)
-    __shared__ int s_sel_ok, s_sel_r, s_sel_any, s_det_ok, s_det_e, s_det_st, s_ent_ok, s_ent_e, s_ent_r, s_ent_st;
+    __shared__ int s_sel_ok, s_sel_r, s_sel_any, s_det_ok, s_det_e, s_det_st, s_ent_ok, s_ent_e, s_ent_r, s_ent_st, s_ent_m;
     __shared__ double s_det_dmin, s_ent_v, s_br, s_ent_p;
     __shared__ int s_welig[SX_TILE / 64];
     const int t = threadIdx.x;
@@ -1660,6 +1693,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
     const int ia = tb * SX_TILE + t;
     const bool liveB = !isA && ia < L;
     const int mj = c.map(1 + (liveB ? ia : 0));
+    if (!isA) reinterpret_cast<int *>(s_a)[t] = mj;  // (as k_batch)
     double dj = liveB ? d[1 + ia] : 0.0;
     double d0 = (!isA && tb == 0 && t == 0) ? d[0] : 0.0;
     if (status0 == SX_NOT_ENDED) {
@@ -1762,6 +1796,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                             s_br = gd(s_g[kOB - kOP], s_g[kOB - kOP + 1]);
                             s_ent_r = (int)s_g[kOR - kOP];
                             s_ent_st = (int)s_g[kOS - kOP];
+                            s_ent_m = (int)s_g[kOM - kOP];
                         }
                     }
                 }
@@ -1775,7 +1810,6 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                     break;
                 }
                 const int enext = s_ent_e;
-                if (liveA) a_pre = T[tl.idx(li, c.map(1 + (enext >= 0 ? enext : 0)))];
                 const int r = s_ent_r;
                 const double p = s_ent_p, br = s_br;
                 if (t == 0) {
@@ -1791,8 +1825,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                     if (row0 + li == r) {
                         b = b / p;
                         bits |= 1u << q;
-                        const u64 w = PM[li];
-                        PM[li] = (((unsigned)(w >> 32) == B) ? w : ((u64)B << 32)) | (1ull << q);
+                        PM[li] = ((u64)B << 32) | bits;  // (as k_batch: written, not read-modified)
                     } else {
                         b = fma(f, br, b);
                     }
@@ -1805,6 +1838,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 }
                 e = enext;
                 dmin = s_ent_v;
+                if (liveA) a_pre = T[tl.idx(li, s_ent_m)];  // (as k_batch)
                 __syncthreads();
             } else {
                 // ---- selection: pass 2 over every rank's ratio tiles (wave 0 polls and reduces)
@@ -1914,11 +1948,13 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                             data = (unsigned)r;
                         } else if (k == kOS) {
                             data = (unsigned)ost;
+                        } else if (k == kOM) {
+                            data = (unsigned)reinterpret_cast<const int *>(s_a)[win];
                         } else {
                             const double val = k < kOP ? wv : k < kOB ? p : k < kOR ? br
                                                                             : s_hist[((k - kOU) >> 1) * SX_TILE + win];
                             const u64 bits64 = (u64)__double_as_longlong(val);
-                            data = (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64;
+                            data = ((k < kOU ? k : k - kOU) & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64;
                         }
                         put_g_sys(pv.gb[rk] + (size_t)tb * SX_GB_STRIDE + k, data, k < kOP ? (tag | pl) : tag);
                     }
@@ -2217,7 +2253,6 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
                                                    const DevState *__restrict__ st,
                                                    const SweepMeta *__restrict__ meta, unsigned B, int rev,
                                                    int *__restrict__ rec) {
-    constexpr int KS = 4 * NKB;  // slots held
     sweep_record(rec, st, nact);
     const int cnt = meta ? (meta->tag == B ? meta->count : 0) : (st->batch_tag == B ? st->batch_count : 0);
     if (cnt <= 0 && Tdst == Tsrc) return;

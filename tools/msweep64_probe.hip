@@ -5,6 +5,8 @@
 //   V1  one tile pair per wave (32 columns): half the U registers, more waves per SIMD
 //   V2  V1 with the next strip's tiles and factors loaded before this strip's matrix steps
 //   V3  V0 with the strip's factors loaded once per block into LDS (4 waves share them)
+//   V4  V3 with the next strip's tiles and factors loaded before this strip's matrix steps
+//   V6  V0 with the next strip's tiles loaded before this strip's matrix steps
 // Factors in the engine's strip-major layout (16-row strips, slot-major inside: sx_fidx).  Every
 // variant is checked against the vector fma chain, bit for bit.
 //   build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/msweep64_probe.hip -o tools/msweep64_probe
@@ -183,6 +185,131 @@ __global__ __launch_bounds__(256) void k_v3(double *T, int rows, int cols, size_
     }
 }
 
+// V4: V3 + the next strip's tableau tiles and factors loaded (to registers) before this strip's
+// matrix steps; the factors go to the other LDS buffer after them (one barrier per strip)
+__global__ __launch_bounds__(256, 2) void k_v4(double *T, int rows, int cols, size_t ld, const double *__restrict__ F,
+                                               const double *__restrict__ U, int G) {
+    __shared__ double s_f[2][16 * K];
+    const int t = threadIdx.x, l = t & 63, w = t >> 6, jl = l & 15, rg = l >> 4;
+    const int c0 = (blockIdx.x * 4 + w) * 64;
+    const bool live = c0 < cols;
+    double2 uf[NKB][2];
+    if (live) load_u<2>(uf, U, ld, c0, rg, jl);
+    const int nstrip = rows / 16;
+    int g = blockIdx.y;
+    if (g >= nstrip) return;
+    double2 cx[2][4];
+    {
+        const __amdgpu_buffer_rsrc_t rs = strip_rsrc(T, g * 16, ld);
+        if (live)
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) cx[p][v] = ld16(rs, (int)(((rg + 4 * v) * ld + c0 + 32 * p + 2 * jl) * 8));
+        const double2 *src = reinterpret_cast<const double2 *>(F + fidx(g * 16, 0));
+        const double2 a = src[2 * t], b = src[2 * t + 1];
+        reinterpret_cast<double2 *>(s_f[0])[2 * t] = a;
+        reinterpret_cast<double2 *>(s_f[0])[2 * t + 1] = b;
+    }
+    for (int buf = 0; g < nstrip; g += G, buf ^= 1) {
+        __syncthreads();
+        const int gn = g + G;
+        double2 cn[2][4], fa, fb;
+        if (gn < nstrip) {
+            const __amdgpu_buffer_rsrc_t rn = strip_rsrc(T, gn * 16, ld);
+            if (live)
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+#pragma unroll
+                    for (int v = 0; v < 4; ++v)
+                        cn[p][v] = ld16(rn, (int)(((rg + 4 * v) * ld + c0 + 32 * p + 2 * jl) * 8));
+            const double2 *src = reinterpret_cast<const double2 *>(F + fidx(gn * 16, 0));
+            fa = src[2 * t];
+            fb = src[2 * t + 1];
+        }
+        if (live) {
+            const __amdgpu_buffer_rsrc_t rs = strip_rsrc(T, g * 16, ld);
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                d4 ax = {cx[p][0].x, cx[p][1].x, cx[p][2].x, cx[p][3].x};
+                d4 ay = {cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
+#pragma unroll
+                for (int kb = 0; kb < NKB; ++kb) {
+                    const double ff = s_f[buf][64 * kb + l];
+                    ax = __builtin_amdgcn_mfma_f64_16x16x4f64(ff, uf[kb][p].x, ax, 0, 0, 0);
+                    ay = __builtin_amdgcn_mfma_f64_16x16x4f64(ff, uf[kb][p].y, ay, 0, 0, 0);
+                }
+#pragma unroll
+                for (int v = 0; v < 4; ++v) st16(rs, (int)(((rg + 4 * v) * ld + c0 + 32 * p + 2 * jl) * 8), ax[v], ay[v]);
+            }
+        }
+        if (gn < nstrip) {
+            reinterpret_cast<double2 *>(s_f[buf ^ 1])[2 * t] = fa;
+            reinterpret_cast<double2 *>(s_f[buf ^ 1])[2 * t + 1] = fb;
+            if (live)
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) cx[p][v] = cn[p][v];
+        }
+    }
+}
+
+// V6: V0 + the next strip's tableau tiles loaded before this strip's matrix steps (factors
+// loaded per strip to registers, as V0)
+__global__ __launch_bounds__(256, 2) void k_v6(double *T, int rows, int cols, size_t ld, const double *__restrict__ F,
+                                               const double *__restrict__ U, int G) {
+    const int l = threadIdx.x & 63, w = threadIdx.x >> 6, jl = l & 15, rg = l >> 4;
+    const int c0 = (blockIdx.x * 4 + w) * 64;
+    if (c0 >= cols) return;
+    double2 uf[NKB][2];
+    load_u<2>(uf, U, ld, c0, rg, jl);
+    const int nstrip = rows / 16;
+    int g = blockIdx.y;
+    if (g >= nstrip) return;
+    double2 cx[2][4];
+    {
+        const __amdgpu_buffer_rsrc_t rs = strip_rsrc(T, g * 16, ld);
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) cx[p][v] = ld16(rs, (int)(((rg + 4 * v) * ld + c0 + 32 * p + 2 * jl) * 8));
+    }
+    for (; g < nstrip; g += G) {
+        const int gn = g + G;
+        double ff[NKB];
+        const double *Fs = F + fidx(g * 16, 0) + l;
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) ff[kb] = Fs[64 * kb];
+        double2 cn[2][4];
+        if (gn < nstrip) {
+            const __amdgpu_buffer_rsrc_t rn = strip_rsrc(T, gn * 16, ld);
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) cn[p][v] = ld16(rn, (int)(((rg + 4 * v) * ld + c0 + 32 * p + 2 * jl) * 8));
+        }
+        const __amdgpu_buffer_rsrc_t rs = strip_rsrc(T, g * 16, ld);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            d4 ax = {cx[p][0].x, cx[p][1].x, cx[p][2].x, cx[p][3].x};
+            d4 ay = {cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) {
+                ax = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].x, ax, 0, 0, 0);
+                ay = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].y, ay, 0, 0, 0);
+            }
+#pragma unroll
+            for (int v = 0; v < 4; ++v) st16(rs, (int)(((rg + 4 * v) * ld + c0 + 32 * p + 2 * jl) * 8), ax[v], ay[v]);
+        }
+        if (gn < nstrip)
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) cx[p][v] = cn[p][v];
+    }
+}
+
 __global__ void k_ref(double *T, int rows, int cols, size_t ld, const double *F, const double *U) {
     const size_t n = (size_t)rows * cols;
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
@@ -269,6 +396,8 @@ int main() {
             run("V1 1 pair/wave           ", k_v01<1>, 128, sz[0], sz[1]);
             run("V2 1 pair/wave, prefetch ", k_v2, 128, sz[0], sz[1]);
             run("V3 2 pairs/wave, F in LDS", k_v3, 256, sz[0], sz[1]);
+            run("V4 V3 + next strip loaded", k_v4, 256, sz[0], sz[1]);
+            run("V6 V0 + next tiles loaded", k_v6, 256, sz[0], sz[1]);
         }
     return 0;
 }
