@@ -49,6 +49,10 @@ CONFIGS = {
 # oracle pivots timed for the CPU baseline (first 50 / 10 / 3 pivots)
 CPU_SAMPLE = {"config2": 200, "config3": 50, "config4": 10, "config5": 5}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+F64_SPEC_TFLOPS = 78.6  # MI355X fp64 matrix (= vector) spec peak
+# the fp64 matrix rate this chip sustains: v_mfma_f64_16x16x4f64 alone on every SIMD, 2-4 waves each
+# (tools/f64_rate_probe.hip, profiles/r03_f64_rate_probe.txt: 46.8-47.6 TFLOP/s)
+F64_MFMA_MEASURED_TFLOPS = 47.6
 # reference: RTX 2070 Super, config 3 phase 1, mean 7607.5 us per pivot
 REF_PIVOTS_PER_S = {"config3": 1e6 / 7607.5}  # (no published number for configs 4-5)
 # reference: RTX 2070 Super, config 3, pivot-loop totals 68.33 s (phase 1) + 0.94 s (phase 2), 8981 + 255 pivots
@@ -245,7 +249,21 @@ def main():
             "timed_launches": tim.update_launches,
             "timing": "HIP events on the engine stream around every timed sweep",
             "sweep_share_of_time": tim.update_ms / max(tim.wall_ms, 1e-9),
+            "compute": compute_roof(tim),
         }
+
+    def compute_roof(tim):
+        """The sweep's fp64 work against the matrix-core rate: 2 flops per swept element per pending
+        pivot.  A 64-slot sweep does 128 flops per 16 bytes moved, so it is co-bound by the fp64
+        matrix rate."""
+        if not tim.update_launches or tim.update_ms <= 0:
+            return None
+        flops = 2.0 * (tim.swept_pivots / tim.update_launches) * (tim.swept_bytes / 16.0)
+        tf = flops / (tim.update_ms / 1e3) / 1e12
+        return {"achieved_tflops": tf, "spec_peak_tflops": F64_SPEC_TFLOPS,
+                "measured_mfma_ceiling_tflops": F64_MFMA_MEASURED_TFLOPS,
+                "frac_of_spec": tf / F64_SPEC_TFLOPS, "frac_of_measured_ceiling": tf / F64_MFMA_MEASURED_TFLOPS,
+                "ceiling_source": "profiles/r03_f64_rate_probe.txt (v_mfma_f64_16x16x4f64 on every SIMD, no memory)"}
 
     def exchange_name():
         if n_gpus == 1:

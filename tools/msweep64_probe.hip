@@ -310,6 +310,132 @@ __global__ __launch_bounds__(256, 2) void k_v6(double *T, int rows, int cols, si
     }
 }
 
+// V7<WPC>: the pivot rows U in LDS (the B operands read per 4-slot step with one ds_read_b128 for
+// both tiles of a pair), freeing the 128 U registers for a prefetch: the next strip's tableau
+// tiles and factors are loaded before this strip's matrix steps.  Block = 4 column groups of 64
+// columns (256 columns, 128 KB of U) x WPC waves per group (the waves of a group take alternate
+// strips); one block per CU, WPC waves per SIMD.
+template <int WPC, bool SGB>
+__global__ __launch_bounds__(256 * WPC, 1) void k_v7(double *T, int rows, int cols, size_t ld,
+                                                    const double *__restrict__ F, const double *__restrict__ U, int G) {
+    extern __shared__ double2 s_u[];  // [kb][cg][p][lane]: 16 x 4 x 2 x 64 double2
+    const int t = threadIdx.x, l = t & 63, w = t >> 6, cg = w & 3, sub = w >> 2, jl = l & 15, rg = l >> 4;
+    const int c0 = (blockIdx.x * 4 + cg) * 64;
+    const bool live = c0 < cols;
+    if (live)
+        for (int kb = sub; kb < NKB; kb += WPC)
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+                s_u[((kb * 4 + cg) * 2 + p) * 64 + l] =
+                    *reinterpret_cast<const double2 *>(U + (size_t)(4 * kb + rg) * ld + c0 + 32 * p + 2 * jl);
+    __syncthreads();
+    if (!live) return;
+    const int nstrip = rows / 16, GS = G * WPC;
+    int g = blockIdx.y * WPC + sub;
+    if (g >= nstrip) return;
+    double2 cx[2][4];
+    double ff[NKB];
+    {
+        const __amdgpu_buffer_rsrc_t rs = strip_rsrc(T, g * 16, ld);
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) cx[p][v] = ld16(rs, (int)(((rg + 4 * v) * ld + c0 + 32 * p + 2 * jl) * 8));
+        const double *Fs = F + fidx(g * 16, 0) + l;
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) ff[kb] = Fs[64 * kb];
+    }
+    for (; g < nstrip; g += GS) {
+        const int gn = g + GS;
+        double2 cn[2][4];
+        double fn[NKB];
+        if (gn < nstrip) {
+            const __amdgpu_buffer_rsrc_t rn = strip_rsrc(T, gn * 16, ld);
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) cn[p][v] = ld16(rn, (int)(((rg + 4 * v) * ld + c0 + 32 * p + 2 * jl) * 8));
+            const double *Fs = F + fidx(gn * 16, 0) + l;
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) fn[kb] = Fs[64 * kb];
+        }
+        const __amdgpu_buffer_rsrc_t rs = strip_rsrc(T, g * 16, ld);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            d4 ax = {cx[p][0].x, cx[p][1].x, cx[p][2].x, cx[p][3].x};
+            d4 ay = {cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) {
+                const double2 u = s_u[((kb * 4 + cg) * 2 + p) * 64 + l];
+                ax = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], u.x, ax, 0, 0, 0);
+                ay = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], u.y, ay, 0, 0, 0);
+                if (SGB) {
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                }
+            }
+#pragma unroll
+            for (int v = 0; v < 4; ++v) st16(rs, (int)(((rg + 4 * v) * ld + c0 + 32 * p + 2 * jl) * 8), ax[v], ay[v]);
+        }
+        if (gn < nstrip) {
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) cx[p][v] = cn[p][v];
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) ff[kb] = fn[kb];
+        }
+    }
+}
+
+// V8<WPC>: V7 without the prefetch (U in LDS only): WPC waves per SIMD doing V0's strip
+template <int WPC, bool SGB>
+__global__ __launch_bounds__(256 * WPC, 1) void k_v8(double *T, int rows, int cols, size_t ld,
+                                                    const double *__restrict__ F, const double *__restrict__ U, int G) {
+    extern __shared__ double2 s_u[];
+    const int t = threadIdx.x, l = t & 63, w = t >> 6, cg = w & 3, sub = w >> 2, jl = l & 15, rg = l >> 4;
+    const int c0 = (blockIdx.x * 4 + cg) * 64;
+    const bool live = c0 < cols;
+    if (live)
+        for (int kb = sub; kb < NKB; kb += WPC)
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+                s_u[((kb * 4 + cg) * 2 + p) * 64 + l] =
+                    *reinterpret_cast<const double2 *>(U + (size_t)(4 * kb + rg) * ld + c0 + 32 * p + 2 * jl);
+    __syncthreads();
+    if (!live) return;
+    const int nstrip = rows / 16, GS = G * WPC;
+    for (int g = blockIdx.y * WPC + sub; g < nstrip; g += GS) {
+        const __amdgpu_buffer_rsrc_t rs = strip_rsrc(T, g * 16, ld);
+        double2 cx[2][4];
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) cx[p][v] = ld16(rs, (int)(((rg + 4 * v) * ld + c0 + 32 * p + 2 * jl) * 8));
+        double ff[NKB];
+        const double *Fs = F + fidx(g * 16, 0) + l;
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) ff[kb] = Fs[64 * kb];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            d4 ax = {cx[p][0].x, cx[p][1].x, cx[p][2].x, cx[p][3].x};
+            d4 ay = {cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) {
+                const double2 u = s_u[((kb * 4 + cg) * 2 + p) * 64 + l];
+                ax = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], u.x, ax, 0, 0, 0);
+                ay = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], u.y, ay, 0, 0, 0);
+                if (SGB) {
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                }
+            }
+#pragma unroll
+            for (int v = 0; v < 4; ++v) st16(rs, (int)(((rg + 4 * v) * ld + c0 + 32 * p + 2 * jl) * 8), ax[v], ay[v]);
+        }
+    }
+}
+
 __global__ void k_ref(double *T, int rows, int cols, size_t ld, const double *F, const double *U) {
     const size_t n = (size_t)rows * cols;
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
@@ -339,7 +465,7 @@ __global__ void k_init(double *p, size_t n, unsigned seed, double lo, double hi)
 
 typedef void (*Kern)(double *, int, int, size_t, const double *, const double *, int);
 
-void run(const char *name, Kern kern, int cols_per_block, int rows, int cols) {
+void run(const char *name, Kern kern, int cols_per_block, int rows, int cols, int threads = 256, size_t lds = 0) {
     const size_t ld = cols;
     double *T, *T2, *F, *U;
     CK(hipMalloc(&T, (size_t)rows * ld * 8));
@@ -350,7 +476,8 @@ void run(const char *name, Kern kern, int cols_per_block, int rows, int cols) {
     k_init<<<4096, 256>>>(F, (size_t)K * rows, 2, -1e-2, 1e-2);
     k_init<<<4096, 256>>>(U, (size_t)K * ld, 3, 1.0, 100.0);
     int per_cu = 0, cus = 0, dev = 0;
-    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0));
+    if (lds) CK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds));
     CK(hipGetDevice(&dev));
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const int cb = cols / cols_per_block;
@@ -359,7 +486,7 @@ void run(const char *name, Kern kern, int cols_per_block, int rows, int cols) {
     if (G < 1) G = 1;
     dim3 grid(cb, G);
     CK(hipMemcpy(T2, T, (size_t)rows * ld * 8, hipMemcpyDeviceToDevice));
-    kern<<<grid, 256>>>(T2, rows, cols, ld, F, U, G);
+    kern<<<grid, threads, lds>>>(T2, rows, cols, ld, F, U, G);
     k_ref<<<8192, 256>>>(T, rows, cols, ld, F, U);
     unsigned long long *bad;
     CK(hipMalloc(&bad, 8));
@@ -371,10 +498,10 @@ void run(const char *name, Kern kern, int cols_per_block, int rows, int cols) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (int i = 0; i < 5; ++i) kern<<<grid, 256>>>(T2, rows, cols, ld, F, U, G);
+    for (int i = 0; i < 5; ++i) kern<<<grid, threads, lds>>>(T2, rows, cols, ld, F, U, G);
     CK(hipEventRecord(e0));
     const int it = 30;
-    for (int i = 0; i < it; ++i) kern<<<grid, 256>>>(T2, rows, cols, ld, F, U, G);
+    for (int i = 0; i < it; ++i) kern<<<grid, threads, lds>>>(T2, rows, cols, ld, F, U, G);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float ms = 0;
@@ -390,7 +517,7 @@ void run(const char *name, Kern kern, int cols_per_block, int rows, int cols) {
 
 int main() {
     const int sizes[3][2] = {{32768, 9216}, {4096, 8192}, {32768, 10240}};
-    for (int rep = 0; rep < 2; ++rep)
+    for (int rep = 0; rep < 1; ++rep)
         for (auto &sz : sizes) {
             run("V0 2 pairs/wave          ", k_v01<2>, 256, sz[0], sz[1]);
             run("V1 1 pair/wave           ", k_v01<1>, 128, sz[0], sz[1]);
@@ -398,6 +525,15 @@ int main() {
             run("V3 2 pairs/wave, F in LDS", k_v3, 256, sz[0], sz[1]);
             run("V4 V3 + next strip loaded", k_v4, 256, sz[0], sz[1]);
             run("V6 V0 + next tiles loaded", k_v6, 256, sz[0], sz[1]);
+            run("V7<1> U in LDS + prefetch", k_v7<1, false>, 256, sz[0], sz[1], 256, 131072);
+            run("V7<1> ... sched groups   ", k_v7<1, true>, 256, sz[0], sz[1], 256, 131072);
+            run("V7<2> ... sched groups   ", k_v7<2, true>, 256, sz[0], sz[1], 512, 131072);
+            run("V7<3> ... sched groups   ", k_v7<3, true>, 256, sz[0], sz[1], 768, 131072);
+            run("V8<1> U in LDS           ", k_v8<1, false>, 256, sz[0], sz[1], 256, 131072);
+            run("V8<2> U in LDS           ", k_v8<2, false>, 256, sz[0], sz[1], 512, 131072);
+            run("V8<2> ... sched groups   ", k_v8<2, true>, 256, sz[0], sz[1], 512, 131072);
+            run("V8<3> ... sched groups   ", k_v8<3, true>, 256, sz[0], sz[1], 768, 131072);
+            run("V8<4> ... sched groups   ", k_v8<4, true>, 256, sz[0], sz[1], 1024, 131072);
         }
     return 0;
 }
