@@ -2292,20 +2292,17 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
                                                  : make_double2(0.0, 0.0);
             }
         const int nstrip = (rows + 15) >> 4;
-        for (int g = gy; g < nstrip; g += G) {
-            const int r0 = (rev ? nstrip - 1 - g : g) * 16;
-            const int fr = r0 + jl;  // the A-operand row of this lane
-            // one buffer resource per strip (wave-uniform), holding the strip's valid rows; rows
-            // past the end read 0 and drop their stores
+        // a strip's tableau tiles (both pairs), through one buffer resource per strip
+        // (wave-uniform) holding the strip's valid rows; rows past the end read 0 and drop their
+        // stores
+        auto strip_r0 = [&](int g) { return (rev ? nstrip - 1 - g : g) * 16; };
+        auto strip_rsrc = [&](const double *base, int r0) {
             const int nr = rows - r0 < 16 ? rows - r0 : 16;
-            const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<double *>(Tr) + (size_t)r0 * ldr, 0, (int)((size_t)nr * ldr * 8), 0x00020000);
-            const __amdgpu_buffer_rsrc_t rss =
-                __builtin_amdgcn_make_buffer_rsrc(Tw + (size_t)r0 * ldr, 0, (int)((size_t)nr * ldr * 8), 0x00020000);
-            // issue order: both pairs' tableau tiles, the strip's factors, its leaving-row bits --
-            // one memory round trip per strip (the bits are only needed after the first pair's
-            // matrix steps, and the counter waits are in issue order)
-            double2 cx[2][4];
+            return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(base) + (size_t)r0 * ldr, 0,
+                                                     (int)((size_t)nr * ldr * 8), 0x00020000);
+        };
+        auto load_tiles = [&](double2 (&cx)[2][4], int r0) {
+            const __amdgpu_buffer_rsrc_t rsl = strip_rsrc(Tr, r0);
 #pragma unroll
             for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -2315,6 +2312,16 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
                     cx[p][v] = __builtin_bit_cast(
                         double2, __builtin_amdgcn_raw_buffer_load_b128(rsl, j < Ns ? off : OOB, 0, 2));
                 }
+        };
+        for (int g = gy; g < nstrip; g += G) {
+            const int r0 = strip_r0(g);
+            const int fr = r0 + jl;  // the A-operand row of this lane
+            const __amdgpu_buffer_rsrc_t rss = strip_rsrc(Tw, r0);
+            // issue order: both pairs' tableau tiles, the strip's factors, its leaving-row bits --
+            // one memory round trip per strip (the bits are only needed after the first pair's
+            // matrix steps, and the counter waits are in issue order)
+            double2 cx[2][4];
+            load_tiles(cx, r0);
             double ff[NKB];
             {
                 // (lane l of step kb: F[sx_fidx(r0 + l % 16, 4 kb + l / 16)] = strip base + 64 kb + l;
@@ -2707,10 +2714,11 @@ void sx_launch_pivot_row(const double *T, int rows, int row0, size_t ld, TLay tl
 static int *g_sweep_rec = nullptr;
 void sx_set_sweep_record(int *rec) { g_sweep_rec = rec; }
 
-// blocks of a kernel resident on the whole device at once
-template <typename K>
-static int sweep_capacity(K kernel) {
-    static int cap = 0;  // per kernel instantiation
+// blocks of a kernel resident on the whole device at once (cached per kernel: the template
+// parameter is the kernel itself -- instantiations of one kernel template share a type)
+template <auto kernel>
+static int sweep_capacity() {
+    static int cap = 0;
     if (cap == 0) {
         int per_cu = 0, dev = 0, cus = 0;
         SX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0));
@@ -2739,7 +2747,7 @@ template <int KT, int RB, int POL>
 static void launch_sweep_t(double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0, const Pending &pd,
                            const DevState *st, int rev, hipStream_t s) {
     const int cb = (Ns + 511) / 512;
-    dim3 grid(cb, row_slots(sweep_capacity(k_sweep<KT, RB, POL>), cb, rows, RB));
+    dim3 grid(cb, row_slots(sweep_capacity<k_sweep<KT, RB, POL>>(), cb, rows, RB));
     k_sweep<KT, RB, POL><<<grid, 256, 0, s>>>(T, rows, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st, pd.batch, rev,
                                               g_sweep_rec);
 }
@@ -2778,11 +2786,11 @@ void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, 
             SX_FATAL("matrix-core sweep: 16-byte rows and 256-aligned regions required");
         const int cb = (Ns + 255) / 256;
         if (cfg.batch > SX_HMAX) {
-            dim3 grid(cb, row_slots(sweep_capacity(k_msweep<SX_KMAX / 4>), cb, rows, 16));
+            dim3 grid(cb, row_slots(sweep_capacity<k_msweep<SX_KMAX / 4>>(), cb, rows, 16));
             k_msweep<SX_KMAX / 4><<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM,
                                                        pd.PM2, st, nullptr, pd.batch, rev, g_sweep_rec);
         } else {
-            dim3 grid(cb, row_slots(sweep_capacity(k_msweep<SX_HMAX / 4>), cb, rows, 16));
+            dim3 grid(cb, row_slots(sweep_capacity<k_msweep<SX_HMAX / 4>>(), cb, rows, 16));
             k_msweep<SX_HMAX / 4><<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM,
                                                        pd.PM2, st, nullptr, pd.batch, rev, g_sweep_rec);
         }
@@ -2811,7 +2819,8 @@ void sx_launch_msweep_oop(const double *Tsrc, double *Tdst, int rows, int row0, 
         SX_FATAL("matrix-core sweep: 16-byte rows and 256-aligned regions required");
     const int cb = (Ns + 255) / 256;
     auto kern = k_msweep<SX_KMAX / 4>;
-    const int cap = grid_cap > 0 ? std::min(grid_cap, sweep_capacity(kern)) : sweep_capacity(kern);
+    const int full = sweep_capacity<k_msweep<SX_KMAX / 4>>();
+    const int cap = grid_cap > 0 ? std::min(grid_cap, full) : full;
     dim3 grid(cb, row_slots(cap, cb, rows, 16));
     kern<<<grid, 256, 0, s>>>(Tsrc, Tdst, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, pd.PM2, st, meta,
                               pd.batch, rev, nullptr);
