@@ -111,6 +111,10 @@ long long simplex_hang_recoveries(void);
 long long simplex_fused_batches(void);           /* fused batch launches in the process */
 /* test hook: make the n-th fused batch from now abort as if a wait had timed out (-1 off) */
 void simplex_set_hang_inject(long long batches);
+/* ... at which slot of that batch: -1 (default) before it starts; s >= 0: the batch runs s
+ * pivots (the objective row already updated by them) and then one block leaves it, so the others
+ * time out inside the batch */
+void simplex_set_hang_inject_slot(int slot);
 /* test hook: batch id of the next engine's first batch (1 .. 32767; ids wrap at 32768) */
 void simplex_set_first_batch_id(unsigned int id);
 

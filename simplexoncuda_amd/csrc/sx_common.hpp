@@ -93,7 +93,8 @@ struct Pending {
 struct BatchChan {
     alignas(128) unsigned exit_cnt;  // blocks that have left the kernel
     alignas(128) unsigned abort_w;   // a wait timed out: every block leaves
-    alignas(128) unsigned pad;
+    alignas(128) unsigned inject_q;  // test hook: 1 + the slot at which ratio block 0 (of rank 0)
+                                     // leaves with the batch aborted (0: off); the last block clears it
 };
 
 // Multi-rank fused batch (k_batch_mr): every rank's buffers as seen from this rank (peer

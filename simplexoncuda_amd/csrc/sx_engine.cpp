@@ -77,6 +77,7 @@ struct Config {
     bool benchmark = false;
     bool no_timer = false;         // the multi-GPU self-check: never write TIMER CSVs
     long long inject_hang = -1;    // test hook: abort the n-th fused batch from now (-1 off)
+    int inject_slot = -1;          // ... before it starts (-1) or at this slot (inside the kernel)
     unsigned first_batch_id = 1;   // test hook: batch id of a new engine's first batch
     int ipc_rank = -1, ipc_world = 0;  // test hook: one shard per process, peers through IPC handles, no RCCL
     int uncached_xchg = 0;         // several shards: d and U in uncached memory (diagnostic; see alloc_shard)
@@ -1137,7 +1138,11 @@ class Engine {
         if (g_cfg.inject_hang >= 0 && g_cfg.inject_hang-- == 0)  // test hook: this batch aborts
             for (auto &x : sh) {
                 DevGuard g(x.dev);
-                SX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&x.chan->abort_w), 1u, 1, x.s));
+                if (g_cfg.inject_slot < 0)
+                    SX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&x.chan->abort_w), 1u, 1, x.s));
+                else
+                    SX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&x.chan->inject_q),
+                                             (unsigned)g_cfg.inject_slot + 1u, 1, x.s));
             }
         if (!xchg) {
             Shard &x = sh[0];
@@ -1729,6 +1734,7 @@ void simplex_set_exchange_mode(int mode) { g_cfg.exchange_mode = (mode >= 0 && m
 void simplex_set_timer_dir(const char *dir) { g_cfg.timer_dir = dir ? dir : ""; }
 
 void simplex_set_hang_inject(long long batches) { g_cfg.inject_hang = batches >= 0 ? batches : -1; }
+void simplex_set_hang_inject_slot(int slot) { g_cfg.inject_slot = slot >= 0 ? slot : -1; }
 long long simplex_hang_recoveries(void) { return g_cfg.hang_recoveries; }
 long long simplex_fused_batches(void) { return g_cfg.fused_batches; }
 void simplex_set_first_batch_id(unsigned int id) { g_cfg.first_batch_id = (id >= 1 && id < SX_BATCH_IDS) ? id : 1; }

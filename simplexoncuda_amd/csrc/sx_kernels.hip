@@ -1197,6 +1197,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
     double dmin = st->dmin_next;
     int status = SX_NOT_ENDED, cnt = 0;
     bool aborted = false;
+    const unsigned inj = ch->inject_q;  // (test hook, normally 0)
     if (status0 == SX_NOT_ENDED) {
         // ratio block: its row; objective block: its logical column d[1 + ia]
         const int li = blockIdx.x * SX_TILE + t;
@@ -1252,6 +1253,11 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     break;
                 }
                 if (q == SX_HMAX) next_stage();
+                if (inj != 0u && blockIdx.x == 0 && (unsigned)q + 1u == inj) {  // test hook: leave, aborted
+                    if (t == 0) __hip_atomic_store(&ch->abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    aborted = true;
+                    break;
+                }
                 const int qq = q - hb;  // slot within the stage
                 const bool done = !(cmp_eps(dmin, 0.0) < 0);  // solver.cu:88: optimal
                 // ---- ratio tile: current entering column, ratios, tile winner
@@ -1579,7 +1585,10 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // (the block's U stores out of its L2)
         const unsigned k = __hip_atomic_fetch_add(&ch->exit_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = k == (unsigned)(NA + NB) - 1;
-        if (s_last) __hip_atomic_store(&ch->exit_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (s_last) {
+            __hip_atomic_store(&ch->exit_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (inj != 0u) ch->inject_q = 0u;  // (every block read it at its start)
+        }
     }
     __syncthreads();
     if (!s_last || status0 != SX_NOT_ENDED) return;
@@ -1682,6 +1691,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
     double dmin = st->dmin_next;
     int status = SX_NOT_ENDED, cnt = 0;
     bool aborted = false;
+    const unsigned inj = ch->inject_q;  // (test hook, normally 0)
     auto gather_a = [](int k) { return rec2_a(k); };
     auto gather_b = [](int k) { return rec2_b(k); };
     auto ident = [](int k) { return k; };
@@ -1710,6 +1720,11 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
             const unsigned tag = make_tag(B, q);
             if (cap >= 0 && piv0 + q >= cap) {
                 status = SX_PIVOT_CAP;
+                break;
+            }
+            if (inj != 0u && isA && rank == 0 && bid == 0 && (unsigned)q + 1u == inj) {  // test hook
+                if (t == 0) __hip_atomic_store(&ch->abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                aborted = true;
                 break;
             }
             if (isA) {
@@ -2006,7 +2021,10 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
     if (t == 0) {
         const unsigned k = __hip_atomic_fetch_add(&ch->exit_cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
         s_flag = (k == nbl - 1);
-        if (s_flag) __hip_atomic_store(&ch->exit_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (s_flag) {
+            __hip_atomic_store(&ch->exit_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (inj != 0u) ch->inject_q = 0u;  // (every block of this rank read it at its start)
+        }
     }
     __syncthreads();
     if (!s_flag) return;

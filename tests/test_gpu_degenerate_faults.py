@@ -111,6 +111,50 @@ def test_hang_recovery_bit_exact(gpu, inject, batch):
     assert tuple(got.pivots) == (2003, 69)
 
 
+@pytest.mark.parametrize("batch,slot", [(0, 5), (0, 31), (64, 20), (64, 45)])
+def test_hang_recovery_mid_batch(gpu, batch, slot):
+    """the abort inside a running batch -- `slot` pivots already applied to the
+    objective row (and, past slot 32, the second stage started) when ratio block 0 leaves and
+    the other blocks time out.  The host restores d from d_save (each entry saved by the thread
+    that wrote it) and re-runs the batch; the solve stays bit-exact"""
+    lib = sx.load()
+    p = sx.generateRandomProblem(2048, 1024, 205824, 1, 100)
+    r0 = lib.simplex_hang_recoveries()
+    lib.simplex_set_hang_inject(3)
+    lib.simplex_set_hang_inject_slot(slot)
+    sx.set_batch(batch)
+    try:
+        got = solve_both(*p.arrays())
+    finally:
+        sx.set_batch(0)
+        lib.simplex_set_hang_inject(-1)
+        lib.simplex_set_hang_inject_slot(-1)
+        p.close()
+    assert lib.simplex_hang_recoveries() == r0 + 1
+    assert tuple(got.pivots) == (2003, 69)
+
+
+def test_hang_recovery_mid_batch_multirank(gpu):
+    """the same inside a peer-memory batch of 2 virtual shards: rank 0's ratio block 0 leaves at
+    slot 9, its peers time out; every shard restores its own slice of d and re-runs the batch"""
+    lib = sx.load()
+    p = sx.generateRandomProblem(129, 1513, 77, -100, 100)
+    r0 = lib.simplex_hang_recoveries()
+    sx.set_virtual_ranks(2)
+    sx.set_p2p(1)
+    lib.simplex_set_hang_inject(2)
+    lib.simplex_set_hang_inject_slot(9)
+    try:
+        solve_both(*p.arrays())
+    finally:
+        lib.simplex_set_hang_inject(-1)
+        lib.simplex_set_hang_inject_slot(-1)
+        sx.set_p2p(-1)
+        sx.set_virtual_ranks(1)
+        p.close()
+    assert lib.simplex_hang_recoveries() == r0 + 1
+
+
 def test_hang_recovery_twice_falls_back(gpu):
     """two aborts in one phase: the rest of the phase runs on the per-pivot path"""
     lib = sx.load()
