@@ -1765,9 +1765,10 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                     const int wl = wi >= 0 ? wi - row0 - bid * SX_TILE : 0;
                     // the record into every rank's copy
                     const unsigned pl = (wi >= 0 ? (unsigned)(wi - gt * SX_TILE) : SX_NOIDX) | ((unsigned)any << 10);
+                    // granule-major over the ranks: the value granules reach every rank first
                     const int nG = kRF + 2 * q;
                     for (int idx = t; idx < W * nG; idx += 64) {
-                        const int rk = idx / nG, k = idx - rk * nG;
+                        const int k = idx / W, rk = idx - k * W;
                         unsigned data;
                         if (k == kRE) {
                             data = (unsigned)e;
@@ -1927,8 +1928,6 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                     cnt = q + 1;
                     u = hist_row(u, q, r, s_hist, s_fr, s_p, s_r);
                     s_hist[q * SX_TILE + t] = u;
-                    if (liveB && 1 + ia < c.Ns)
-                        for (int k = 0; k < W; ++k) st_sys(pv.U[k] + (size_t)q * ld + mj, u);
                     const double fd = -dmin / p;  // updateCostsVector, solver.cu:48-56
                     if (tb == 0 && t == 0) d0 = fma(fd, br, d0);
                     if (liveB) {
@@ -1955,9 +1954,10 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                                               (long long)(unsigned)__builtin_amdgcn_readfirstlane((int)vb));
                     const int win = wi >= 0 ? wi - tb * SX_TILE : 0;
                     const unsigned pl = wi >= 0 ? (unsigned)win : SX_NOIDX;
+                    // granule-major over the ranks: the value granules reach every rank first
                     const int nG = kOU + 2 * (q + 1);
                     for (int idx = t; idx < W * nG; idx += 64) {
-                        const int rk = idx / nG, k = idx - rk * nG;
+                        const int k = idx / W, rk = idx - k * W;
                         unsigned data;
                         if (k == kOR) {
                             data = (unsigned)r;
@@ -1973,6 +1973,12 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                         }
                         put_g_sys(pv.gb[rk] + (size_t)tb * SX_GB_STRIDE + k, data, k < kOP ? (tag | pl) : tag);
                     }
+                }
+                // the pivot row into every rank's U[q] (the sweep's input, read after the batch):
+                // issued behind the record, so the W-fold stores do not delay it
+                if (ost == SX_NOT_ENDED && liveB && 1 + ia < c.Ns) {
+                    const double uq = s_hist[q * SX_TILE + t];
+                    for (int k = 0; k < W; ++k) st_sys(pv.U[k] + (size_t)q * ld + mj, uq);
                 }
                 if (ost != SX_NOT_ENDED) {
                     status = ost;
