@@ -1496,8 +1496,6 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     u = hist_row(u, qq, r, s_hist, s_fr, s_p + hb, s_r + hb);
                     s_hist[qq * SX_TILE + t] = u;
                     if (tb == 0) SX_STAMP(7);
-                    // (plain stores: written back at the stage switch and before the block leaves)
-                    if (liveB && 1 + ia < c.Ns) U[(size_t)q * ld + mj] = u;
                     const double fd = -dmin / p;  // updateCostsVector, solver.cu:48-56
                     if (tb == 0 && t == 0) d0 = fma(fd, br, d0);
                     if (liveB) {
@@ -1544,6 +1542,9 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                         put_g(gb + (size_t)tb * SX_GB_STRIDE + k, data, k < kOP ? (tag | pl) : tag);
                     }
                 }
+                // the pivot row into U[q] (the sweep's input) behind the record (plain stores:
+                // written back at the stage switch and before the block leaves)
+                if (ost == SX_NOT_ENDED && liveB && 1 + ia < c.Ns) U[(size_t)q * ld + mj] = s_hist[qq * SX_TILE + t];
                 if (tb == 0) SX_STAMP(4);
                 SX_BSTAMP(2);
                 if (ost != SX_NOT_ENDED) {
