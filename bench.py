@@ -120,7 +120,7 @@ def main():
     ap.add_argument("--config", default="config5", choices=sorted(CONFIGS))
     ap.add_argument("--update-rows", type=int, default=0, help="rows per sweep step (0 = auto)")
     ap.add_argument("--batch", type=int, default=0,
-                    help="pivots per tableau sweep (0 = library default: 64 on one GPU, 32 on several)")
+                    help="pivots per tableau sweep (0 = library default: 64 from 4096 rows, else 32)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--update-events", type=int, default=1,
                     help="bracket every k-th sweep launch with HIP events (0 = none)")

@@ -106,6 +106,7 @@ struct PeerView {
     unsigned long long *gb[SX_MAXW]; // objective-tile records (written)
     unsigned long long *gdone[SX_MAXW];  // batch-end done granules (written)
     double *U[SX_MAXW];              // pending pivot rows (written)
+    const double *F[SX_MAXW];        // pending row factors (read: the leaving row's first stage)
     double *d[SX_MAXW];              // objective rows (written)
 };
 
@@ -198,7 +199,8 @@ void sx_launch_msweep_oop(const double *Tsrc, double *Tdst, int rows, int row0, 
 // slack compaction, after a batch's selections and before its sweep: move the slack column
 // of every row that left the basis for the first time into the swept block
 void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, int m, double *T, int rows, int row0,
-                        size_t ld, TLay tl, int s0, const Pending &pd, const DevState *st, hipStream_t s);
+                        size_t ld, TLay tl, int s0, const Pending &pd, const DevState *st, int slots,
+                        hipStream_t s);  // slots: the batch size (two passes above SX_HMAX)
 // fused batch of up to k pivots on one shard (ratio tiles + objective tiles in one resident
 // grid); returns false (nothing launched) when the grid cannot be resident at once
 bool sx_batch_fits(int rows, Cols c, int k);

@@ -78,6 +78,7 @@ struct Config {
     bool no_timer = false;         // the multi-GPU self-check: never write TIMER CSVs
     long long inject_hang = -1;    // test hook: abort the n-th fused batch from now (-1 off)
     int inject_slot = -1;          // ... before it starts (-1) or at this slot (inside the kernel)
+    int mr_two_stage = -1;         // peer-memory multi-rank batches of two stages (-1: unless SIMPLEX_MR_STAGES=1)
     unsigned first_batch_id = 1;   // test hook: batch id of a new engine's first batch
     int ipc_rank = -1, ipc_world = 0;  // test hook: one shard per process, peers through IPC handles, no RCCL
     int uncached_xchg = 0;         // several shards: d and U in uncached memory (diagnostic; see alloc_shard)
@@ -489,6 +490,7 @@ class Engine {
                 pv.gb[x.rank] = x.gb;
                 pv.gdone[x.rank] = x.gdone;
                 pv.U[x.rank] = x.U;
+                pv.F[x.rank] = x.F;
                 pv.d[x.rank] = x.d;
                 if (multidev) continue;  // (one launch per device on its engine stream)
                 SX_HIP(hipStreamCreateWithFlags(&x.ss, hipStreamNonBlocking));
@@ -521,13 +523,14 @@ class Engine {
         p2p = true;
     }
 
-    // IPC handles of this process's six exchanged buffers (T, ga, gb, gdone, U, d)
-    static constexpr size_t kHandles = 6 * sizeof(hipIpcMemHandle_t);
+    // IPC handles of this process's seven exchanged buffers (T, ga, gb, gdone, U, d, F)
+    static constexpr int kBufs = 7;
+    static constexpr size_t kHandles = kBufs * sizeof(hipIpcMemHandle_t);
     int export_handles(unsigned char *out) {
         const Shard &x = sh[0];
-        void *bufs[6] = {x.T, x.ga, x.gb, x.gdone, x.U, x.d};
+        void *bufs[kBufs] = {x.T, x.ga, x.gb, x.gdone, x.U, x.d, x.F};
         int ok = 1;
-        for (int k = 0; k < 6; ++k) {
+        for (int k = 0; k < kBufs; ++k) {
             hipIpcMemHandle_t h;
             std::memset(&h, 0, sizeof(h));
             ok &= hipIpcGetMemHandle(&h, bufs[k]) == hipSuccess;
@@ -540,32 +543,33 @@ class Engine {
     // map every other rank's buffers from `all` (W x kHandles bytes) into pv; false if any fails
     bool map_peers(const unsigned char *all, int me) {
         const Shard &x = sh[0];
-        void *mine[6] = {x.T, x.ga, x.gb, x.gdone, x.U, x.d};
-        std::vector<void *> mapped((size_t)W * 6, nullptr);
+        void *mine[kBufs] = {x.T, x.ga, x.gb, x.gdone, x.U, x.d, x.F};
+        std::vector<void *> mapped((size_t)W * kBufs, nullptr);
         bool ok = true;
         for (int r = 0; r < W && ok; ++r)
-            for (int k = 0; k < 6 && ok; ++k) {
+            for (int k = 0; k < kBufs && ok; ++k) {
                 if (r == me) {
-                    mapped[(size_t)r * 6 + k] = mine[k];
+                    mapped[(size_t)r * kBufs + k] = mine[k];
                     continue;
                 }
                 hipIpcMemHandle_t h;
                 std::memcpy(&h, all + (size_t)r * kHandles + k * sizeof(h), sizeof(h));
-                if (hipIpcOpenMemHandle(&mapped[(size_t)r * 6 + k], h, hipIpcMemLazyEnablePeerAccess) == hipSuccess)
-                    opened.push_back(mapped[(size_t)r * 6 + k]);
+                if (hipIpcOpenMemHandle(&mapped[(size_t)r * kBufs + k], h, hipIpcMemLazyEnablePeerAccess) == hipSuccess)
+                    opened.push_back(mapped[(size_t)r * kBufs + k]);
                 else
                     ok = false;
             }
         (void)hipGetLastError();
         if (!ok) return false;
         for (int r = 0; r < W; ++r) {
-            void *const *p = &mapped[(size_t)r * 6];
+            void *const *p = &mapped[(size_t)r * kBufs];
             pv.T[r] = static_cast<const double *>(p[0]);
             pv.ga[r] = static_cast<unsigned long long *>(p[1]);
             pv.gb[r] = static_cast<unsigned long long *>(p[2]);
             pv.gdone[r] = static_cast<unsigned long long *>(p[3]);
             pv.U[r] = static_cast<double *>(p[4]);
             pv.d[r] = static_cast<double *>(p[5]);
+            pv.F[r] = static_cast<const double *>(p[6]);
         }
         return true;
     }
@@ -1049,8 +1053,9 @@ class Engine {
     }
 
     // pivots per sweep: the configured batch (1 while tracing every pivot); two stages (SX_KMAX)
-    // only in one shard's fused batch -- the per-pivot kernels, the vector sweep and the
-    // multi-rank batch hold one stage (run_phase caps it again when the batch is not fused)
+    // only in the fused batches -- one shard's and the peer-memory multi-rank one; the per-pivot
+    // kernels and the vector sweep hold one stage (run_phase caps it again when the batch is not
+    // fused)
     // Default: two stages when the tableau has >= 4096 rows -- the second stage's longer chains
     // (+0.7 to +1.4 us per pivot, the first stage's 32 pending pivots applied on the fly) cost
     // less than the sweep they save (same box: config 5 27.6 -> 15.4 us of sweep per pivot,
@@ -1058,7 +1063,12 @@ class Engine {
     int batch_size() const {
         if (on_pivot) return 1;
         const int want = g_cfg.batch > 0 ? g_cfg.batch : (m >= 4096 ? SX_KMAX : SX_HMAX);
-        const int cap = (!xchg && sh.size() == 1 && g_cfg.fused != 0) ? SX_KMAX : SX_HMAX;
+        if (g_cfg.mr_two_stage < 0) {
+            const char *e = getenv("SIMPLEX_MR_STAGES");
+            g_cfg.mr_two_stage = (e && atoi(e) == 1) ? 0 : 1;
+        }
+        const bool two_stage = g_cfg.fused != 0 && ((!xchg && sh.size() == 1) || (xchg && p2p && g_cfg.mr_two_stage));
+        const int cap = two_stage ? SX_KMAX : SX_HMAX;
         return std::max(1, std::min(want, cap));
     }
 
@@ -1225,7 +1235,7 @@ class Engine {
             for (auto &x : sh) {
                 DevGuard g(x.dev);
                 sx_launch_activate(x.perm, x.iperm, x.act, x.nact, m, x.T, x.rows, x.row0, ld, tl, 1 + n, pending(x), x.st,
-                                   x.s);
+                                   q_host, x.s);
             }
         if (ev0) SX_HIP(hipEventRecord(ev0, s));
         for (auto &x : sh) {

@@ -1665,7 +1665,8 @@ __device__ __forceinline__ double ld_sys(const double *p) {
 __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const double *__restrict__ T, int rows, int row0,
                                               int rpr, size_t ld, TLay tl, Cols c, double *__restrict__ d,
                                               double *__restrict__ d_save, int *base, DevState *st, double *U, double *F,
-                                              PivRec *recs, unsigned long long *PM, unsigned B, int K, int slots, int W,
+                                              PivRec *recs, unsigned long long *PM, unsigned long long *PM2, unsigned B,
+                                              int K, int slots, int W,
                                               int rank, int tb0, int tb1, int NBg, BatchChan *ch, const u64 *ga,
                                               const u64 *gb, const u64 *gdone, PeerView pv,
                                               unsigned long long timeout) {
@@ -1675,6 +1676,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
     __shared__ double s_p[SX_KMAX];
     __shared__ int s_r[SX_KMAX], s_e[SX_KMAX];
     __shared__ double s_ue[SX_KMAX], s_fr[SX_KMAX];
+    __shared__ double s_ue1[SX_HMAX], s_fr1[SX_HMAX];  // the first stage's U[s][e] / F[r][s] (second stage)
     __shared__ double s_a[SX_TILE], s_b[SX_TILE];
     __shared__ unsigned s_g[4 * SX_TILE];
     __shared__ unsigned s_pay[SX_TILE];
@@ -1713,24 +1715,55 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
         if (liveB) d_save[1 + ia] = dj;
         if (!isA && tb == 0 && t == 0) d_save[0] = d0;
         double b = liveA ? T[tl.idx(li, 0)] : 0.0;
-        unsigned bits = 0u;
+        unsigned bits = 0u;   // slots of this stage where this row left the basis
+        unsigned bits1 = 0u;  // ... of the first stage (second stage)
+        double h1[SX_HMAX];   // this thread's first-stage history (second stage)
+#pragma unroll
+        for (int s1 = 0; s1 < SX_HMAX; ++s1) h1[s1] = 0.0;
+        int hb = 0;  // first slot of the current stage
         // the entering column's stored value of this row: loaded as soon as the entering
         // variable is known, so the load overlaps the wait for its pending history
         double a_pre = liveA ? T[tl.idx(li, c.map(1 + (e >= 0 ? e : 0)))] : 0.0;
-        for (int q = 0; q < K; ++q) {
-            const unsigned tag = make_tag(B, q);
-            if (cap >= 0 && piv0 + q >= cap) {
-                status = SX_PIVOT_CAP;
-                break;
-            }
-            if (inj != 0u && isA && rank == 0 && bid == 0 && (unsigned)q + 1u == inj) {  // test hook
-                if (t == 0) __hip_atomic_store(&ch->abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                aborted = true;
-                break;
-            }
-            if (isA) {
+        // The two roles run separate loops (the same steps per pivot, as k_batch), so neither
+        // role's registers are held across the other's code.
+        if (isA) {
+            for (int q = 0; q < K; ++q) {
+                const unsigned tag = make_tag(B, q);
+                if (cap >= 0 && piv0 + q >= cap) {
+                    status = SX_PIVOT_CAP;
+                    break;
+                }
+                if (inj != 0u && isA && rank == 0 && bid == 0 && (unsigned)q + 1u == inj) {  // test hook
+                    if (t == 0) __hip_atomic_store(&ch->abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    aborted = true;
+                    break;
+                }
+                if (q == SX_HMAX) {
+                    // the stage switch (k_batch's, at system scope): this thread's first-stage history
+                    // to registers, the LDS history reused.  Every thread's stores acknowledged -- the
+                    // objective tiles' U rows (write-through into every rank), the ratio tiles' F --
+                    // then one system-scope release writes this device's L2 back, before any
+                    // second-stage record: a block that has seen one reads the first stage's U[s][e]
+                    // (its own rank's U) and F[r][s] (the owner's F) with system-scope loads
+    #pragma unroll
+                    for (int s1 = 0; s1 < SX_HMAX; ++s1) h1[s1] = s_hist[s1 * SX_TILE + t];
+                    bits1 = bits;
+                    bits = 0u;
+                    if (t < SX_HMAX) s_ue1[t] = s_ue[t];  // (U[s][e] of pivot SX_HMAX: its objective record)
+                    drain();
+                    __syncthreads();
+                    if (t == 0) {
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                        drain();
+                    }
+                    __syncthreads();
+                    hb = SX_HMAX;
+                }
+                const int qq = q - hb;  // slot within the stage
                 const bool done = !(cmp_eps(dmin, 0.0) < 0);  // solver.cu:88: optimal
-                const double a = done ? 0.0 : hist_col(a_pre, q, bits, s_hist, s_ue, s_p);
+                double a1 = a_pre;
+                if (hb && !done) a1 = stage1_col(a1, h1, bits1, s_ue1, s_p);
+                const double a = done ? 0.0 : hist_col(a1, qq, bits, s_hist, s_ue, s_p + hb);
                 double rv = DBL_MAX;
                 int ri = -1, elig = 0;
                 if (liveA && !done) {
@@ -1767,7 +1800,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                     // the record into every rank's copy
                     const unsigned pl = (wi >= 0 ? (unsigned)(wi - gt * SX_TILE) : SX_NOIDX) | ((unsigned)any << 10);
                     // granule-major over the ranks: the value granules reach every rank first
-                    const int nG = kRF + 2 * q;
+                    const int nG = kRF + 2 * qq;
                     for (int idx = t; idx < W * nG; idx += 64) {
                         const int k = idx / W, rk = idx - k * W;
                         unsigned data;
@@ -1797,13 +1830,20 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                     int ei = -1, any = 0;
                     if (ok) wave_pass2(s_g, s_pay, NBg, s_v, s_i, ev, ei, any);
                     ei = __builtin_amdgcn_readfirstlane(ei);
+                    // second stage: the next entering column's first-stage pivot-row values U[s][e]
+                    // from this rank's U (written through by every rank before the stage switch),
+                    // loaded while the record is polled
+                    u64 ue1 = 0ull;
+                    if (hb && ok && ei >= 0 && t < SX_HMAX)
+                        ue1 = ld_sys(reinterpret_cast<const u64 *>(U + (size_t)t * ld + c.map(1 + ei)));
                     if (ok) {
                         const int wt = ei >= 0 ? ei / SX_TILE : 0;
                         ok = poll_wave<decltype(ident), true>(gb + (size_t)wt * SX_GB_STRIDE + kOP,
-                                                              (kOU - kOP) + 2 * (q + 1), ident, tag, s_g, &ch->abort_w,
+                                                              (kOU - kOP) + 2 * (qq + 1), ident, tag, s_g, &ch->abort_w,
                                                               timeout, (unsigned *)nullptr);
-                        if (ok && t <= q) s_ue[t] = gd(s_g[kOU - kOP + 2 * t], s_g[kOU - kOP + 1 + 2 * t]);
+                        if (ok && t <= qq) s_ue[t] = gd(s_g[kOU - kOP + 2 * t], s_g[kOU - kOP + 1 + 2 * t]);
                     }
+                    if (hb && t < SX_HMAX) s_ue1[t] = __longlong_as_double((long long)ue1);
                     if (t == 0) {
                         s_ent_ok = ok;
                         s_ent_e = ei;
@@ -1836,13 +1876,13 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 }
                 cnt = q + 1;
                 const double f = -a / p;
-                s_hist[q * SX_TILE + t] = f;
+                s_hist[qq * SX_TILE + t] = f;
                 if (liveA) {
                     F[sx_fidx(li, q)] = f;
                     if (row0 + li == r) {
                         b = b / p;
-                        bits |= 1u << q;
-                        PM[li] = ((u64)B << 32) | bits;  // (as k_batch: written, not read-modified)
+                        bits |= 1u << qq;
+                        (hb ? PM2 : PM)[li] = ((u64)B << 32) | bits;  // (as k_batch: written, not read-modified)
                     } else {
                         b = fma(f, br, b);
                     }
@@ -1857,7 +1897,41 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 dmin = s_ent_v;
                 if (liveA) a_pre = T[tl.idx(li, s_ent_m)];  // (as k_batch)
                 __syncthreads();
-            } else {
+            }
+        } else {
+            for (int q = 0; q < K; ++q) {
+                const unsigned tag = make_tag(B, q);
+                if (cap >= 0 && piv0 + q >= cap) {
+                    status = SX_PIVOT_CAP;
+                    break;
+                }
+                if (inj != 0u && isA && rank == 0 && bid == 0 && (unsigned)q + 1u == inj) {  // test hook
+                    if (t == 0) __hip_atomic_store(&ch->abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    aborted = true;
+                    break;
+                }
+                if (q == SX_HMAX) {
+                    // the stage switch (k_batch's, at system scope): this thread's first-stage history
+                    // to registers, the LDS history reused.  Every thread's stores acknowledged -- the
+                    // objective tiles' U rows (write-through into every rank), the ratio tiles' F --
+                    // then one system-scope release writes this device's L2 back, before any
+                    // second-stage record: a block that has seen one reads the first stage's U[s][e]
+                    // (its own rank's U) and F[r][s] (the owner's F) with system-scope loads
+    #pragma unroll
+                    for (int s1 = 0; s1 < SX_HMAX; ++s1) h1[s1] = s_hist[s1 * SX_TILE + t];
+                    bits1 = bits;
+                    bits = 0u;
+                    if (t < SX_HMAX) s_ue1[t] = s_ue[t];  // (U[s][e] of pivot SX_HMAX: its objective record)
+                    drain();
+                    __syncthreads();
+                    if (t == 0) {
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                        drain();
+                    }
+                    __syncthreads();
+                    hb = SX_HMAX;
+                }
+                const int qq = q - hb;  // slot within the stage
                 // ---- selection: pass 2 over every rank's ratio tiles (wave 0 polls and reduces)
                 if (t < 64) {
                     const int ok = poll_wave<decltype(gather_a), true>(ga, 2 * NAg, gather_a, tag, s_g, &ch->abort_w,
@@ -1885,14 +1959,22 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                     u = owner == rank ? *src : ld_sys(src);
                 }
                 // the winner's record (ratio tile 0's when there is none): d_e, p, the RHS, e, the
-                // ratio side's status and F[r][s < q], read by wave 0 into LDS
+                // ratio side's status and F[r][s < q] of this stage, read by wave 0 into LDS
                 if (t < 64) {
                     const int wt = r >= 0 ? r / SX_TILE : 0;
+                    // second stage: the leaving row's first-stage factors F[r][s] from its owner's F
+                    // (written back before the stage switch), loaded while the record is polled
+                    u64 fr1 = 0ull;
+                    if (hb && t < SX_HMAX && r >= 0) {
+                        const int owner = r / rpr;
+                        fr1 = ld_sys(reinterpret_cast<const u64 *>(pv.F[owner] + sx_fidx(r - owner * rpr, t)));
+                    }
                     const int ok = poll_wave<decltype(ident), true>(ga + (size_t)wt * SX_GA_STRIDE + kRD,
-                                                                    (kRF - kRD) + 2 * q, ident, tag, s_g, &ch->abort_w,
+                                                                    (kRF - kRD) + 2 * qq, ident, tag, s_g, &ch->abort_w,
                                                                     timeout, (unsigned *)nullptr);
+                    if (hb && t < SX_HMAX) s_fr1[t] = __longlong_as_double((long long)fr1);
                     if (ok) {
-                        if (t < q) s_fr[t] = gd(s_g[kRF - kRD + 2 * t], s_g[kRF - kRD + 1 + 2 * t]);
+                        if (t < qq) s_fr[t] = gd(s_g[kRF - kRD + 2 * t], s_g[kRF - kRD + 1 + 2 * t]);
                         if (t == 0) {
                             s_det_dmin = gd(s_g[0], s_g[1]);
                             s_p[q] = gd(s_g[kRA - kRD], s_g[kRA - kRD + 1]);
@@ -1927,8 +2009,9 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 int i = -1;
                 if (ost == SX_NOT_ENDED) {
                     cnt = q + 1;
-                    u = hist_row(u, q, r, s_hist, s_fr, s_p, s_r);
-                    s_hist[q * SX_TILE + t] = u;
+                    if (hb) u = stage1_row(u, h1, r, s_fr1, s_p, s_r);
+                    u = hist_row(u, qq, r, s_hist, s_fr, s_p + hb, s_r + hb);
+                    s_hist[qq * SX_TILE + t] = u;
                     const double fd = -dmin / p;  // updateCostsVector, solver.cu:48-56
                     if (tb == 0 && t == 0) d0 = fma(fd, br, d0);
                     if (liveB) {
@@ -1956,7 +2039,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                     const int win = wi >= 0 ? wi - tb * SX_TILE : 0;
                     const unsigned pl = wi >= 0 ? (unsigned)win : SX_NOIDX;
                     // granule-major over the ranks: the value granules reach every rank first
-                    const int nG = kOU + 2 * (q + 1);
+                    const int nG = kOU + 2 * (qq + 1);
                     for (int idx = t; idx < W * nG; idx += 64) {
                         const int k = idx / W, rk = idx - k * W;
                         unsigned data;
@@ -1978,7 +2061,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 // the pivot row into every rank's U[q] (the sweep's input, read after the batch):
                 // issued behind the record, so the W-fold stores do not delay it
                 if (ost == SX_NOT_ENDED && liveB && 1 + ia < c.Ns) {
-                    const double uq = s_hist[q * SX_TILE + t];
+                    const double uq = s_hist[qq * SX_TILE + t];
                     for (int k = 0; k < W; ++k) st_sys(pv.U[k] + (size_t)q * ld + mj, uq);
                 }
                 if (ost != SX_NOT_ENDED) {
@@ -2070,11 +2153,11 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
 __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, int rows, int row0, int rpr, size_t ld, TLay tl,
                                                   Cols c, double *__restrict__ d, double *__restrict__ d_save, int *base,
                                                   DevState *st, double *U, double *F, PivRec *recs,
-                                                  unsigned long long *PM, unsigned B, int K,
+                                                  unsigned long long *PM, unsigned long long *PM2, unsigned B, int K,
                                                   int slots, int W, int rank, int tb0, int tb1, int NBg,
                                                   BatchChan *ch, const u64 *ga, const u64 *gb, const u64 *gdone,
                                                   PeerView pv, unsigned long long timeout) {
-    batch_mr_body((int)blockIdx.x, gridDim.x, T, rows, row0, rpr, ld, tl, c, d, d_save, base, st, U, F, recs, PM, B, K,
+    batch_mr_body((int)blockIdx.x, gridDim.x, T, rows, row0, rpr, ld, tl, c, d, d_save, base, st, U, F, recs, PM, PM2, B, K,
                   slots, W, rank, tb0, tb1, NBg, ch, ga, gb, gdone, pv, timeout);
 }
 
@@ -2093,7 +2176,7 @@ struct MrRank {
     DevState *st;
     double *U, *F;
     PivRec *recs;
-    unsigned long long *PM;
+    unsigned long long *PM, *PM2;
     BatchChan *ch;
     const u64 *ga, *gb, *gdone;
 };
@@ -2110,7 +2193,7 @@ __global__ __launch_bounds__(512) void k_batch_mr_multi(MrRanks R, int nloc, int
     Cols cx = c;
     cx.perm = x.perm;
     batch_mr_body((int)blockIdx.x - R.first[k], (unsigned)(R.first[k + 1] - R.first[k]), x.T, x.rows, x.row0, rpr, ld,
-                  tl, cx, x.d, x.d_save, x.base, x.st, x.U, x.F, x.recs, x.PM, B, K, slots, W, x.rank, x.tb0, x.tb1,
+                  tl, cx, x.d, x.d_save, x.base, x.st, x.U, x.F, x.recs, x.PM, x.PM2, B, K, slots, W, x.rank, x.tb0, x.tb1,
                   NBg, x.ch, x.ga, x.gb, x.gdone, pv, timeout);
 }
 
@@ -2456,13 +2539,19 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
 // applied at once: to the pending pivot rows U[s] (whose entries at the two columns are
 // the leaving rows' current values there), to T (zeros and ones of the unit vectors, this
 // shard's rows only) and to perm / iperm / act / nact.  The shards run it alike.
+// A batch of more than SX_HMAX pivots is activated in two passes (sb = 0, then sb = SX_HMAX, from
+// the state the first left -- the same exchanges in slot order, as the fused batch's last block
+// does): a pass lists the exchanges of the slots [sb, sb + SX_HMAX) -- at most 2 entries per slot,
+// one per lane -- and swaps the entries of every pending row U[s], s < cnt.
 __global__ __launch_bounds__(256) void k_activate(int *__restrict__ perm, int *__restrict__ iperm,
                                                   unsigned char *__restrict__ act, int *__restrict__ nact_p, int m,
                                                   double *__restrict__ T, int rows, int row0, size_t ld, TLay tl,
                                                   int s0, double *__restrict__ U, const PivRec *__restrict__ recs,
-                                                  const DevState *__restrict__ st, unsigned B) {
+                                                  const DevState *__restrict__ st, unsigned B, int sb) {
     const int cnt = st->batch_tag == B ? st->batch_count : 0;
-    if (cnt <= 0) return;
+    if (cnt <= sb) return;
+    const int pc = cnt - sb < SX_HMAX ? cnt - sb : SX_HMAX;  // this pass's slots
+    recs += sb;
     const int t = threadIdx.x;
     const int na0 = *nact_p;
     __shared__ int s_pl[64], s_ol[64], s_cl[64], s_src[64];
@@ -2472,7 +2561,7 @@ __global__ __launch_bounds__(256) void k_activate(int *__restrict__ perm, int *_
         // lane s: slot s's leaving row, whether its slack was ever touched, its stored offset,
         // and the slack at window offset na0 + s
         int r = 0, a = 1, pr = 0, win = -1;
-        if (t < cnt) {
+        if (t < pc) {
             r = recs[t].r;
             a = act[r];
             pr = perm[r];
@@ -2480,7 +2569,7 @@ __global__ __launch_bounds__(256) void k_activate(int *__restrict__ perm, int *_
         }
         int pl = -1, ol = -1, cl = -1;  // this lane's list entry
         int nl = 0, added = 0;
-        for (int s = 0; s < cnt; ++s) {
+        for (int s = 0; s < pc; ++s) {
             const int rs = __shfl(r, s);
             if (__shfl(a, s)) continue;  // its slack was touched in an earlier batch
             // already moved into the window in this batch?
@@ -2799,8 +2888,11 @@ static void launch_sweep_k(int rb, int pol, double *T, int rows, size_t ld, TLay
 }
 
 void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, int m, double *T, int rows, int row0,
-                        size_t ld, TLay tl, int s0, const Pending &pd, const DevState *st, hipStream_t s) {
-    k_activate<<<1, 256, 0, s>>>(perm, iperm, act, nact, m, T, rows, row0, ld, tl, s0, pd.U, pd.recs, st, pd.batch);
+                        size_t ld, TLay tl, int s0, const Pending &pd, const DevState *st, int slots, hipStream_t s) {
+    k_activate<<<1, 256, 0, s>>>(perm, iperm, act, nact, m, T, rows, row0, ld, tl, s0, pd.U, pd.recs, st, pd.batch, 0);
+    if (slots > SX_HMAX)
+        k_activate<<<1, 256, 0, s>>>(perm, iperm, act, nact, m, T, rows, row0, ld, tl, s0, pd.U, pd.recs, st, pd.batch,
+                                     SX_HMAX);
 }
 
 void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, const int *nact, int s0,
@@ -2889,7 +2981,7 @@ void sx_launch_batch(const double *T, int rows, size_t ld, TLay tl, Cols c, doub
 }
 
 bool sx_batch_mr_fits(int slots, int nb_local, int k, int grids) {
-    if (k < 1 || k > SX_HMAX || slots < 1 || slots > SX_TILE) return false;  // (one stage)
+    if (k < 1 || k > SX_KMAX || slots < 1 || slots > SX_TILE) return false;  // (two stages at most)
     static int per_cu[SX_KMAX + 1] = {0};
     static int cus = 0;
     if (per_cu[k] == 0) {
@@ -2920,7 +3012,7 @@ void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld,
     if (W < 1 || W > SX_MAXW || W * slots > SX_TILE || NBg > SX_TILE || NBg < 1 || tb0 < 0 || tb1 > NBg || tb0 > tb1)
         SX_FATAL("multi-rank fused batch: bad shape");
     k_batch_mr<<<slots + (tb1 - tb0), SX_TILE, batch_lds(k), s>>>(T, rows, row0, rpr, ld, tl, c, d, d_save, base, st, pd.U, pd.F,
-                                                                  pd.recs, pd.PM, pd.batch, k, slots, W, rank, tb0,
+                                                                  pd.recs, pd.PM, pd.PM2, pd.batch, k, slots, W, rank, tb0,
                                                                   tb1, NBg, chan, ga, gb, gdone, pv, timeout);
 }
 
@@ -2950,6 +3042,7 @@ void sx_launch_batch_mr_multi(const MrLaunchRank *ranks, int nloc, int W, int rp
         x.F = q.pd.F;
         x.recs = q.pd.recs;
         x.PM = q.pd.PM;
+        x.PM2 = q.pd.PM2;
         x.ch = q.chan;
         x.ga = q.ga;
         x.gb = q.gb;

@@ -134,21 +134,25 @@ def test_hang_recovery_mid_batch(gpu, batch, slot):
     assert tuple(got.pivots) == (2003, 69)
 
 
-def test_hang_recovery_mid_batch_multirank(gpu):
+@pytest.mark.parametrize("batch,slot", [(0, 9), (64, 40)])
+def test_hang_recovery_mid_batch_multirank(gpu, batch, slot):
     """the same inside a peer-memory batch of 2 virtual shards: rank 0's ratio block 0 leaves at
-    slot 9, its peers time out; every shard restores its own slice of d and re-runs the batch"""
+    `slot` (64: in the second stage), its peers time out; every shard restores its own slice of
+    d and re-runs the batch"""
     lib = sx.load()
     p = sx.generateRandomProblem(129, 1513, 77, -100, 100)
     r0 = lib.simplex_hang_recoveries()
     sx.set_virtual_ranks(2)
     sx.set_p2p(1)
+    sx.set_batch(batch)
     lib.simplex_set_hang_inject(2)
-    lib.simplex_set_hang_inject_slot(9)
+    lib.simplex_set_hang_inject_slot(slot)
     try:
         solve_both(*p.arrays())
     finally:
         lib.simplex_set_hang_inject(-1)
         lib.simplex_set_hang_inject_slot(-1)
+        sx.set_batch(0)
         sx.set_p2p(-1)
         sx.set_virtual_ranks(1)
         p.close()

@@ -332,11 +332,12 @@ def test_matrix_core_sweep_virtual_ranks(gpu, W):
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 
-@pytest.mark.parametrize("batch", [1, 16, 32])
+@pytest.mark.parametrize("batch", [1, 16, 32, 40, 64])
 @pytest.mark.parametrize("W", [2, 3, 4, 8])
 def test_p2p_fused_virtual_ranks(gpu, batch, W):
     """the multi-rank fused batch (ranks hand off through each other's memory, objective tiles
-    split across ranks): W virtual shards on one GPU, their launches running at once"""
+    split across ranks): W virtual shards on one GPU, their launches running at once; 40 and 64:
+    two-stage batches (the first stage's operands read from U / the owner's F)"""
     T, d, base = _phase1_state(300, 1100, 11)
     Tg, dg, bg, st, done = _pivots_with({"batch": batch, "W": W, "p2p": 1}, T, d, base, 150)
     st_o, done_o = oracle.solve(T, d, base, max_pivots=150)
@@ -344,9 +345,10 @@ def test_p2p_fused_virtual_ranks(gpu, batch, W):
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 
+@pytest.mark.parametrize("batch", [32, 64])
 @pytest.mark.parametrize("single", [1, 0])
 @pytest.mark.parametrize("W", [2, 3])
-def test_p2p_fused_launch_forms(gpu, W, single):
+def test_p2p_fused_launch_forms(gpu, W, single, batch):
     """the virtual ranks' peer-memory batches as one launch and as one launch per rank on its own
     stream (the RCCL ranks' form): bit-exact, and every batch completed on the fused path (no
     hand-off timed out and fell back to the per-pivot path)"""
@@ -355,7 +357,7 @@ def test_p2p_fused_launch_forms(gpu, W, single):
     h0, f0 = lib.simplex_hang_recoveries(), lib.simplex_fused_batches()
     try:
         sx.set_mr_single_launch(single)
-        Tg, dg, bg, st, done = _pivots_with({"batch": 32, "W": W, "p2p": 1}, T, d, base, 150)
+        Tg, dg, bg, st, done = _pivots_with({"batch": batch, "W": W, "p2p": 1}, T, d, base, 150)
     finally:
         sx.set_mr_single_launch(1)
     st_o, done_o = oracle.solve(T, d, base, max_pivots=150)
@@ -375,6 +377,23 @@ def test_p2p_fused_two_phase(gpu, W, n, m, seed, lo, hi):
         sx.set_p2p(1)
         _check_two_phase(p)
     finally:
+        sx.set_p2p(-1)
+        sx.set_virtual_ranks(1)
+
+
+@pytest.mark.parametrize("W", [2, 3, 8])
+@pytest.mark.parametrize("n,m,seed,lo,hi", [(300, 1100, 41100, 1, 100), (129, 1513, 77, -100, 100)])
+def test_p2p_fused_two_phase_two_stages(gpu, W, n, m, seed, lo, hi):
+    """the same with two-stage (64-pivot) multi-rank batches -- the default from 4096 rows: phase
+    ends inside either stage, slack activation in two passes"""
+    p = sx.generateRandomProblem(n, m, seed, lo, hi)
+    try:
+        sx.set_virtual_ranks(W)
+        sx.set_p2p(1)
+        sx.set_batch(64)
+        _check_two_phase(p)
+    finally:
+        sx.set_batch(0)
         sx.set_p2p(-1)
         sx.set_virtual_ranks(1)
 
