@@ -1652,29 +1652,44 @@ int two_phase(problem_t *P, double *solution, double *opt, int *base_out, long l
 }
 
 // A small instance (n = 300, m = 1100: 1318 + 23 pivots, phases ending mid-batch) solved with the
-// multi-rank fused batch over peer memory and with the per-pivot exchange: true when the fused
-// path ran (no hand-off timed out) and both answers are bit-identical.
+// multi-rank fused batch over peer memory -- in one-stage (32) and two-stage (64-pivot) batches --
+// and with the per-pivot exchange: true when the fused path ran (no hand-off timed out) and every
+// answer is bit-identical.
 bool selftest_solves() {
     problem_t *P = generateRandomProblem(300, 1100, 41100, 1, 100);
     const int n = P->vars, m = P->constraints;
-    std::vector<double> xa(n), xb(n);
-    std::vector<int> ba(m), bb(m);
-    long long pa[2] = {0, 0}, pb[2] = {0, 0};
-    double za = 0.0, zb = 0.0;
-    const int save = g_cfg.p2p;
+    const int save = g_cfg.p2p, save_batch = g_cfg.batch;
     const bool save_nt = g_cfg.no_timer;
-    g_cfg.no_timer = true;  // (timing would switch both solves to the per-pivot path; no CSVs either)
-    g_cfg.p2p = 1;
+    g_cfg.no_timer = true;  // (timing would switch the solves to the per-pivot path; no CSVs either)
+    struct Answer {
+        std::vector<double> x;
+        std::vector<int> base;
+        long long piv[2] = {0, 0};
+        double z = 0.0;
+        int st = 0;
+    };
+    auto solve = [&](int p2p, int batch) {
+        Answer a;
+        a.x.assign(n, 0.0);
+        a.base.assign(m, 0);
+        g_cfg.p2p = p2p;
+        g_cfg.batch = batch;
+        a.st = two_phase(P, a.x.data(), &a.z, a.base.data(), a.piv, -1);
+        return a;
+    };
+    auto same = [&](const Answer &a, const Answer &b) {
+        return a.st == b.st && a.st != SX_HANG && a.piv[0] == b.piv[0] && a.piv[1] == b.piv[1] &&
+               std::memcmp(&a.z, &b.z, sizeof(a.z)) == 0 && a.base == b.base &&
+               std::memcmp(a.x.data(), b.x.data(), sizeof(double) * n) == 0;
+    };
     const long long fb0 = g_cfg.fused_batches, hr0 = g_cfg.hang_recoveries;
-    const int sa = two_phase(P, xa.data(), &za, ba.data(), pa, -1);
+    const Answer a32 = solve(1, SX_HMAX), a64 = solve(1, SX_KMAX);
     const bool went_fused = g_cfg.fused_batches > fb0 && g_cfg.hang_recoveries == hr0;
-    g_cfg.p2p = 0;
-    const int sb = two_phase(P, xb.data(), &zb, bb.data(), pb, -1);
+    const Answer ref = solve(0, 0);
     g_cfg.p2p = save;
+    g_cfg.batch = save_batch;
     g_cfg.no_timer = save_nt;
-    const bool ok = went_fused && sa == sb && sa != SX_HANG && pa[0] == pb[0] && pa[1] == pb[1] &&
-                    std::memcmp(&za, &zb, sizeof(za)) == 0 && ba == bb &&
-                    std::memcmp(xa.data(), xb.data(), sizeof(double) * n) == 0;
+    const bool ok = went_fused && same(a32, ref) && same(a64, ref);
     freeProblem(P);
     free(P);
     return ok;
