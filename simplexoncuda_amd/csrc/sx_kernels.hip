@@ -2496,29 +2496,51 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
         }
     }
     // the leaving rows: row r_s (first slot s where it left) by the row slot s % G, one column
-    // per lane, the guarded chain from its stored values (the strips left them unwritten)
+    // per lane, the guarded chain from its stored values (the strips left them unwritten).
+    // The row slot's rows are found in one round trip (lane k: slot gy + G k), and each row's
+    // operands -- its stored values, the column's pivot-row values (32 slots at a time), the row's
+    // factors and the pivots (lane s: slot s, read by v_readlane) -- are loaded together: one or
+    // two round trips per row instead of one per 16 slots.
     if (cnt <= 0) return;
     const int j = c0 + l;
-    for (int s = gy; s < cnt; s += G) {
-        const int r = recs[s].r - row0;
-        if (r < 0 || r >= rows) continue;
-        const unsigned long long bits = (unsigned long long)pend_bits(PM, r, B, mask) |
-                                        ((unsigned long long)(mask2 ? pend_bits(PM2, r, B, mask2) : 0u) << SX_HMAX);
-        if (bits == 0ull || (int)__builtin_ctzll(bits) != s) continue;  // (not its first slot)
+    int rk = -1;                // lane k: the row of slot gy + G k, if this is its first slot
+    unsigned long long bk = 0;  // ... and its leaving slots
+    {
+        const int sk = gy + G * l;
+        if (sk < cnt) {
+            const int r = recs[sk].r - row0;
+            if (r >= 0 && r < rows) {
+                bk = (unsigned long long)pend_bits(PM, r, B, mask) |
+                     ((unsigned long long)(mask2 ? pend_bits(PM2, r, B, mask2) : 0u) << SX_HMAX);
+                if (bk != 0ull && (int)__builtin_ctzll(bk) == sk) rk = r;
+            }
+        }
+    }
+    const double pl = l < cnt ? recs[l].p : 1.0;  // lane s: p_s
+    unsigned long long todo = __ballot(rk >= 0);
+    while (todo) {
+        const int k = __builtin_ctzll(todo);
+        todo &= todo - 1ull;
+        const int r = __builtin_amdgcn_readlane(rk, k);
+        const unsigned long long bits =
+            ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(bk >> 32), k) << 32) |
+            (unsigned)__builtin_amdgcn_readlane((int)bk, k);
         double x = j < Ns ? Tr[(size_t)r * ldr + cr + l] : 0.0;
-        // (the column's pivot-row values 16 slots at a time: few registers, loads only here)
-        for (int c1 = 0; c1 < cnt; c1 += 16) {
-            double uu[16];
+        const double fl = l < cnt ? F[sx_fidx(r, l)] : 0.0;  // lane s: F[r][s]
+        // (32 slots of the column's pivot-row values at a time: registers)
+        for (int c1 = 0; c1 < cnt; c1 += SX_HMAX) {
+            double uu[SX_HMAX];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) uu[k] = (c1 + k < cnt && j < Ns) ? U[(size_t)(c1 + k) * ld + j] : 0.0;
+            for (int k1 = 0; k1 < SX_HMAX; ++k1)
+                uu[k1] = (c1 + k1 < cnt && j < Ns) ? U[(size_t)(c1 + k1) * ld + j] : 0.0;
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const int sl = c1 + k;
-                if (sl < cnt) {
-                    if ((bits >> sl) & 1ull)
-                        x = x / recs[sl].p;
+            for (int k1 = 0; k1 < SX_HMAX; ++k1) {
+                const int s1 = c1 + k1;
+                if (s1 < cnt) {
+                    if ((bits >> s1) & 1ull)
+                        x = x / rdlane(pl, s1);
                     else
-                        x = fma(F[sx_fidx(r, sl)], uu[k], x);
+                        x = fma(rdlane(fl, s1), uu[k1], x);
                 }
             }
         }
