@@ -2518,15 +2518,29 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
     }
     const double pl = l < cnt ? recs[l].p : 1.0;  // lane s: p_s
     unsigned long long todo = __ballot(rk >= 0);
+    // NR rows at a time (independent chains; within each kernel's register budget: the
+    // two-stage kernel's pivot-row registers are free here, the one-stage kernel keeps its 3
+    // waves per SIMD)
+    constexpr int NR = NKB == SX_KMAX / 4 ? 4 : 2;
     while (todo) {
-        const int k = __builtin_ctzll(todo);
-        todo &= todo - 1ull;
-        const int r = __builtin_amdgcn_readlane(rk, k);
-        const unsigned long long bits =
-            ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(bk >> 32), k) << 32) |
-            (unsigned)__builtin_amdgcn_readlane((int)bk, k);
-        double x = j < Ns ? Tr[(size_t)r * ldr + cr + l] : 0.0;
-        const double fl = l < cnt ? F[sx_fidx(r, l)] : 0.0;  // lane s: F[r][s]
+        int r[NR];
+        unsigned long long bits[NR];
+        bool live[NR];
+#pragma unroll
+        for (int q1 = 0; q1 < NR; ++q1) {
+            live[q1] = todo != 0ull;
+            const int k = live[q1] ? __builtin_ctzll(todo) : 0;
+            if (live[q1]) todo &= todo - 1ull;
+            r[q1] = __builtin_amdgcn_readlane(rk, k);
+            bits[q1] = ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(bk >> 32), k) << 32) |
+                       (unsigned)__builtin_amdgcn_readlane((int)bk, k);
+        }
+        double x[NR], fl[NR];
+#pragma unroll
+        for (int q1 = 0; q1 < NR; ++q1) {
+            x[q1] = (live[q1] && j < Ns) ? Tr[(size_t)r[q1] * ldr + cr + l] : 0.0;
+            fl[q1] = (live[q1] && l < cnt) ? F[sx_fidx(r[q1], l)] : 0.0;  // lane s: F[r][s]
+        }
         // (32 slots of the column's pivot-row values at a time: registers)
         for (int c1 = 0; c1 < cnt; c1 += SX_HMAX) {
             double uu[SX_HMAX];
@@ -2537,18 +2551,25 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
             for (int k1 = 0; k1 < SX_HMAX; ++k1) {
                 const int s1 = c1 + k1;
                 if (s1 < cnt) {
-                    if ((bits >> s1) & 1ull)
-                        x = x / rdlane(pl, s1);
-                    else
-                        x = fma(rdlane(fl, s1), uu[k1], x);
+#pragma unroll
+                    for (int q1 = 0; q1 < NR; ++q1) {
+                        if ((bits[q1] >> s1) & 1ull)
+                            x[q1] = x[q1] / rdlane(pl, s1);
+                        else
+                            x[q1] = fma(rdlane(fl[q1], s1), uu[k1], x[q1]);
+                    }
                 }
             }
         }
-        const __amdgpu_buffer_rsrc_t rsr =
-            __builtin_amdgcn_make_buffer_rsrc(Tw + (size_t)r * ldr, 0, (int)(ldr * 8), 0x00020000);
-        const unsigned long long xb = (unsigned long long)__double_as_longlong(x);
-        const u32x2 w = {(unsigned)xb, (unsigned)(xb >> 32)};
-        __builtin_amdgcn_raw_buffer_store_b64(w, rsr, j < Ns ? (cr + l) * 8 : OOB, 0, 16);  // (write-through, as the strips)
+#pragma unroll
+        for (int q1 = 0; q1 < NR; ++q1) {
+            if (!live[q1]) continue;
+            const __amdgpu_buffer_rsrc_t rsr =
+                __builtin_amdgcn_make_buffer_rsrc(Tw + (size_t)r[q1] * ldr, 0, (int)(ldr * 8), 0x00020000);
+            const unsigned long long xb = (unsigned long long)__double_as_longlong(x[q1]);
+            const u32x2 w = {(unsigned)xb, (unsigned)(xb >> 32)};
+            __builtin_amdgcn_raw_buffer_store_b64(w, rsr, j < Ns ? (cr + l) * 8 : OOB, 0, 16);  // (write-through, as the strips)
+        }
     }
 }
 
