@@ -2891,8 +2891,8 @@ static int sweep_capacity() {
 static float g_sweep_waves = 1.0f;
 void sx_set_update_waves(float w) { g_sweep_waves = w > 0.f ? w : 1.0f; }
 
-static int row_slots(int capacity, int col_blocks, int rows, int rb) {
-    long long g = (long long)(g_sweep_waves * (float)capacity) / col_blocks;
+static int row_slots(int capacity, int col_blocks, int rows, int rb, float waves = -1.f) {
+    long long g = (long long)((waves > 0.f ? waves : g_sweep_waves) * (float)capacity) / col_blocks;
     const long long groups = rows > 0 ? (rows + rb - 1) / rb : 1;
     if (g > groups) g = groups;
     if (g < 1) g = 1;
@@ -2930,6 +2930,18 @@ static void launch_sweep_k(int rb, int pol, double *T, int rows, size_t ld, TLay
     launch_sweep_rb<KT, 1>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
 }
 
+// Row slots of the matrix-core sweeps (measured, profiles/r03_msweep_waves_ab.txt): the one-stage
+// kernel with 2 of its 3 resident blocks per CU (4096 x 8192: 87-90 vs 95-100 us; the same at
+// 32768 rows); the two-stage kernel with twice its resident grid when each block would walk 64
+// strips or more (32768 x 9216: 974 vs 1006 us; at 4096 rows the resident grid stays best).  An
+// explicit simplex_set_update_waves overrides both.
+static int msweep_slots(int capacity, int cb, int rows, bool two_stage) {
+    if (g_sweep_waves != 1.0f) return row_slots(capacity, cb, rows, 16);
+    if (!two_stage) return row_slots(capacity, cb, rows, 16, 2.0f / 3.0f);
+    const long long nstrip = (rows + 15) / 16, g0 = std::max(1, capacity / std::max(cb, 1));
+    return row_slots(capacity, cb, rows, 16, nstrip / g0 >= 64 ? 2.0f : 1.0f);
+}
+
 void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, int m, double *T, int rows, int row0,
                         size_t ld, TLay tl, int s0, const Pending &pd, const DevState *st, int slots, hipStream_t s) {
     k_activate<<<1, 256, 0, s>>>(perm, iperm, act, nact, m, T, rows, row0, ld, tl, s0, pd.U, pd.recs, st, pd.batch, 0);
@@ -2946,11 +2958,11 @@ void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, 
             SX_FATAL("matrix-core sweep: 16-byte rows and 256-aligned regions required");
         const int cb = (Ns + 255) / 256;
         if (cfg.batch > SX_HMAX) {
-            dim3 grid(cb, row_slots(sweep_capacity<k_msweep<SX_KMAX / 4>>(), cb, rows, 16));
+            dim3 grid(cb, msweep_slots(sweep_capacity<k_msweep<SX_KMAX / 4>>(), cb, rows, true));
             k_msweep<SX_KMAX / 4><<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM,
                                                        pd.PM2, st, nullptr, pd.batch, rev, g_sweep_rec);
         } else {
-            dim3 grid(cb, row_slots(sweep_capacity<k_msweep<SX_HMAX / 4>>(), cb, rows, 16));
+            dim3 grid(cb, msweep_slots(sweep_capacity<k_msweep<SX_HMAX / 4>>(), cb, rows, false));
             k_msweep<SX_HMAX / 4><<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM,
                                                        pd.PM2, st, nullptr, pd.batch, rev, g_sweep_rec);
         }
