@@ -4,8 +4,8 @@ Workload (BASELINE.json configs[4], the m=32768 problem north_star's scaling tar
 quoted on): generateRandomProblem(n=8192, m=32768, seed=851968, [1,100]) -- seed n*100+m as
 the reference's -t sweep (main.cu:56-64) -- phase-1 tableau 32768 x 73729 fp64, synthesised
 in HBM (10.7 GB stored: artificial columns aliased to their slack columns).
-A "step" is one pass of the hot path over the tableau: one batch of simplex pivots (64 on one
-GPU: two stages of 32; 32 per batch on several) -- entering argmin, ratio test,
+A "step" is one pass of the hot path over the tableau: one batch of simplex pivots (64: two
+stages of 32, DESIGN.md §3, on one GPU and on several) -- entering argmin, ratio test,
 pivot row and objective row of each -- followed by one sweep that applies their rank-1 updates
 to every stored tableau element.  W untimed steps, then K timed steps: by default about the
 first 2000 phase-1 pivots after the warmup (the scaling curve is the first 2000
