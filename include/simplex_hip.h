@@ -19,6 +19,7 @@ extern "C" {
 #define SIMPLEX_PIVOT_CAP -11    /* opt-in pivot budget reached */
 #define SIMPLEX_NUMERIC_FAIL -12 /* eligible pivot but the ratio argmin found no row */
 #define SIMPLEX_HANG -13         /* fused batch: an in-kernel hand-off timed out (never expected) */
+#define SIMPLEX_MAX_GPUS 8        /* shards (GPUs) one solve can use: simplex_set_gpus, SIMPLEX_GPUS, --gpus */
 
 /* ---- configuration ---- */
 int simplex_version(void);
@@ -30,9 +31,10 @@ void simplex_set_store_sc1(int mode);
 /* the sweep on the matrix cores (v_mfma_f64_16x16x4f64, bit-identical to the vector chain):
  * -1 auto (matrix cores), 0 vector sweep (batches of at most 32), 1 matrix-core sweep */
 void simplex_set_sweep_mfma(int mode);
-/* pivots per tableau sweep (1..64; 0 = default: 64 in one shard's fused batch of a tableau with
- * >= 4096 rows -- two stages of 32, applied by the matrix-core sweep -- else 32; more than 32
- * only in one shard's fused batch): the pivots of a batch are selected on the
+/* pivots per tableau sweep (1..64; 0 = auto: 64 when the tableau has >= 4096 rows -- two stages
+ * of 32, applied by the matrix-core sweep -- else 32; more than 32 only in the fused batches, one
+ * shard's and the peer-memory multi-rank one, the per-pivot path caps it at 32): the pivots of a
+ * batch are selected on the
  * current values (pending pivots applied on the fly) and then applied to the tableau in one
  * sweep -- the same IEEE operations in the same order as one sweep per pivot */
 void simplex_set_batch(int pivots);
@@ -88,6 +90,11 @@ int simplex_p2p_ready(void);
 /* wall time (s) of the last twoPhaseMethod call's two pivot loops (solve calls): out[0] phase 1,
  * out[1] phase 2 -- the reference's TIMER CSV reports the two phases separately */
 void simplex_last_phase_seconds(double *out);
+/* the last twoPhaseMethod call's final objective row d[0, N) in logical columns (N = 1+n+m after
+ * phase 2, 1+n+2m when phase 1 ended the solve): copies min(N, cap) entries, returns N.  After a
+ * FEASIBLE solve, d[1+n+i] = y_i (the dual of constraint i, also for the rows negated by the b < 0
+ * quirk, twoPhaseMethod.cu:100-111) and d[1+j] = (A^T y)_j - c_j: a dual certificate */
+long long simplex_last_objective_row(double *out, long long cap);
 /* the sweep's grid: waves x (blocks resident on the device) blocks (default 1; <= 0 resets) */
 void simplex_set_update_waves(double waves);
 /* new engines' tableau layout: plain row-major rows (0), the two-region layout when aliasing and
@@ -207,7 +214,9 @@ int simplex_ipc_session_connect(simplex_session *s, const unsigned char *all_han
  * (between fused batches each rank keeps only its own slice current); barrier the processes
  * before and after.  Returns 0, or -1 for a session that is not in IPC mode. */
 int simplex_session_sync_d(simplex_session *s);
-/* this process's rows of the resident tableau (logical columns), d and base; returns rows */
+/* this process's rows of the resident tableau (logical columns), d and base; returns rows, -1 for
+ * ld_host < N, -2 for an IPC session whose objective row is split after its pivots (call
+ * simplex_session_sync_d in every process first) */
 long long simplex_session_rows(simplex_session *s, double *T_rows, long long ld_host, double *d, int *base);
 
 /* ---- kernel bench (SURVEY.md §8d config 3') ---- */

@@ -7,7 +7,7 @@ thin Python mirror of that API; see DESIGN.md.
 from .api import (  # noqa: F401
     DEGENERATE, FEASIBLE, HANG, INFEASIBLE, NOT_ENDED, NUMERIC_FAIL, PIVOT_CAP, RAND_GLIBC, RAND_MSVC,
     STATUS_NAMES, UNBOUNDED, Problem, Result, Session, bench_sweep, dev_argmin, dev_build_phase1,
-    dev_build_phase1_generated, dev_pivots, dev_update_objective, generateRandomProblem,
+    dev_build_phase1_generated, dev_pivots, dev_update_objective, generateRandomProblem, last_objective_row,
     generateRandomProblemDevice, gpus, p2p_ready, printProblemToStream, readProblemFromFile, readRandomProblemFromFile,
     set_alias, set_batch, set_compact, set_exchange_mode, set_force_exchange, set_fused, set_mr_single_launch,
     set_gpus, set_p2p, set_regions, set_store_sc1, set_sweep_mfma, set_update_rows, set_update_waves, set_verbose, set_virtual_ranks,

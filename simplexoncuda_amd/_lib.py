@@ -101,6 +101,7 @@ SIGNATURES = {
     "simplex_set_compact": (None, [ctypes.c_int]),
     "simplex_set_fused": (None, [ctypes.c_int]),
     "simplex_last_phase_seconds": (None, [ctypes.POINTER(ctypes.c_double)]),
+    "simplex_last_objective_row": (ctypes.c_longlong, [ctypes.POINTER(ctypes.c_double), ctypes.c_longlong]),
     "simplex_set_p2p": (None, [ctypes.c_int]),
     "simplex_p2p_ready": (ctypes.c_int, []),
     "simplex_set_update_waves": (None, [ctypes.c_double]),

@@ -171,6 +171,15 @@ def twoPhaseMethodEx(problem, max_pivots=-1):
     return Result(st, x[:problem.n], opt.value, base[:problem.m], (piv[0], piv[1]))
 
 
+def last_objective_row():
+    """The last twoPhaseMethod call's final objective row (simplex_last_objective_row)."""
+    lib = _lib.load()
+    n = lib.simplex_last_objective_row(None, 0)
+    d = np.zeros(max(n, 1))
+    lib.simplex_last_objective_row(_dp(d), n)
+    return d[:n]
+
+
 class Session:
     """A resident phase-1 tableau on this process's GPU shard, for timed pivots."""
 
@@ -403,5 +412,7 @@ def set_sweep_mfma(mode):
 
 
 def set_batch(p):
-    """Pivots per tableau sweep (1..32; <= 0: default 32)."""
+    """Pivots per tableau sweep (1..64; <= 0: auto -- 64 when the tableau has >= 4096 rows, else 32).
+    Batches above 32 run only in the fused batches (one shard's and the peer-memory multi-rank
+    one); the per-pivot path caps them at 32 (simplex_hip.h simplex_set_batch)."""
     _lib.load().simplex_set_batch(int(p))

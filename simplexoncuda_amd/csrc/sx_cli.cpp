@@ -45,14 +45,33 @@ static problem_t *random_input(int vars, int constraints, int seed) {
     return generate(vars, constraints, (unsigned)seed, MIN_V, MAX_V);
 }
 
-// twoPhaseMethod, or twoPhaseMethodEx under a pivot budget
+// twoPhaseMethod, or twoPhaseMethodEx under a pivot budget.  Returns FEASIBLE / INFEASIBLE /
+// UNBOUNDED / DEGENERATE, or SIMPLEX_PIVOT_CAP under a budget; every other engine outcome is
+// fatal, as twoPhaseMethod itself makes it (error.cu:5-12 convention: message, exit non-zero).
 static int solve_problem(problem_t *p, double *solution, double *optimalValue) {
     if (g_pivot_budget < 0) return twoPhaseMethod(p, solution, optimalValue);
     long long piv[2] = {0, 0};
     const int st = twoPhaseMethodEx(p, solution, optimalValue, nullptr, piv, g_pivot_budget);
-    if (st == SIMPLEX_PIVOT_CAP) printf("\nPivot budget of %lld reached (phase pivots %lld + %lld)\n", g_pivot_budget,
-                                        piv[0], piv[1]);
-    return st;
+    switch (st) {
+    case FEASIBLE:
+    case INFEASIBLE:
+    case UNBOUNDED:
+    case DEGENERATE:
+        return st;
+    case SIMPLEX_PIVOT_CAP:
+        printf("\nPivot budget of %lld reached (phase pivots %lld + %lld)\n", g_pivot_budget, piv[0], piv[1]);
+        return st;
+    case SIMPLEX_NUMERIC_FAIL:
+        fprintf(stderr, "simplex: the ratio test found no leaving row although a pivot is eligible\n");
+        break;
+    case SIMPLEX_HANG:
+        fprintf(stderr, "simplex: a fused-batch hand-off between GPUs timed out\n");
+        break;
+    default:
+        fprintf(stderr, "simplex: unexpected solver status %d\n", st);
+        break;
+    }
+    exit(EXIT_FAILURE);
 }
 
 static void save_random_input(int vars, int constraints, int seed) {
@@ -71,11 +90,11 @@ int main(int argc, const char *argv[]) {
     while (argc > 2 && strncmp(argv[1], "--", 2) == 0) {
         if (strcmp(argv[1], "--gpus") == 0) {
             const int n = atoi(argv[2]);
-            if (n < 1 || n > 64) {
-                fprintf(stderr, "--gpus: expected 1..64\n");
+            if (n < 1 || n > SIMPLEX_MAX_GPUS) {
+                fprintf(stderr, "--gpus: expected 1..%d GPUs, got %s\n", SIMPLEX_MAX_GPUS, argv[2]);
                 exit(-1);
             }
-            int devs[64];
+            int devs[SIMPLEX_MAX_GPUS];
             for (int k = 0; k < n; ++k) devs[k] = k;
             simplex_set_gpus(devs, n);
         } else if (strcmp(argv[1], "--pivot-budget") == 0) {
@@ -168,9 +187,9 @@ int main(int argc, const char *argv[]) {
     case DEGENERATE:
         printf("\nProblem DEGENERATE!\n");
         break;
-    case SIMPLEX_PIVOT_CAP:
+    case SIMPLEX_PIVOT_CAP:  // (no solution: the phase did not finish)
         break;
-    default:
+    case FEASIBLE:
         printf("\nProblem solved!\n");
         for (int i = 0; i < problem->vars; i++) fprintf(fileSolution, "%lf\n", solution[i]);
         fprintf(fileSolution, "\nOptimal value: %lf\n", optimalValue);

@@ -23,6 +23,7 @@
 #include "../../include/simplex_hip.h"
 #include "../../include/twoPhaseMethod.h"
 #include "sx_common.hpp"
+static_assert(SX_MAXW == SIMPLEX_MAX_GPUS, "simplex_hip.h SIMPLEX_MAX_GPUS is the engine's shard limit");
 
 // ------------------------------------------------------------------ errors (error.cu:5-18)
 void sx_handle_error(hipError_t err, const char *file, int line) {
@@ -1410,6 +1411,15 @@ class Engine {
         SX_HIP(hipStreamSynchronize(s));
     }
 
+    // the whole objective row d[0, width) (logical columns)
+    void read_d(std::vector<double> &out, int width) {
+        gather_d();
+        sync_all();
+        out.assign((size_t)width, 0.0);
+        SX_HIP(hipMemcpyAsync(out.data(), sh[0].d, sizeof(double) * width, hipMemcpyDeviceToHost, s));
+        SX_HIP(hipStreamSynchronize(s));
+    }
+
     void write_base(const int *in) {
         for (auto &x : sh) {
             DevGuard g(x.dev);
@@ -1552,6 +1562,7 @@ int public_status(int st) {
 
 // ------------------------------------------------------------------ the two-phase driver
 double g_phase_seconds[2] = {0.0, 0.0};  // wall time of the last solve's pivot loops (P1, P2)
+std::vector<double> g_last_d;             // the last solve's final objective row (its last phase's width)
 
 static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -1609,6 +1620,7 @@ int two_phase(problem_t *P, double *solution, double *opt, int *base_out, long l
         ch.stop(E.s);
     }
     E.read_base(base.data());
+    if (status != FEASIBLE) E.read_d(g_last_d, E.N1);
     if (status == FEASIBLE) {
         // phase2 (:285-356): drop the artificial columns, costs -c / 0, d[0] kept
         say("Phase 2: Filling costs vector with the original one");
@@ -1628,6 +1640,7 @@ int two_phase(problem_t *P, double *solution, double *opt, int *base_out, long l
             print_tableau(stdout, E, E.N2);
         }
         E.read_base(base.data());
+        E.read_d(g_last_d, E.N2);
         if (status == FEASIBLE) {
             // getSolutionHost (:370-383)
             ch.start(E.s, E.N2, m, "solution");
@@ -1752,6 +1765,11 @@ int simplex_p2p_ready(void) {
 void simplex_last_phase_seconds(double *out) {
     out[0] = g_phase_seconds[0];
     out[1] = g_phase_seconds[1];
+}
+long long simplex_last_objective_row(double *out, long long cap) {
+    const long long n = (long long)g_last_d.size();
+    for (long long j = 0; out != nullptr && j < n && j < cap; ++j) out[j] = g_last_d[(size_t)j];
+    return n;
 }
 void simplex_set_update_waves(double waves) { sx_set_update_waves((float)waves); }
 void simplex_set_uncached_exchange(int mode) { g_cfg.uncached_xchg = mode < 0 ? 0 : mode & 3; }
@@ -2177,6 +2195,9 @@ int simplex_session_sync_d(simplex_session *S) {
 long long simplex_session_rows(simplex_session *S, double *T_rows, long long ld_host, double *d, int *base) {
     Engine &E = *S->E;
     if (ld_host < E.N) return -1;
+    // IPC ranks keep only their own slice of d current between fused batches: the whole row
+    // exists only after simplex_session_sync_d (every process) -- refuse a stale read
+    if (E.ipc && E.d_split) return -2;
     E.download(T_rows, (size_t)ld_host, E.N, d, /*local_rows=*/true);
     E.read_base(base);
     return E.sh[0].rows;
