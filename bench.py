@@ -118,7 +118,6 @@ def main():
                     help="timed steps; a step = one batch of pivots + one tableau sweep (0 = about 2016 pivots)")
     ap.add_argument("--warmup", type=int, default=2, help="untimed steps before timing")
     ap.add_argument("--config", default="config5", choices=sorted(CONFIGS))
-    ap.add_argument("--update-rows", type=int, default=0, help="rows per sweep step (0 = auto)")
     ap.add_argument("--batch", type=int, default=0,
                     help="pivots per tableau sweep (0 = library default: 64 from 4096 rows, else 32)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -166,7 +165,6 @@ def main():
         sx.load().simplex_set_device(local_rank)
         if single_process_gpus:
             sx.set_gpus(list(range(args.gpus)))
-    sx.set_update_rows(args.update_rows)
     sx.set_batch(args.batch)
 
     def barrier():

@@ -24,10 +24,6 @@ extern "C" {
 /* ---- configuration ---- */
 int simplex_version(void);
 void simplex_set_verbose(int on);            /* reference progress lines on stdout */
-void simplex_set_update_rows(int rb);        /* rows per sweep step: 1, 2, 4; 0 = auto */
-/* the sweep's cache policy: -1 auto; 0 nt loads + plain stores, 1 nt loads + write-through (sc1)
- * stores, 2 default loads + sc1 stores, 3 default loads + plain stores, 4 nt loads + nt stores */
-void simplex_set_store_sc1(int mode);
 /* the sweep on the matrix cores (v_mfma_f64_16x16x4f64, bit-identical to the vector chain):
  * -1 auto (matrix cores), 0 vector sweep (batches of at most 32), 1 matrix-core sweep */
 void simplex_set_sweep_mfma(int mode);
@@ -104,12 +100,6 @@ void simplex_set_regions(int mode);
 /* virtual shards with the peer-memory batch: every rank's batch in one launch (1, default) or one
  * launch per rank on its own stream (0; needs as many hardware queues running at once) */
 void simplex_set_mr_single_launch(int on);
-/* several shards, diagnostic: allocate the exchanged buffers uncached -- bit 0 d, bit 1 U (3 = both,
- * 0 = plain memory, the default) -- see DESIGN.md §5 for what uncached exchange buffers did */
-void simplex_set_uncached_exchange(int mode);
-/* bench sessions, diagnostic: a shadow 32-pivot matrix-core sweep (into a scratch copy) on a second
- * stream concurrent with every fused batch -- 0 off, -1 on, n > 0 on with at most n resident blocks */
-void simplex_set_shadow_sweep(int mode);
 
 /* ---- fault handling and test hooks ---- */
 /* a fused batch whose in-kernel hand-off wait times out (SIMPLEX_HANG, never expected) is

@@ -33,9 +33,9 @@ for sz in "4096 8192" "8192 8192" "16384 8192"; do
     step ub_${tag}_$c 180 timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d $O/ub_${tag}_$c -o run -- python3 tools/update_bench_probe.py $sz 32 || exit $?
   done
 done
-step reuse 120 tools/uncached_reuse_probe || exit $?
-step reuse_wb 120 tools/uncached_reuse_probe --writeback || exit $?
+step reuse 120 experiments/uncached_reuse_probe || exit $?
+step reuse_wb 120 experiments/uncached_reuse_probe --writeback || exit $?
 for mode in 0 1 2 3; do
-  step bisect_$mode 300 python -u tools/uncached_exchange_probe.py $mode || exit $?
+  step bisect_$mode 300 python -u experiments/uncached_exchange_probe.py $mode || exit $?
 done
 exit 0

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 3, first GPU probe: the reference's -t sweep (36 instances, TIMER CSVs), the MX250's
-# failing instance (n=1024, m=8192, seed 110592), and the sweep grid-size A/B on 4096 x 8192.
+# failing instance (n=1024, m=8192, seed 110592).
 set -o pipefail
 mkdir -p gpurun_out/r03_cli_t
 export SIMPLEX_DATA_DIR=$PWD/gpurun_out/r03_cli_t
@@ -13,5 +13,4 @@ for seed in (110592, 110593):
     p = sx.generateRandomProblem(1024, 8192, seed, 1, 100)
     t0 = time.time(); r = sx.twoPhaseMethodEx(p); dt = time.time() - t0
     print("n=1024 m=8192 seed", seed, "status", r.status_name, "pivots", r.pivots, "objective", repr(r.optimal_value), "s", round(dt, 3), flush=True)
-' > gpurun_out/r03_seed110592.log 2>&1 && \
-timeout -k 10 300 python3 -u tools/sweep_waves_ab.py 4096x8192 8192x8192 waves=0.25,0.5,0.75,1,1.5 rb=4,2 > gpurun_out/r03_sweep_waves.log 2>&1
+' > gpurun_out/r03_seed110592.log 2>&1

@@ -82,8 +82,6 @@ SIGNATURES = {
     # simplex_hip.h
     "simplex_version": (ctypes.c_int, []),
     "simplex_set_verbose": (None, [ctypes.c_int]),
-    "simplex_set_update_rows": (None, [ctypes.c_int]),
-    "simplex_set_store_sc1": (None, [ctypes.c_int]),
     "simplex_set_sweep_mfma": (None, [ctypes.c_int]),
     "simplex_set_batch": (None, [ctypes.c_int]),
     "simplex_set_device": (None, [ctypes.c_int]),
@@ -107,8 +105,6 @@ SIGNATURES = {
     "simplex_set_update_waves": (None, [ctypes.c_double]),
     "simplex_set_regions": (None, [ctypes.c_int]),
     "simplex_set_mr_single_launch": (None, [ctypes.c_int]),
-    "simplex_set_uncached_exchange": (None, [ctypes.c_int]),
-    "simplex_set_shadow_sweep": (None, [ctypes.c_int]),
     "simplex_hang_recoveries": (ctypes.c_longlong, []),
     "simplex_fused_batches": (ctypes.c_longlong, []),
     "simplex_set_hang_inject": (None, [ctypes.c_longlong]),

@@ -398,14 +398,6 @@ def set_verbose(on):
     _lib.load().simplex_set_verbose(1 if on else 0)
 
 
-def set_update_rows(rb):
-    _lib.load().simplex_set_update_rows(int(rb))
-
-
-def set_store_sc1(mode):
-    _lib.load().simplex_set_store_sc1(int(mode))
-
-
 def set_sweep_mfma(mode):
     """The tableau sweep on the matrix cores (1), the vector sweep (0) or auto (-1)."""
     _lib.load().simplex_set_sweep_mfma(int(mode))

@@ -160,12 +160,8 @@ struct TLay {
 
 // ---- kernel launchers (sx_kernels.hip) ----
 struct SweepCfg {
-    int batch;           // pivots per sweep (1..SX_KMAX; the vector sweep: up to SX_HMAX)
-    int rows_per_block;  // 1, 2 or 4 rows per step
-    int sc1;             // cache policy of the tableau traffic: 0 nt loads + plain stores, 1 nt loads +
-                         // write-through (sc1) stores (default), 2 default loads + sc1 stores,
-                         // 3 default loads + plain stores, 4 nt loads + nt stores (32-slot sweeps)
-    int mfma;            // 1: the matrix-core sweep (k_msweep), 0: the vector sweep (k_sweep)
+    int batch;  // pivots per sweep (1..SX_KMAX; the vector sweep: up to SX_HMAX)
+    int mfma;   // 1: the matrix-core sweep (k_msweep), 0: the vector sweep (k_sweep)
 };
 
 int sx_enter_blocks(int L);
@@ -183,19 +179,6 @@ void sx_launch_pivot_row(const double *T, int rows, int row0, size_t ld, TLay tl
 // nact (device, or null): sweep only the columns [0, s0 + *nact) (slack compaction)
 void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, const int *nact, int s0,
                      const Pending &pd, const DevState *st, int rev, SweepCfg cfg, hipStream_t s);
-// What a batch's last block records for its (pipelined) sweep: the batch id, its pivots and the
-// swept slack columns after its activation.
-struct SweepMeta {
-    unsigned tag;
-    int count;
-    int nact;  // < 0: read *nact
-    int pad;
-};
-// the matrix-core sweep out of place (Tsrc -> Tdst; every swept element written); grid_cap > 0
-// caps the resident blocks (room for a concurrent batch)
-void sx_launch_msweep_oop(const double *Tsrc, double *Tdst, int rows, int row0, size_t ld, TLay tl, int Ns,
-                          const int *nact, int s0, const Pending &pd, const DevState *st, const SweepMeta *meta, int rev,
-                          int grid_cap, hipStream_t s);
 // slack compaction, after a batch's selections and before its sweep: move the slack column
 // of every row that left the basis for the first time into the swept block
 void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, int m, double *T, int rows, int row0,

@@ -54,10 +54,7 @@ namespace {
 
 struct Config {
     int verbose = 0;
-    int update_rows = 0;  // 0: auto (by tableau size)
-    int sc1 = -1;         // write-through tableau stores: -1 auto, 0, 1
     int sweep_mfma = -1;  // the matrix-core sweep: -1 auto, 0 off, 1 on
-    int shadow_sweep = 0;  // diagnostic (bench sessions): 0 off, -1 / cap > 0: a concurrent shadow sweep
     int batch = 0;           // pivots per tableau sweep (deferred updates), 1..SX_KMAX; 0 = auto
     int device = -1;
     int virtual_ranks = 1;
@@ -82,7 +79,6 @@ struct Config {
     int mr_two_stage = -1;         // peer-memory multi-rank batches of two stages (-1: unless SIMPLEX_MR_STAGES=1)
     unsigned first_batch_id = 1;   // test hook: batch id of a new engine's first batch
     int ipc_rank = -1, ipc_world = 0;  // test hook: one shard per process, peers through IPC handles, no RCCL
-    int uncached_xchg = 0;         // several shards: d and U in uncached memory (diagnostic; see alloc_shard)
     long long hang_recoveries = 0; // fused batches aborted and re-run on the per-pivot path
     long long fused_batches = 0;   // fused batch launches (every shard's counted once)
     // distributed
@@ -659,25 +655,9 @@ class Engine {
     void alloc_shard(Shard &x) {
         const size_t rows_alloc = x.rows > 0 ? (size_t)x.rows : 1;
         x.T = dalloc<double>(t_doubles(rows_alloc));
-        // d and U: plain device memory.  Other ranks write them over xGMI (system-scope stores)
-        // inside the multi-rank batch; this rank reads them only in later kernels, after the
-        // batch has seen every rank's done granule, across a kernel boundary.  Allocating them
-        // uncached instead (simplex_set_uncached_exchange(1)) was measured WRONG: after earlier
-        // engines had used and freed plain memory, a W = 8 virtual-shard solve diverged from
-        // the oracle in 3 of 3 runs (1126 / 1124 / 1181 phase-1 pivots instead of 1318), and
-        // never with plain memory (tools/_bisect_seq.py) -- dirty L2 lines of a
-        // page's earlier cached use written back over the uncached data is the likely cause.
-        // (diagnostic bisect: bit 0 = d uncached, bit 1 = U uncached)
-        if (xchg && (g_cfg.uncached_xchg & 1))
-            SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&x.d), round_up((size_t)N1, 16) * sizeof(double),
-                                         hipDeviceMallocUncached));
-        else
-            x.d = dalloc<double>(round_up((size_t)N1, 16));
-        if (xchg && (g_cfg.uncached_xchg & 2))
-            SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&x.U), (size_t)SX_KMAX * ld * sizeof(double),
-                                         hipDeviceMallocUncached));
-        else
-            x.U = dalloc<double>((size_t)SX_KMAX * ld);
+        // d and U: plain device memory (the coherence of the rows other ranks write).
+        x.d = dalloc<double>(round_up((size_t)N1, 16));
+        x.U = dalloc<double>((size_t)SX_KMAX * ld);
         x.d_save = dalloc<double>(round_up((size_t)N1, 16));
         x.colE = dalloc<double>(rows_alloc);
         x.prow = dalloc<double>(ld);
@@ -1034,22 +1014,18 @@ class Engine {
 
     // ---------------------------------------------------------------- one pivot
     SweepCfg sweep_cfg(int batch) const {
-        // Measured on MI355X: 4 rows per step at 32 pivots per sweep (config 3: 138 us), 2 rows
-        // at 16 (127 us); write-through (sc1) stores faster at every size from 32 MiB to
-        // 512 MiB (tools/sweep_bench_ab.py, profiles/r02_sweep_sc1_sizes.txt: 4096 x 8192
-        // 98 vs 110 us, 1024 x 4096 17.8 vs 22 us), so they are on by default.
+        // The vector sweep steps 4 rows at 32 pivots per sweep (config 3: 138 us), 2 at 16 (127 us)
+        // and stores write-through (sc1; faster at every size from 32 MiB to 512 MiB, 4096 x 8192
+        // 98 vs 110 us, profiles/r02_sweep_sc1_sizes.txt) -- which also keeps no row of the tableau
+        // dirty in an L2 of this device when peer ranks read leaving rows from it (system-scope
+        // loads over xGMI); the matrix-core sweep stores write-through too.
         SweepCfg c;
         c.batch = batch;
-        c.rows_per_block = g_cfg.update_rows > 0 ? std::min(g_cfg.update_rows, 4) : (batch > 16 ? 4 : 2);
-        c.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : 1;
         // (a two-stage batch: the matrix-core sweep, the only one holding SX_KMAX slots; one stage:
         // the matrix cores too by default -- with the strip-major factors the vector sweep's
         // per-row factor loads are scalar loads 128 B apart, config 2/3/5 no faster on the vector
         // units, profiles/r03_onestage_mfma_ab.txt)
         c.mfma = batch > SX_HMAX ? 1 : (g_cfg.sweep_mfma >= 0 ? g_cfg.sweep_mfma : 1);
-        // peer ranks read leaving rows straight from this tableau (system-scope loads over
-        // xGMI): its stores must write through to memory, not stay dirty in an L2 of this device
-        if (p2p && (rccl || multidev) && c.sc1 != 1 && c.sc1 != 2) c.sc1 = 1;
         return c;
     }
 
@@ -1664,12 +1640,15 @@ int two_phase(problem_t *P, double *solution, double *opt, int *base_out, long l
     return status;
 }
 
-// A small instance (n = 300, m = 1100: 1318 + 23 pivots, phases ending mid-batch) solved with the
-// multi-rank fused batch over peer memory -- in one-stage (32) and two-stage (64-pivot) batches --
-// and with the per-pivot exchange: true when the fused path ran (no hand-off timed out) and every
-// answer is bit-identical.
-bool selftest_solves() {
-    problem_t *P = generateRandomProblem(300, 1100, 41100, 1, 100);
+// A small instance solved with the multi-rank fused batch over peer memory -- in one-stage (32) and
+// two-stage (64-pivot) batches -- and with the per-pivot exchange: true when the fused path ran (no
+// hand-off timed out) and every answer is bit-identical.  The instance gives each of the W shards
+// 512 rows (m = 512 W, rows per shard round_up(m / W, 512) = 512), so every rank sweeps, owns
+// leaving rows and writes and reads peer pivot rows during the check (W = 2: m = 1100 -- 1318 + 23
+// pivots, phases ending mid-batch -- as before).
+bool selftest_solves(int W) {
+    const int sm = W > 2 ? 512 * W : 1100;
+    problem_t *P = generateRandomProblem(300, sm, 300 * 100 + sm, 1, 100);
     const int n = P->vars, m = P->constraints;
     const int save = g_cfg.p2p, save_batch = g_cfg.batch;
     const bool save_nt = g_cfg.no_timer;
@@ -1714,7 +1693,7 @@ bool gpus_selftest(const std::vector<int> &devs) {
     auto it = g_cfg.p2p_checked.find(devs);
     if (it != g_cfg.p2p_checked.end()) return it->second;
     g_cfg.p2p_checked[devs] = false;  // (while the check runs)
-    const bool ok = selftest_solves();
+    const bool ok = selftest_solves((int)devs.size());
     g_cfg.p2p_checked[devs] = ok;
     if (!ok) fprintf(stderr, "simplex: peer-memory fused batches disagree with the per-pivot exchange on these GPUs; "
                              "using the per-pivot exchange\n");
@@ -1728,10 +1707,7 @@ extern "C" {
 
 int simplex_version(void) { return 1; }
 void simplex_set_verbose(int on) { g_cfg.verbose = on; }
-void simplex_set_update_rows(int rb) { g_cfg.update_rows = (rb == 1 || rb == 2 || rb == 4 || rb == 8) ? rb : 0; }
-void simplex_set_shadow_sweep(int mode) { g_cfg.shadow_sweep = mode; }
 void simplex_set_sweep_mfma(int mode) { g_cfg.sweep_mfma = mode < 0 ? -1 : (mode ? 1 : 0); }
-void simplex_set_store_sc1(int mode) { g_cfg.sc1 = mode < 0 ? -1 : (mode <= 4 ? mode : 1); }
 void simplex_set_batch(int pivots) { g_cfg.batch = pivots > 0 ? std::min(pivots, SX_KMAX) : 0; }
 void simplex_set_device(int device) {
     g_cfg.device = device;
@@ -1772,7 +1748,6 @@ long long simplex_last_objective_row(double *out, long long cap) {
     return n;
 }
 void simplex_set_update_waves(double waves) { sx_set_update_waves((float)waves); }
-void simplex_set_uncached_exchange(int mode) { g_cfg.uncached_xchg = mode < 0 ? 0 : mode & 3; }
 void simplex_set_exchange_mode(int mode) { g_cfg.exchange_mode = (mode >= 0 && mode <= 2) ? mode : 0; }
 void simplex_set_timer_dir(const char *dir) { g_cfg.timer_dir = dir ? dir : ""; }
 
@@ -1800,7 +1775,7 @@ int simplex_dist_get_unique_id(unsigned char *out) {
 static void p2p_selftest() {
     g_cfg.p2p_ready = false;
     if (g_cfg.world > SX_MAXW || g_cfg.p2p == 0) return;
-    int ok = selftest_solves() ? 1 : 0;
+    int ok = selftest_solves(g_cfg.world) ? 1 : 0;
     int *dv = nullptr;
     SX_HIP(hipMalloc(reinterpret_cast<void **>(&dv), sizeof(int)));
     SX_HIP(hipMemcpy(dv, &ok, sizeof(int), hipMemcpyHostToDevice));
@@ -1985,40 +1960,11 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
         }
         ++nsw;
     };
-    // diagnostic: a shadow sweep (a full 32-pivot matrix-core sweep of the tableau into a scratch
-    // buffer) on a second stream, concurrent with every batch -- what a pipelined sweep would
-    // cost the chain and get from the device while the batch runs
-    const bool shadow = g_cfg.shadow_sweep != 0 && fused && E.sh.size() == 1;
-    double *Tsh = nullptr;
-    SweepMeta *meta_dev = nullptr;
-    hipStream_t s2 = nullptr;
-    hipEvent_t sh_a = nullptr, sh_b = nullptr;
-    if (shadow) {
-        Shard &x = E.sh[0];
-        Tsh = dalloc<double>(E.t_doubles(x.rows > 0 ? (size_t)x.rows : 1));
-        meta_dev = dalloc<SweepMeta>(1);
-        SweepMeta mh{1u, SX_KMAX, -1, 0};
-        SX_HIP(hipMemcpy(meta_dev, &mh, sizeof(mh), hipMemcpyHostToDevice));
-        SX_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
-        SX_HIP(hipEventCreateWithFlags(&sh_a, hipEventDisableTiming));
-        SX_HIP(hipEventCreateWithFlags(&sh_b, hipEventDisableTiming));
-    }
     SX_HIP(hipEventRecord(w0, E.s));
     for (long long i = 0; i < k;) {
         if (fused) {
             const int kb = (int)std::min<long long>(K, k - i);
-            if (shadow) {
-                Shard &x = E.sh[0];
-                SX_HIP(hipEventRecord(sh_a, E.s));
-                SX_HIP(hipStreamWaitEvent(s2, sh_a, 0));
-                Pending pd = E.pending(x);
-                pd.batch = 1u;
-                sx_launch_msweep_oop(x.T, Tsh, x.rows, x.row0, E.ld, E.tl, E.cols(E.N).Ns, E.compact ? x.nact : nullptr, 1 + E.n,
-                                     pd, x.st, meta_dev, 0, g_cfg.shadow_sweep > 0 ? g_cfg.shadow_sweep : 0, s2);
-                SX_HIP(hipEventRecord(sh_b, s2));
-            }
             E.enqueue_batch(kb);
-            if (shadow) SX_HIP(hipStreamWaitEvent(E.s, sh_b, 0));
             i += kb;
         } else {
             E.enqueue_pivot();
@@ -2070,13 +2016,6 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
     for (auto &e : evs) (void)hipEventDestroy(e);
     (void)hipEventDestroy(w0);
     (void)hipEventDestroy(w1);
-    if (shadow) {
-        (void)hipFree(Tsh);
-        (void)hipFree(meta_dev);
-        (void)hipStreamDestroy(s2);
-        (void)hipEventDestroy(sh_a);
-        (void)hipEventDestroy(sh_b);
-    }
     S->total = f.pivots;
     E.gather_d();  // (outside the timed region: the whole objective row on every shard)
     E.sync_all();
@@ -2271,8 +2210,6 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     btl.jB = cols;
     SweepCfg cfg;
     cfg.batch = pivots;
-    cfg.rows_per_block = g_cfg.update_rows > 0 ? std::min(g_cfg.update_rows, 4) : (pivots > 16 ? 4 : 2);
-    cfg.sc1 = g_cfg.sc1 >= 0 ? g_cfg.sc1 : 1;  // (as sweep_cfg: write-through at every size)
     cfg.mfma = pivots > SX_HMAX ? 1 : (g_cfg.sweep_mfma >= 0 ? g_cfg.sweep_mfma : 1);
     long long sweeps = 0;
     auto one = [&]() { sx_launch_sweep(T, rows, 0, ld, btl, cols, nullptr, 0, pd, st, (int)(sweeps & 1), cfg, s); };

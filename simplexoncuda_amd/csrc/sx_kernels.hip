@@ -51,11 +51,6 @@ __device__ __forceinline__ void argmin_step(double &v, int &i, double sv, int si
 // reference's combines.  The offset-16 step crosses DPP rows (a bpermute shuffle); offsets
 // 8, 4, 2, 1 stay inside row 0 and use DPP row shifts (VALU, no LDS round trip).
 __device__ __forceinline__ void half_argmin(double &v, int &i) {
-#ifdef SX_SHFL_ARGMIN  // (diagnostic build: every step a bpermute shuffle)
-#pragma unroll
-    for (int off = 16; off > 0; off >>= 1) argmin_step<0>(v, i, __shfl_down(v, off, 32), __shfl_down(i, off, 32));
-    return;
-#endif
     argmin_step<16>(v, i, __shfl_down(v, 16, 32), __shfl_down(i, 16, 32));
     argmin_step<8>(v, i, dpp_down<8>(v), dpp_down<8>(i));
     argmin_step<4>(v, i, dpp_down<4>(v), dpp_down<4>(i));
@@ -687,6 +682,34 @@ __device__ __forceinline__ unsigned ld_sc1(const unsigned *p) {
     return __hip_atomic_load(const_cast<unsigned *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// k_batch's objective-tile records as its ratio blocks poll them: 4 granules per tile (the tile
+// winner's d value and its pivot-row value of the pivot), at most SX_OBJ_TILES
+// tiles, SX_OBJ_PER_LANE granules per lane of the polling wave
+#define SX_GB4 4
+#define SX_GBS 16  // their stride in memory, granules: one 128-byte line per record (no two producers share a line)
+#define SX_OBJ_TILES 160
+#define SX_OBJ_PER_LANE 10
+
+// 8-byte write-through (sc1) store / L1-bypassing load of a double
+__device__ __forceinline__ void st_sc1(double *p, double v) {
+    __hip_atomic_store(reinterpret_cast<u64 *>(p), (u64)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1d(const double *p) {
+    return __longlong_as_double((long long)ld_sc1(reinterpret_cast<const u64 *>(p)));
+}
+struct IdOff {
+    __device__ __forceinline__ int operator()(int k) const { return k; }
+};
+// the value granules (2 per tile) of k_batch's 4-granule objective records
+struct Rec4Val {
+    __device__ __forceinline__ int operator()(int k) const { return (k >> 1) * SX_GBS + (k & 1); }
+};
+// all 4 granules of each record
+struct Rec4All {
+    __device__ __forceinline__ int operator()(int k) const { return (k >> 2) * SX_GBS + (k & 3); }
+};
+
 __device__ __forceinline__ u64 ld_sys(const u64 *p) {
     return __hip_atomic_load(const_cast<u64 *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -698,14 +721,14 @@ __device__ __forceinline__ u64 ld_sys(const u64 *p) {
 // measured no different)
 __device__ __forceinline__ void poll_pause() { __builtin_amdgcn_s_sleep(1); }
 
-// Wave 0 of the block (threads 0..63) polls n <= 64 * SX_GATHER_PER_LANE granules, granule k
-// at base[off(k)], each until it carries `tag`, into out[k] (LDS), all of a round's loads in
-// flight together, no block barrier per poll.  (pay: the payload of every even granule k goes
-// to pay[k / 2] -- records of two granules.)  Wave-uniform result: false when the batch was
-// aborted (or this wait timed out, which aborts it).  Only wave 0 may call it.
-template <typename OFF, bool SYS = false>
-__device__ int poll_wave(const u64 *base, int n, OFF off, unsigned tag, unsigned *out, unsigned *abort_w,
-                         unsigned long long timeout, unsigned *pay) {
+// Wave 0 of the block (threads 0..63) polls n <= 64 * PL granules, granule k at base[off(k)], each
+// until it carries `tag`, into out[k] (LDS), all of a round's loads in flight together, no block
+// barrier per poll; payf(k, payload) is called for every granule as it arrives.  Wave-uniform
+// result: false when the batch was aborted (or this wait timed out, which aborts it).  Only wave 0
+// may call it.
+template <typename OFF, bool SYS, int PL, typename PAYF>
+__device__ __forceinline__ int poll_wave_f(const u64 *base, int n, OFF off, unsigned tag, unsigned *out, unsigned *abort_w,
+                           unsigned long long timeout, PAYF payf) {
     const int t = threadIdx.x;
     const u64 t0 = __builtin_amdgcn_s_memrealtime();
     if (n <= 64) {
@@ -716,7 +739,7 @@ __device__ int poll_wave(const u64 *base, int n, OFF off, unsigned tag, unsigned
                 if (((unsigned)(w >> 32) | SX_PAYMASK) == (tag | SX_PAYMASK)) {
                     have = true;
                     out[t] = (unsigned)w;
-                    if (pay && !(t & 1)) pay[t >> 1] = (unsigned)(w >> 32) & SX_PAYMASK;
+                    payf(t, (unsigned)(w >> 32) & SX_PAYMASK);
                 }
             }
             if (__ballot(!have) == 0ull) return 1;
@@ -733,20 +756,20 @@ __device__ int poll_wave(const u64 *base, int n, OFF off, unsigned tag, unsigned
     }
     unsigned miss = 0u;  // bit c: granule t + 64 c still missing
 #pragma unroll
-    for (int c = 0; c < SX_GATHER_PER_LANE; ++c)
+    for (int c = 0; c < PL; ++c)
         if (t + 64 * c < n) miss |= 1u << c;
     for (unsigned it = 0;; ++it) {
-        u64 w[SX_GATHER_PER_LANE];
+        u64 w[PL];
 #pragma unroll
-        for (int c = 0; c < SX_GATHER_PER_LANE; ++c)
+        for (int c = 0; c < PL; ++c)
             if ((miss >> c) & 1u) w[c] = SYS ? ld_sys(base + off(t + 64 * c)) : ld_sc1(base + off(t + 64 * c));
 #pragma unroll
-        for (int c = 0; c < SX_GATHER_PER_LANE; ++c) {
+        for (int c = 0; c < PL; ++c) {
             const int k = t + 64 * c;
             if (((miss >> c) & 1u) && ((unsigned)(w[c] >> 32) | SX_PAYMASK) == (tag | SX_PAYMASK)) {
                 miss &= ~(1u << c);
                 out[k] = (unsigned)w[c];
-                if (pay && !(k & 1)) pay[k >> 1] = (unsigned)(w[c] >> 32) & SX_PAYMASK;
+                payf(k, (unsigned)(w[c] >> 32) & SX_PAYMASK);
             }
         }
         if (__ballot(miss != 0u) == 0ull) return 1;
@@ -762,6 +785,17 @@ __device__ int poll_wave(const u64 *base, int n, OFF off, unsigned tag, unsigned
     }
 }
 
+// The same with the payload of every even granule k stored to pay[k / 2] (records whose value
+// granules come in pairs), or dropped (pay null).
+template <typename OFF, bool SYS = false>
+__device__ int poll_wave(const u64 *base, int n, OFF off, unsigned tag, unsigned *out, unsigned *abort_w,
+                         unsigned long long timeout, unsigned *pay) {
+    return poll_wave_f<OFF, SYS, SX_GATHER_PER_LANE>(base, n, off, tag, out, abort_w, timeout,
+                                                     [pay](int k, unsigned pl) {
+                                                         if (pay && !(k & 1)) pay[k >> 1] = pl;
+                                                     });
+}
+
 // Pass 2 of the reference's argmin (deviceReduceKernel<false><<<1,1024>>>, reduction.cu:239-241)
 // over nt <= 256 two-granule tile records already gathered into s_g / s_pay, run by wave 0
 // alone: part p (tile p's winner) sits on lane p % 64 of round p / 64, so round r's two halves
@@ -769,7 +803,9 @@ __device__ int poll_wave(const u64 *base, int n, OFF off, unsigned tag, unsigned
 // 0..2R-1, padded with (DBL_MAX, -1) to the reference's 32 warps, and one more half_argmin
 // combines them -- the combines of block_argmin512 on the same parts.  Result in lane 0;
 // any_elig (wave-uniform): some record carries the "entry >= eps" payload bit (ratio tiles).
-__device__ __forceinline__ void wave_pass2(const unsigned *s_g, const unsigned *s_pay, int nt, double *s_v,
+// (S: granules per gathered record, its value in the first two)
+template <int S = 2, typename PT = unsigned>
+__device__ __forceinline__ void wave_pass2(const unsigned *s_g, const PT *s_pay, int nt, double *s_v,
                                            int *s_i, double &v_out, int &i_out, int &any_elig) {
     const int lane = threadIdx.x;
     const int R = (nt + 63) >> 6;
@@ -779,7 +815,7 @@ __device__ __forceinline__ void wave_pass2(const unsigned *s_g, const unsigned *
         double v = DBL_MAX;
         int i = -1;
         if (p < nt) {
-            const double cv = gd(s_g[2 * p], s_g[2 * p + 1]);
+            const double cv = gd(s_g[S * p], s_g[S * p + 1]);
             const unsigned pl = s_pay[p];
             te |= (pl >> 10) & 1u;
             if (cmp_eps(cv, v) < 0) {
@@ -922,6 +958,49 @@ __device__ __forceinline__ double hist_col(double a, int q, unsigned bits, const
     return a;
 }
 
+// 64-bit value of lane src (per-lane src; ds_bpermute)
+__device__ __forceinline__ double shfl_d(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __shfl((int)b, src), hi = __shfl((int)(b >> 32), src);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+// hist_col with the entering column's pending pivot-row values in a register of the wave (lane s:
+// U[s][e] of the stage's slot s) instead of LDS: k_batch's ratio blocks load them from U themselves
+// (every wave its own copy), in the same round trip as the column's stored values.
+__device__ __forceinline__ double hist_col_w(double a, int q, unsigned bits, const double *s_hist, double wu,
+                                             const double *s_p) {
+    const int t = threadIdx.x;
+    if (__ballot(bits != 0u) == 0ull) {
+        int s = 0;
+        for (; s + 8 <= q; s += 8) {
+            double h[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) h[k] = s_hist[(s + k) * SX_TILE + t];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a = fma(h[k], rdlane(wu, s + k), a);
+        }
+        for (; s < q; ++s) a = fma(s_hist[s * SX_TILE + t], rdlane(wu, s), a);
+        return a;
+    }
+    const int sl = bits ? 31 - __builtin_clz(bits) : 0;  // the row's last leaving slot
+    const double usl = shfl_d(wu, sl);
+    if (bits) a = usl / s_p[sl];
+    for (int s0 = 0; s0 < q; s0 += 8) {  // (slots past q read slot s0 and are not used)
+        double h[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) h[k] = s_hist[(s0 + k < q ? s0 + k : s0) * SX_TILE + t];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (s0 + k < q) {
+                const double y = fma(h[k], rdlane(wu, s0 + k), a);
+                a = (bits && s0 + k > sl) || !bits ? y : a;
+            }
+        }
+    }
+    return a;
+}
+
 // The same for the pivot row's entry `u` on an objective tile's column: u / p_s at the slots
 // where the leaving row r itself left before (s_r[s] == r), else fma(F[r][s], U[s][j], u).
 // The slots where r left are block-uniform: with none the chain is branch-free; else it starts
@@ -970,6 +1049,24 @@ __device__ __forceinline__ double stage1_col(double a, const double (&h)[SX_HMAX
     for (int s = 0; s < SX_HMAX; ++s) {
         const double y = fma(h[s], rdlane(wu, s), a);
         a = s > sl ? y : a;
+    }
+    return a;
+}
+// stage1_col with the first stage's U[s][e] in a register of the wave (lane s), as hist_col_w
+__device__ __forceinline__ double stage1_col_w(double a, const double (&h)[SX_HMAX], unsigned bits, double wu,
+                                               const double *s_p) {
+    if (__ballot(bits != 0u) == 0ull) {
+#pragma unroll
+        for (int s = 0; s < SX_HMAX; ++s) a = fma(h[s], rdlane(wu, s), a);
+        return a;
+    }
+    const int sl = bits ? 31 - __builtin_clz(bits) : 0;
+    const double usl = shfl_d(wu, sl);
+    if (bits) a = usl / s_p[sl];
+#pragma unroll
+    for (int s = 0; s < SX_HMAX; ++s) {
+        const double y = fma(h[s], rdlane(wu, s), a);
+        a = (bits && s > sl) || !bits ? y : a;
     }
     return a;
 }
@@ -1163,15 +1260,16 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
     __shared__ int s_i[16];
     __shared__ double s_p[SX_KMAX];                  // pivots of the batch
     __shared__ int s_r[SX_KMAX], s_e[SX_KMAX];       // leaving rows / entering variables of the batch
-    __shared__ double s_ue[SX_HMAX], s_fr[SX_HMAX];  // U[s][e] (entering column) / F[r][s] (leaving row), this stage
-    __shared__ double s_ue1[SX_HMAX], s_fr1[SX_HMAX];  // the same for the first stage's slots (second stage)
+    __shared__ double s_fr[SX_HMAX], s_fr1[SX_HMAX];  // F[r][s] (leaving row), this stage / the first stage's slots
     __shared__ double s_a[SX_TILE], s_b[SX_TILE];    // ratio blocks: entering column, RHS (winner lookup)
     __shared__ unsigned s_g[4 * SX_TILE];            // gathered granules
     __shared__ unsigned s_pay[SX_TILE];              // their payloads (two-granule records)
+    __shared__ unsigned short s_payo[3 * SX_OBJ_TILES];  // payloads of the objective records' granules 0..2
+    __shared__ double s_uq;                          // the entering column's pivot-row value of this pivot
     __shared__ int s_last;
     // per-step results written by wave 0 before the step's one barrier (each step its own
     // words, so no wave still reading an earlier step's result can see them change)
-    __shared__ int s_sel_ok, s_sel_r, s_sel_any, s_det_ok, s_det_e, s_det_st, s_ent_ok, s_ent_e, s_ent_r, s_ent_st, s_ent_m;
+    __shared__ int s_sel_ok, s_sel_r, s_sel_any, s_det_ok, s_det_e, s_det_st, s_ent_ok, s_ent_e, s_ent_m;
     __shared__ double s_det_dmin, s_ent_v, s_br, s_ent_p;
     __shared__ int s_welig[SX_TILE / 64];
     const int t = threadIdx.x;
@@ -1235,7 +1333,6 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
             for (int s1 = 0; s1 < SX_HMAX; ++s1) h1[s1] = s_hist[s1 * SX_TILE + t];
             bits1 = bits;
             bits = 0u;
-            if (t < SX_HMAX) s_ue1[t] = s_ue[t];  // (U[s][e] of pivot SX_HMAX: its objective record)
             drain();
             __syncthreads();
             if (t == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -1246,6 +1343,10 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
         // counter waits on one role's path never cover the other role's loads.  Per pivot q: does
         // the phase end here (the pivot cap: the same decision in every block), the stage switch.
         if (isA) {
+            // the entering column's pending pivot-row values, one register per wave (lane s: U[hb + s][e]
+            // of the current stage; wu1: U[s][e] of the first stage), loaded by every wave with the
+            // column's stored values (the fresh slot from the objective record)
+            double wu = 0.0, wu1 = 0.0;
             for (int q = 0; q < K; ++q) {
                 const unsigned tag = make_tag(B, q);
                 if (cap >= 0 && piv0 + q >= cap) {
@@ -1264,8 +1365,8 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 if (blockIdx.x == 0) SX_STAMP(0);
                 SX_BSTAMP(0);
                 double a1 = a_pre;
-                if (hb && !done) a1 = stage1_col(a1, h1, bits1, s_ue1, s_p);
-                const double a = done ? 0.0 : hist_col(a1, qq, bits, s_hist, s_ue, s_p + hb);
+                if (hb && !done) a1 = stage1_col_w(a1, h1, bits1, wu1, s_p);
+                const double a = done ? 0.0 : hist_col_w(a1, qq, bits, s_hist, wu, s_p + hb);
                 double rv = DBL_MAX;
                 int ri = -1, elig = 0;
                 if (liveA && !done) {
@@ -1279,6 +1380,9 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 if (blockIdx.x == 0) SX_STAMP(2);
                 s_a[t] = a;
                 s_b[t] = b;
+                // (every wave's F store of the previous pivot acknowledged before this pivot's record:
+                // the objective side reads F[r][s < q] from memory after seeing it)
+                drain();
                 // pass 1 (reduction.cu:51-80): every half-wave its tree, one block barrier, then
                 // wave 0 combines the 16 half winners (block_argmin512's second step) and
                 // publishes the record alone
@@ -1326,54 +1430,45 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     status = SX_FEASIBLE;
                     break;
                 }
-                // ---- the objective side's answer: pass 2 over the objective tiles (the entering
-                // variable of pivot q + 1), then r, p, the RHS, the status and U[s <= q][e] from
-                // the winner's record (wave 0 polls; one block barrier)
+                // ---- this pivot's leaving row, from the ratio records (every ratio block runs the pass 2
+                // the objective blocks run, reduction.cu:116-140, and takes p and the RHS from the
+                // winner's record): the objective side answers much later, so this is off the chain
                 if (t < 64) {
-                    int ok = poll_wave(gb, 2 * NB, rec2_b, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
-                    double ev = DBL_MAX;
-                    int ei = -1, any = 0;
-                    if (ok) wave_pass2(s_g, s_pay, NB, s_v, s_i, ev, ei, any);
-                    ei = __builtin_amdgcn_readfirstlane(ei);
-                    // second stage: the next entering column's first-stage pivot-row values U[s][e]
-                    // (write-through, drained at the stage switch), loaded while the record is polled
-                    u64 ue1 = 0ull;
-                    if (hb && ok && ei >= 0 && t < SX_HMAX)
-                        ue1 = ld_sc1(reinterpret_cast<const u64 *>(U + (size_t)t * ld + c.map(1 + ei)));
-                    if (ok) {
-                        const int wt = ei >= 0 ? ei / SX_TILE : 0;
-                        ok = poll_wave(gb + (size_t)wt * SX_GB_STRIDE + kOP, (kOU - kOP) + 2 * (qq + 1),
-                                       [](int k) { return k; }, tag, s_g, &ch->abort_w, 20000000ull, (unsigned *)nullptr);
-                        if (ok && t <= qq) s_ue[t] = gd(s_g[kOU - kOP + 2 * t], s_g[kOU - kOP + 1 + 2 * t]);
+                    int ok = poll_wave(ga, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
+                    double tv = DBL_MAX;
+                    int ti = -1, any = 0;
+                    if (ok) wave_pass2(s_g, s_pay, NA, s_v, s_i, tv, ti, any);
+                    ti = __builtin_amdgcn_readfirstlane(ti);
+                    if (ok && ti >= 0) {
+                        const int wt = ti / SX_TILE;
+                        ok = poll_wave(ga + (size_t)wt * SX_GA_STRIDE + kRA, 4, IdOff(), tag, s_g + 2048 - 64,
+                                       &ch->abort_w, 20000000ull, (unsigned *)nullptr);
                     }
-                    if (hb && t < SX_HMAX) s_ue1[t] = __longlong_as_double((long long)ue1);
                     if (t == 0) {
-                        s_ent_ok = ok;
-                        s_ent_e = ei;
-                        s_ent_v = ev;
-                        if (ok) {
-                            s_ent_p = gd(s_g[0], s_g[1]);
-                            s_br = gd(s_g[kOB - kOP], s_g[kOB - kOP + 1]);
-                            s_ent_r = (int)s_g[kOR - kOP];
-                            s_ent_st = (int)s_g[kOS - kOP];
-                            s_ent_m = (int)s_g[kOM - kOP];
+                        s_sel_ok = ok;
+                        s_sel_r = ti;
+                        s_sel_any = any;
+                        if (ok && ti >= 0) {
+                            s_ent_p = gd(s_g[2048 - 64], s_g[2048 - 63]);
+                            s_br = gd(s_g[2048 - 62], s_g[2048 - 61]);
                         }
                     }
                 }
                 __syncthreads();
-                if (blockIdx.x == 0) SX_STAMP(5);
-                SX_BSTAMP(2);
-                if (!s_ent_ok) {
+                if (!s_sel_ok) {
                     aborted = true;
                     break;
                 }
-                if (s_ent_st != SX_NOT_ENDED) {  // the objective side found UNBOUNDED / NUMERIC_FAIL
-                    status = s_ent_st;
+                if (!s_sel_any) {  // solver.cu:96-102 (the objective side decides the same)
+                    status = SX_UNBOUNDED;
+                    break;
+                }
+                const int r = s_sel_r;
+                if (r < 0) {
+                    status = SX_NUMERIC_FAIL;
                     break;
                 }
                 // ---- this pivot's factor column and the rows' new RHS (solver.cu:34-46)
-                const int enext = s_ent_e;
-                const int r = s_ent_r;
                 const double p = s_ent_p, br = s_br;
                 if (t == 0) {
                     s_p[q] = p;
@@ -1384,7 +1479,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 const double f = -a / p;
                 s_hist[qq * SX_TILE + t] = f;
                 if (liveA) {
-                    F[sx_fidx(li, q)] = f;
+                    st_sc1(F + sx_fidx(li, q), f);  // (write-through: read by the objective side from memory)
                     if (li == r) {
                         b = b / p;
                         bits |= 1u << qq;
@@ -1401,13 +1496,52 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     recs[q].p = p;
                     U[(size_t)q * ld] = br;  // the pivot row's RHS entry, for the sweep
                 }
-                e = enext;
+                // ---- the objective side's answer: pass 2 over the objective tiles (the entering variable
+                // of pivot q + 1), its stored column and its pivot-row entry of this pivot from the
+                // winner's record (wave 0 polls; one block barrier)
+                if (t < 64) {
+                    unsigned short *po = s_payo;
+                    const int ok = poll_wave_f<Rec4All, false, SX_OBJ_PER_LANE>(
+                        gb, SX_GB4 * NB, Rec4All(), tag, s_g, &ch->abort_w, 20000000ull, [po](int k, unsigned pl) {
+                            if ((k & 3) < 3) po[(k & 3) * SX_OBJ_TILES + (k >> 2)] = (unsigned short)pl;
+                        });
+                    double ev = DBL_MAX;
+                    int ei = -1, any = 0;
+                    if (ok) wave_pass2<SX_GB4, unsigned short>(s_g, s_payo, NB, s_v, s_i, ev, ei, any);
+                    if (t == 0) {
+                        s_ent_ok = ok;
+                        s_ent_e = ei;
+                        s_ent_v = ev;
+                        s_ent_m = 0;
+                        s_uq = 0.0;
+                        if (ok && ei >= 0) {
+                            const int wt = ei / SX_TILE;
+                            s_ent_m = (int)s_payo[SX_OBJ_TILES + wt] | ((int)s_payo[2 * SX_OBJ_TILES + wt] << SX_PAYBITS);
+                            s_uq = gd(s_g[SX_GB4 * wt + 2], s_g[SX_GB4 * wt + 3]);
+                        }
+                    }
+                }
+                __syncthreads();
+                if (blockIdx.x == 0) SX_STAMP(5);
+                SX_BSTAMP(2);
+                if (!s_ent_ok) {
+                    aborted = true;
+                    break;
+                }
+                e = s_ent_e;
                 dmin = s_ent_v;
-                // the next entering column's stored value of this row (its stored position from the
-                // winner's record): issued after this pivot's stores, so no wait of the compiler's
-                // for a register reused above covers it; it is waited for in the next chain
-                if (liveA) a_pre = T[tl.idx(li, s_ent_m)];
-                __syncthreads();  // (s_p / s_ue of this step are read by the next pivot's chain)
+                // the next pivot's operands, issued together: this row's stored value of the entering
+                // column and (every wave) the column's pending pivot-row values U[s][e] -- U[q][e] from
+                // the record, the older ones from memory (write-through, acknowledged before their
+                // objective records)
+                {
+                    const int me = s_ent_m, lane = t & 63, q1 = q + 1, hb1 = q1 >= SX_HMAX ? SX_HMAX : 0;
+                    const double uq = s_uq;
+                    if (liveA) a_pre = T[tl.idx(li, me)];
+                    const int sa = hb1 + lane;
+                    wu = lane < q1 - hb1 ? (sa == q ? uq : ld_sc1d(U + (size_t)sa * ld + me)) : 0.0;
+                    if (hb1) wu1 = lane < SX_HMAX ? (lane == q ? uq : ld_sc1d(U + (size_t)lane * ld + me)) : 0.0;
+                }
             }
         } else {
             for (int q = 0; q < K; ++q) {
@@ -1507,12 +1641,15 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     }
                 }
                 // pass 1 (reduction.cu:51-80): half-wave trees, one block barrier, wave 0 combines
-                // the half winners and publishes the record alone
+                // the half winners and publishes the record alone.  (Every wave's U store of the
+                // previous pivot is acknowledged first: the ratio side reads U[s < q] from memory
+                // after seeing this record.)
                 half_argmin(v, i);
                 if ((t & 31) == 0) {
                     s_v[t >> 5] = v;
                     s_i[t >> 5] = i;
                 }
+                drain();
                 __syncthreads();
                 if (t < 64) {
                     double wv = t < 16 ? s_v[t] : DBL_MAX;
@@ -1523,28 +1660,23 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     wv = __longlong_as_double(((long long)__builtin_amdgcn_readfirstlane((int)(vb >> 32)) << 32) |
                                               (long long)(unsigned)__builtin_amdgcn_readfirstlane((int)vb));
                     const int win = wi >= 0 ? wi - tb * SX_TILE : 0;
-                    const unsigned pl = wi >= 0 ? (unsigned)win : SX_NOIDX;
-                    const int nG = kOU + 2 * (qq + 1);
-                    for (int k = t; k < nG; k += 64) {
-                        unsigned data;
-                        if (k == kOR) {
-                            data = (unsigned)r;
-                        } else if (k == kOS) {
-                            data = (unsigned)ost;
-                        } else if (k == kOM) {
-                            data = (unsigned)reinterpret_cast<const int *>(s_a)[win];
-                        } else {
-                            const double val = k < kOP ? wv : k < kOB ? p : k < kOR ? br
-                                                                          : s_hist[((k - kOU) >> 1) * SX_TILE + win];
-                            const u64 bits64 = (u64)__double_as_longlong(val);
-                            data = ((k < kOU ? k : k - kOU) & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64;
-                        }
-                        put_g(gb + (size_t)tb * SX_GB_STRIDE + k, data, k < kOP ? (tag | pl) : tag);
+                    // the record: the winner's d value (payload: its index in the tile) and its pivot-row
+                    // value of this pivot U[q][w] (the ratio side's newest pending entry of the entering
+                    // column if w enters), the winner's stored column in the payloads of granules 1, 2
+                    if (t < SX_GB4) {
+                        const int mw = reinterpret_cast<const int *>(s_a)[win];
+                        const double val = t < 2 ? wv : s_hist[qq * SX_TILE + win];
+                        const u64 bits64 = (u64)__double_as_longlong(val);
+                        const unsigned data = (t & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64;
+                        const unsigned pl = t == 0 ? (wi >= 0 ? (unsigned)win : SX_NOIDX)
+                                          : t == 1 ? ((unsigned)mw & SX_PAYMASK)
+                                          : t == 2 ? (((unsigned)mw >> SX_PAYBITS) & SX_PAYMASK) : 0u;
+                        put_g(gb + (size_t)tb * SX_GBS + t, data, tag | pl);
                     }
                 }
-                // the pivot row into U[q] (the sweep's input) behind the record (plain stores:
-                // written back at the stage switch and before the block leaves)
-                if (ost == SX_NOT_ENDED && liveB && 1 + ia < c.Ns) U[(size_t)q * ld + mj] = s_hist[qq * SX_TILE + t];
+                // the pivot row into U[q] (the sweep's input, and the ratio side's pending entries of
+                // later entering columns) behind the record, write-through
+                if (ost == SX_NOT_ENDED && liveB && 1 + ia < c.Ns) st_sc1(U + (size_t)q * ld + mj, s_hist[qq * SX_TILE + t]);
                 if (tb == 0) SX_STAMP(4);
                 SX_BSTAMP(2);
                 if (ost != SX_NOT_ENDED) {
@@ -1559,7 +1691,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
         if (!isA && !aborted && (status == SX_NOT_ENDED || status == SX_PIVOT_CAP) && cnt > 0) {
             const unsigned tag = make_tag(B, cnt - 1);
             if (t < 64) {
-                const int ok = poll_wave(gb, 2 * NB, rec2_b, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
+                const int ok = poll_wave(gb, 2 * NB, Rec4Val(), tag, s_g, &ch->abort_w, 20000000ull, s_pay);
                 double ev = DBL_MAX;
                 int ei = -1, any = 0;
                 if (ok) wave_pass2(s_g, s_pay, NB, s_v, s_i, ev, ei, any);
@@ -2223,10 +2355,9 @@ __device__ __forceinline__ void sweep_record(int *rec, const DevState *st, const
     }
 }
 
-// POL: cache policy of the tableau traffic -- 0 nt loads + plain stores, 1 nt loads + write-through
-// (sc1) stores (default), 2 default-policy loads + sc1 stores, 3 default loads + plain stores,
-// 4 nt loads + nt stores (sweep-policy A/B, SweepCfg.sc1)
-template <int KT, int RB, int POL>
+// Cache policy of the tableau traffic: non-temporal loads, write-through (sc1) stores (measured best
+// of five load/store policies at both sizes, profiles/r03_sweep_policy_ab.txt).
+template <int KT, int RB>
 __global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, TLay tl, int Ns,
                                                const int *__restrict__ nact, int s0,
                                                const double *__restrict__ F, const double *__restrict__ U,
@@ -2265,7 +2396,7 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, T
         double2 x[RB];
         // non-temporal loads (cache policy nt): each element is read once per sweep; measured
         // 1.5 % faster at config 5, neutral at config 3 (profiles/r01_v13_sweep_load_policy.txt)
-        constexpr int LAUX = (POL == 2 || POL == 3) ? 0 : 2;
+        constexpr int LAUX = 2;
 #pragma unroll
         for (int k = 0; k < RB; ++k) {
             const int i = i0 + k < rows ? i0 + k : i0;
@@ -2321,7 +2452,7 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, T
             }
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc(Tr + (size_t)i * ldr, 0, oob, 0x00020000);
-            constexpr int SAUX = (POL == 1 || POL == 2) ? 16 : POL == 4 ? 2 : 0;
+            constexpr int SAUX = 16;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, jr * 8, 0, SAUX);
         }
     }
@@ -2346,9 +2477,7 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, T
 // loop, by the waves of the row slot s % G, from its stored values with the vector chain (one
 // column per lane).  The strips never write those rows, so the values read are the originals.
 // Grid, column order, regions, compaction and cache policy as k_sweep (POL 1), with 256-column
-// tiles.  Out of place (Tdst != Tsrc, the pipelined sweep): every swept element is written, also
-// when the batch selected no pivot (a copy).  meta (or null: the count from st): the batch's
-// count and swept slacks as its last block recorded them.
+// tiles.  In place (Tsrc == Tdst: the strips read through one pointer and write through the other).
 // NKB: 4-slot steps held (SX_HMAX / 4: one stage, 3 waves per SIMD; SX_KMAX / 4: two stages,
 // 2 waves per SIMD).
 template <int NKB>
@@ -2358,16 +2487,12 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
                                                    const PivRec *__restrict__ recs,
                                                    const unsigned long long *__restrict__ PM,
                                                    const unsigned long long *__restrict__ PM2,
-                                                   const DevState *__restrict__ st,
-                                                   const SweepMeta *__restrict__ meta, unsigned B, int rev,
+                                                   const DevState *__restrict__ st, unsigned B, int rev,
                                                    int *__restrict__ rec) {
     sweep_record(rec, st, nact);
-    const int cnt = meta ? (meta->tag == B ? meta->count : 0) : (st->batch_tag == B ? st->batch_count : 0);
-    if (cnt <= 0 && Tdst == Tsrc) return;
-    if (nact) {
-        const int na = meta && meta->nact >= 0 ? meta->nact : *nact;
-        if (s0 + na < Ns) Ns = s0 + na;
-    }
+    const int cnt = st->batch_tag == B ? st->batch_count : 0;
+    if (cnt <= 0) return;
+    if (nact && s0 + *nact < Ns) Ns = s0 + *nact;
     const int cb = (Ns + 255) / 256;
     const int lin = (int)(blockIdx.y * gridDim.x + blockIdx.x);
     const int G = (int)(gridDim.x * gridDim.y) / cb;
@@ -2900,34 +3025,23 @@ static int row_slots(int capacity, int col_blocks, int rows, int rb, float waves
     return (int)g;
 }
 
-template <int KT, int RB, int POL>
+template <int KT, int RB>
 static void launch_sweep_t(double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0, const Pending &pd,
                            const DevState *st, int rev, hipStream_t s) {
     const int cb = (Ns + 511) / 512;
-    dim3 grid(cb, row_slots(sweep_capacity<k_sweep<KT, RB, POL>>(), cb, rows, RB));
-    k_sweep<KT, RB, POL><<<grid, 256, 0, s>>>(T, rows, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st, pd.batch, rev,
-                                              g_sweep_rec);
+    dim3 grid(cb, row_slots(sweep_capacity<k_sweep<KT, RB>>(), cb, rows, RB));
+    k_sweep<KT, RB><<<grid, 256, 0, s>>>(T, rows, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, st, pd.batch, rev,
+                                         g_sweep_rec);
 }
 
-template <int KT, int POL>
-static void launch_sweep_rb(int rb, double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0,
-                            const Pending &pd, const DevState *st, int rev, hipStream_t s) {
-    switch (rb) {
-    case 1: launch_sweep_t<KT, 1, POL>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s); break;
-    case 2: launch_sweep_t<KT, 2, POL>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s); break;
-    default: launch_sweep_t<KT, 4, POL>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s); break;
-    }
-}
-
-// (the cache-policy variants 2..4 exist for full 32-slot sweeps only; smaller batches take 0 / 1)
+// rows per step: 4 for batches of more than 16 pivots, else 2 (round 1 measurements)
 template <int KT>
-static void launch_sweep_k(int rb, int pol, double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0,
-                           const Pending &pd, const DevState *st, int rev, hipStream_t s) {
-    if (KT == SX_HMAX && pol == 2) return launch_sweep_rb<KT, 2>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
-    if (KT == SX_HMAX && pol == 3) return launch_sweep_rb<KT, 3>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
-    if (KT == SX_HMAX && pol == 4) return launch_sweep_rb<KT, 4>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
-    if (pol == 0) return launch_sweep_rb<KT, 0>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
-    launch_sweep_rb<KT, 1>(rb, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+static void launch_sweep_k(double *T, int rows, size_t ld, TLay tl, int Ns, const int *nact, int s0, const Pending &pd,
+                           const DevState *st, int rev, hipStream_t s) {
+    if (KT > 16)
+        launch_sweep_t<KT, 4>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+    else
+        launch_sweep_t<KT, 2>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
 }
 
 // Row slots of the matrix-core sweeps (measured, profiles/r03_msweep_waves_ab.txt): the one-stage
@@ -2960,42 +3074,27 @@ void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, 
         if (cfg.batch > SX_HMAX) {
             dim3 grid(cb, msweep_slots(sweep_capacity<k_msweep<SX_KMAX / 4>>(), cb, rows, true));
             k_msweep<SX_KMAX / 4><<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM,
-                                                       pd.PM2, st, nullptr, pd.batch, rev, g_sweep_rec);
+                                                       pd.PM2, st, pd.batch, rev, g_sweep_rec);
         } else {
             dim3 grid(cb, msweep_slots(sweep_capacity<k_msweep<SX_HMAX / 4>>(), cb, rows, false));
             k_msweep<SX_HMAX / 4><<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM,
-                                                       pd.PM2, st, nullptr, pd.batch, rev, g_sweep_rec);
+                                                       pd.PM2, st, pd.batch, rev, g_sweep_rec);
         }
         return;
     }
     const int k = cfg.batch;  // pivots the sweep may have to apply (register slots)
     if (k <= 1)
-        launch_sweep_k<1>(cfg.rows_per_block, cfg.sc1, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+        launch_sweep_k<1>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else if (k <= 4)
-        launch_sweep_k<4>(cfg.rows_per_block, cfg.sc1, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+        launch_sweep_k<4>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else if (k <= 8)
-        launch_sweep_k<8>(cfg.rows_per_block, cfg.sc1, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+        launch_sweep_k<8>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else if (k <= 16)
-        launch_sweep_k<16>(cfg.rows_per_block, cfg.sc1, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+        launch_sweep_k<16>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else if (k <= SX_HMAX)
-        launch_sweep_k<SX_HMAX>(cfg.rows_per_block, cfg.sc1, T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
+        launch_sweep_k<SX_HMAX>(T, rows, ld, tl, Ns, nact, s0, pd, st, rev, s);
     else
         SX_FATAL("the vector sweep holds at most SX_HMAX slots");
-}
-
-void sx_launch_msweep_oop(const double *Tsrc, double *Tdst, int rows, int row0, size_t ld, TLay tl, int Ns,
-                          const int *nact, int s0, const Pending &pd, const DevState *st, const SweepMeta *meta, int rev,
-                          int grid_cap, hipStream_t s) {
-    if (rows <= 0) return;
-    if (ld % 2 != 0 || tl.ldA % 2 != 0 || (tl.jB < Ns && (tl.jB % 256 != 0 || tl.ldB % 2 != 0 || tl.offB % 2 != 0)))
-        SX_FATAL("matrix-core sweep: 16-byte rows and 256-aligned regions required");
-    const int cb = (Ns + 255) / 256;
-    auto kern = k_msweep<SX_KMAX / 4>;
-    const int full = sweep_capacity<k_msweep<SX_KMAX / 4>>();
-    const int cap = grid_cap > 0 ? std::min(grid_cap, full) : full;
-    dim3 grid(cb, row_slots(cap, cb, rows, 16));
-    kern<<<grid, 256, 0, s>>>(Tsrc, Tdst, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM, pd.PM2, st, meta,
-                              pd.batch, rev, nullptr);
 }
 
 // LDS history of a fused batch of k pivots: one stage
@@ -3007,7 +3106,7 @@ size_t sx_batch_granules_b() { return sx_gb_size(); }
 bool sx_batch_fits(int rows, Cols c, int k) {
     if (k < 1 || k > SX_KMAX || rows <= 0) return false;
     const int NA = (rows + SX_TILE - 1) / SX_TILE, NB = (c.N - 1 + SX_TILE - 1) / SX_TILE;
-    if (NA > SX_TILE || NB > SX_TILE || NB < 1) return false;
+    if (NA > SX_TILE || NB > SX_OBJ_TILES || NB < 1) return false;
     static int per_cu[SX_KMAX + 1] = {0};
     static int cus = 0;
     if (per_cu[k] == 0) {

@@ -8,7 +8,8 @@ n*100+m (main.cu:63) -- the same data the GPU generator produces bit for bit
 (tests/test_gpu_generator.py).  Each instance gets a wall-clock limit; an instance HiGHS does not
 finish is recorded with its status (the test skips it).
 
-usage: python tests/golden/scripts/make_highs_objectives.py [name ...] [--time-limit S]
+usage: python tests/golden/scripts/make_highs_objectives.py [name ...] [--time-limit S] [--method highs-ipm]
+(a method other than the default is recorded under "<name>_<method>")
 """
 import json
 import os
@@ -40,6 +41,10 @@ def main():
     if "--time-limit" in sys.argv:
         limit = float(sys.argv[sys.argv.index("--time-limit") + 1])
         args = [a for a in args if a != sys.argv[sys.argv.index("--time-limit") + 1]]
+    method = "highs"
+    if "--method" in sys.argv:
+        method = sys.argv[sys.argv.index("--method") + 1]
+        args = [a for a in args if a != method]
     names = args or list(CASES)
     out = {}
     if os.path.exists(OUT):
@@ -49,15 +54,15 @@ def main():
         n, m, seed, lo, hi = CASES[name]
         A, b, c = oracle.generate(n, m, seed, lo, hi)
         t0 = time.time()
-        r = linprog(-c, A_ub=A, b_ub=b, bounds=[(0, None)] * n, method="highs",
+        r = linprog(-c, A_ub=A, b_ub=b, bounds=[(0, None)] * n, method=method,
                     options={"time_limit": limit, "presolve": True})
         dt = time.time() - t0
         del A
         rec = {"n": n, "m": m, "seed": seed, "lo": lo, "hi": hi, "highs_status": int(r.status),
-               "highs_message": str(r.message), "seconds": round(dt, 1), "scipy": "1.15.3", "method": "highs"}
+               "highs_message": str(r.message), "seconds": round(dt, 1), "scipy": "1.15.3", "method": method}
         if r.status == 0:
             rec["highs_opt"] = float(-r.fun)
-        out[name] = rec
+        out[name if method == "highs" else f"{name}_{method}"] = rec
         print(name, rec, flush=True)
         with open(OUT, "w") as f:
             json.dump(out, f, indent=1, sort_keys=True)

@@ -91,7 +91,9 @@ def test_cli_rejects_bad_options(tmp_path):
     r = run(["--frobnicate", "1", "-r", "3", "3", "1"], tmp_path)
     assert r.returncode == 255 and "Unknown option --frobnicate" in r.stderr
     r = run(["--gpus", "0", "-r", "3", "3", "1"], tmp_path)
-    assert r.returncode == 255 and "--gpus: expected 1..64" in r.stderr
+    assert r.returncode == 255 and "--gpus: expected 1..8 GPUs, got 0" in r.stderr
+    r = run(["--gpus", "9", "-r", "3", "3", "1"], tmp_path)  # (SIMPLEX_MAX_GPUS shards at most)
+    assert r.returncode == 255 and "--gpus: expected 1..8 GPUs, got 9" in r.stderr
 
 
 @pytest.mark.gpu

@@ -228,7 +228,7 @@ def test_session_two_stage_batches(gpu):
 
 def _pivots_with(cfg, T, d, base, k):
     Tg, dg, bg = T.copy(), d.copy(), base.copy()
-    setters = {"batch": (sx.set_batch, 0), "rb": (sx.set_update_rows, 0), "sc1": (sx.set_store_sc1, -1),
+    setters = {"batch": (sx.set_batch, 0),
                "fused": (sx.set_fused, -1), "p2p": (sx.set_p2p, -1),
                "waves": (sx.set_update_waves, 0), "W": (sx.set_virtual_ranks, 1),
                "mfma": (sx.set_sweep_mfma, -1)}
@@ -257,25 +257,21 @@ def test_batched_sweep_bit_exact(gpu, batch, fused):
 
 
 @pytest.mark.parametrize("batch", [1, 3, 7, 16, 17])
-@pytest.mark.parametrize("rb", [1, 4])
-def test_vector_sweep_slots_bit_exact(gpu, batch, rb):
+def test_vector_sweep_slots_bit_exact(gpu, batch):
     """the vector sweep (simplex_set_sweep_mfma(0)) at every register-slot variant (1, 4, 8, 16,
-    32 slots) and row step, with a partial last batch"""
+    32 slots) and both row steps (2 rows up to 16 slots, 4 above), with a partial last batch"""
     T, d, base = _phase1_state(333, 1025, 7)
-    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "rb": rb, "mfma": 0}, T, d, base, 45)
+    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "mfma": 0}, T, d, base, 45)
     oracle.solve(T, d, base, max_pivots=45)
     assert done == 45
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 
 @pytest.mark.parametrize("batch", [20, 32])
-@pytest.mark.parametrize("rb", [1, 2, 4])
-@pytest.mark.parametrize("sc1", [0, 1])
-def test_large_batch_sweeps_bit_exact(gpu, batch, rb, sc1):
-    """the vector sweep's 32-slot variant (batches above 16 pivots), every row step and store
-    flavour, with a partial last batch"""
+def test_large_batch_sweeps_bit_exact(gpu, batch):
+    """the vector sweep's 32-slot variant (batches above 16 pivots), with a partial last batch"""
     T, d, base = _phase1_state(333, 1025, 7)
-    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "rb": rb, "sc1": sc1, "mfma": 0}, T, d, base, 70)
+    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "mfma": 0}, T, d, base, 70)
     oracle.solve(T, d, base, max_pivots=70)
     assert done == 70
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
@@ -398,13 +394,13 @@ def test_p2p_fused_two_phase_two_stages(gpu, W, n, m, seed, lo, hi):
         sx.set_virtual_ranks(1)
 
 
-@pytest.mark.parametrize("sc1", [0, 1])
+@pytest.mark.parametrize("mfma", [1, 0])
 @pytest.mark.parametrize("waves", [1e-4, 0.3, 1, 4])
-def test_sweep_grid_bit_exact(gpu, sc1, waves):
+def test_sweep_grid_bit_exact(gpu, mfma, waves):
     """one block per column tile walking every row group (both directions) up to more blocks
-    than row groups; plain and write-through stores"""
+    than row groups; both sweeps"""
     T, d, base = _phase1_state(210, 1700, 3)
-    Tg, dg, bg, st, done = _pivots_with({"sc1": sc1, "waves": waves, "batch": 16}, T, d, base, 90)
+    Tg, dg, bg, st, done = _pivots_with({"mfma": mfma, "waves": waves, "batch": 16}, T, d, base, 90)
     oracle.solve(T, d, base, max_pivots=90)
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
