@@ -101,6 +101,15 @@ void simplex_set_regions(int mode);
  * launch per rank on its own stream (0; needs as many hardware queues running at once) */
 void simplex_set_mr_single_launch(int on);
 
+/* the pending pivot rows U (written by peer ranks in the multi-rank batch) in fine-grained memory:
+ * -1 auto (when the shards span devices, default), 1 always (test hook: the one-GPU cost and
+ * parity of that path), 0 never */
+void simplex_set_fine_pivot_rows(int mode);
+/* new engines' tableau storage inside each region: -1 default (4x4 blocks unless the environment sets
+ * SIMPLEX_BLOCKED=0), 1 blocks of 4 rows x 4 columns in 16-row strips, 0 plain row-major (DESIGN.md §2;
+ * callers' tableaux, tabular.h, are always row-major) */
+void simplex_set_blocked(int mode);
+
 /* ---- fault handling and test hooks ---- */
 /* a fused batch whose in-kernel hand-off wait times out (SIMPLEX_HANG, never expected) is
  * undone and re-run on the per-pivot path; this counts such recoveries in the process */

@@ -95,6 +95,7 @@ struct BatchChan {
     alignas(128) unsigned abort_w;   // a wait timed out: every block leaves
     alignas(128) unsigned inject_q;  // test hook: 1 + the slot at which ratio block 0 (of rank 0)
                                      // leaves with the batch aborted (0: off); the last block clears it
+    alignas(128) unsigned backoff;   // k_batch: adaptive poll back-off on (1) / off (0)
 };
 
 // Multi-rank fused batch (k_batch_mr): every rank's buffers as seen from this rank (peer
@@ -143,17 +144,30 @@ struct Cols {
     }
 };
 
-// Tableau storage in HBM: two row-major regions.  Region A holds stored
-// columns [0, jB) of every row at stride ldA; region B, starting offB doubles later, holds
-// stored columns [jB, Ns) at stride ldB.  With slack compaction the swept columns
-// [0, 1 + n + nact) lie in region A while nact fits, so the sweep streams dense rows (a row of
-// A is only a little wider than what is swept) instead of a prefix of every full-width row;
-// without a region B (jB = Ns, the default for small m and for callers' tableaux) this is the
-// plain row-major layout.  jB is a multiple of 512, so no 512-column tile straddles the two.
+// Tableau storage in HBM: two regions.  Region A holds stored columns [0, jB) of
+// every row at stride ldA; region B, starting offB doubles later, holds stored columns [jB, Ns)
+// at stride ldB.  With slack compaction the swept columns [0, 1 + n + nact) lie in region A while
+// nact fits, so the sweep streams dense rows (a row of A is only a little wider than what is
+// swept) instead of a prefix of every full-width row; without a region B (jB = Ns, the default for
+// small m and for callers' tableaux) there is one region.  jB is a multiple of 512, so no
+// 512-column tile straddles the two.
+// Inside a region, blk = 0: plain row-major (callers' tableaux: tabular.h); blk = 1 (the engine's
+// own tableaux): 16-row strips of ld * 16 doubles, each strip a sequence of 4-column
+// groups of 64 doubles, each group 4 blocks of 4 rows x 4 columns (one 128-byte line each).  A
+// column of 512 rows then spans 128 lines instead of 512 (the fused batch's entering-column
+// gather), a row's 512 columns 128 lines instead of 32 (its pivot-row read), and a strip is still
+// one contiguous range (the sweep); two adjacent columns 2c, 2c + 1 of a row stay adjacent.
+// Rows are allocated in whole strips.
 struct TLay {
     size_t ldA = 0, ldB = 0, offB = 0;
     int jB = 0x7fffffff;
+    int blk = 0;
+    __host__ __device__ __forceinline__ static size_t b4(long long i, int j, size_t ld) {
+        return (size_t)(i >> 4) * 16 * ld + (size_t)(j >> 2) * 64 + (size_t)(((int)i & 15) >> 2) * 16 +
+               (size_t)(((int)i & 3) * 4 + (j & 3));
+    }
     __host__ __device__ __forceinline__ size_t idx(long long i, int j) const {
+        if (blk) return j < jB ? b4(i, j, ldA) : offB + b4(i, j - jB, ldB);
         return j < jB ? (size_t)i * ldA + (size_t)j : offB + (size_t)i * ldB + (size_t)(j - jB);
     }
 };
@@ -235,10 +249,15 @@ void sx_launch_build_rows(double *T, int rows, int row0, TLay tl, int n, int m, 
                           const double *b_full, hipStream_t s);
 void sx_launch_init_vectors(double *d, int N1, int n, int m, int *base, hipStream_t s);
 void sx_launch_phase2_costs(double *d, int n, int m, const double *c, hipStream_t s);
-void sx_launch_gather_rhs(const double *T, int rows, size_t ld, double *out, hipStream_t s);
+void sx_launch_gather_rhs(const double *T, int rows, TLay tl, double *out, hipStream_t s);
+// rows [i0, i0 + nr), stored columns [0, Ns) -> row-major out (nr x Ns); and row-major in (pitch
+// ld_in) -> stored columns [j0, j0 + Ns) of those rows
+void sx_launch_rows_out(const double *T, TLay tl, int i0, int nr, int Ns, double *out, hipStream_t s);
+void sx_launch_rows_in(double *T, TLay tl, int i0, int nr, int Ns, int j0, const double *in, size_t ld_in,
+                       hipStream_t s);
 // device generator (sx_generator.hip) and the CRT seeding (sx_problem.cpp)
 void sx_crt_seeds(unsigned seed, int kind, uint32_t out[3]);
-void sx_launch_gen_rows(uint32_t seedA, int n, int m, int row0, int rows, double lo, double hi, double *T, size_t ld,
+void sx_launch_gen_rows(uint32_t seedA, int n, int m, int row0, int rows, double lo, double hi, double *T, TLay tl,
                         double *A_cm, hipStream_t s);
 void sx_launch_gen_vector(uint32_t seed, long long first, int count, double lo, double hi, double *out,
                           hipStream_t s);

@@ -78,6 +78,9 @@ struct Config {
     int inject_slot = -1;          // ... before it starts (-1) or at this slot (inside the kernel)
     int mr_two_stage = -1;         // peer-memory multi-rank batches of two stages (-1: unless SIMPLEX_MR_STAGES=1)
     unsigned first_batch_id = 1;   // test hook: batch id of a new engine's first batch
+    int fine_u = -1;               // U in fine-grained memory: -1 across devices, 1 always, 0 never
+    int blocked = -1;              // the engine's tableaux in 4x4 blocks (TLay::blk): -1 default (on unless
+                                   // SIMPLEX_BLOCKED=0), 0 row-major, 1 blocked
     int ipc_rank = -1, ipc_world = 0;  // test hook: one shard per process, peers through IPC handles, no RCCL
     long long hang_recoveries = 0; // fused batches aborted and re-run on the per-pivot path
     long long fused_batches = 0;   // fused batch launches (every shard's counted once)
@@ -220,6 +223,16 @@ std::vector<int> shard_devices() {
 
 bool gpus_selftest(const std::vector<int> &devs);  // (below two_phase)
 
+// the engine's own tableaux in 4x4 blocks (TLay::blk) unless SIMPLEX_BLOCKED=0 or
+// simplex_set_blocked(0)
+bool use_blocked() {
+    if (g_cfg.blocked < 0) {
+        const char *e = getenv("SIMPLEX_BLOCKED");
+        return !(e && atoi(e) == 0);
+    }
+    return g_cfg.blocked != 0;
+}
+
 // makes `dev` current for its scope
 struct DevGuard {
     int prev = -1;
@@ -273,6 +286,7 @@ struct Shard {
     int dev = 0;                      // the device holding the shard's buffers
     hipStream_t s = nullptr;          // the engine's stream on that device (every per-shard operation)
     int urec = -1;                    // ga / gb / gdone: index of the uncached record set (g_urec), or -1
+    bool fineU = false;               // U in fine-grained memory (peers on other devices write it)
     DevState *st = nullptr;
 };
 
@@ -363,6 +377,7 @@ class Engine {
         // with rows 4.4x wider than the swept part, profiles/r02_sweep_row_stride.txt)
         tl.ldA = ld;
         tl.jB = Ns1;
+        tl.blk = alias && use_blocked() ? 1 : 0;  // (callers' tableaux -- tabular.h, no aliasing -- stay row-major)
         if (alias && g_cfg.regions) {
             const int capA = g_cfg.regions >= 2 ? g_cfg.regions : std::max(4096, (m + 7) / 8);
             const int jB = (int)round_up((size_t)(1 + n + capA), SX_TILE);
@@ -627,8 +642,9 @@ class Engine {
         }
     }
 
-    // doubles of a shard's tableau allocation
+    // doubles of a shard's tableau allocation (the blocked layout: whole 16-row strips)
     size_t t_doubles(size_t rows_alloc) const {
+        if (tl.blk) rows_alloc = round_up(rows_alloc, 16);
         return tl.jB < Ns1 ? tl.offB + (size_t)rpr * tl.ldB : rows_alloc * ld;
     }
 
@@ -655,9 +671,18 @@ class Engine {
     void alloc_shard(Shard &x) {
         const size_t rows_alloc = x.rows > 0 ? (size_t)x.rows : 1;
         x.T = dalloc<double>(t_doubles(rows_alloc));
-        // d and U: plain device memory (the coherence of the rows other ranks write).
+        // d: plain device memory (no rank writes another's).  U: other ranks write the pending pivot
+        // rows into it over xGMI (system-scope stores) in the multi-rank batch, and this rank's sweep
+        // reads them with plain loads in a later kernel.  Across devices it is fine-grained memory
+        // (coherent with the peers' system-scope writes by construction, not through this device's
+        // L2: DESIGN.md §5); on one device, or when forced off, plain device memory.
         x.d = dalloc<double>(round_up((size_t)N1, 16));
-        x.U = dalloc<double>((size_t)SX_KMAX * ld);
+        x.fineU = g_cfg.fine_u > 0 || (g_cfg.fine_u < 0 && ((rccl && !ipc) || multidev));
+        if (x.fineU)
+            SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&x.U), (size_t)SX_KMAX * ld * sizeof(double),
+                                         hipDeviceMallocFinegrained));
+        else
+            x.U = dalloc<double>((size_t)SX_KMAX * ld);
         x.d_save = dalloc<double>(round_up((size_t)N1, 16));
         x.colE = dalloc<double>(rows_alloc);
         x.prow = dalloc<double>(ld);
@@ -703,6 +728,12 @@ class Engine {
         }
         if (x.gdone) SX_HIP(hipMemsetAsync(x.gdone, 0, SX_MAXW * 8, x.s));
         SX_HIP(hipMemsetAsync(x.chan, 0, sizeof(BatchChan), x.s));
+        {  // the fused batch's adaptive poll back-off (SIMPLEX_BACKOFF=0 turns it off)
+            const char *e = getenv("SIMPLEX_BACKOFF");
+            const unsigned bo = (e && atoi(e) == 0) ? 0u : 1u;
+            SX_HIP(hipMemcpyAsync(&x.chan->backoff, &bo, sizeof(unsigned), hipMemcpyHostToDevice, x.s));
+            SX_HIP(hipStreamSynchronize(x.s));
+        }
         SX_HIP(hipMemsetAsync(x.ga, 0, sx_batch_granules_a() * sizeof(unsigned long long), x.s));
         SX_HIP(hipMemsetAsync(x.gb, 0, sx_batch_granules_b() * sizeof(unsigned long long), x.s));
         x.tiles_local = dalloc<TilePart>(slots);
@@ -782,7 +813,7 @@ class Engine {
         SX_HIP(hipStreamSynchronize(s));
         for (auto &x : sh) {
             DevGuard g(x.dev);
-            sx_launch_gen_rows(sd[2], n, m, x.row0, x.rows, lo, hi, x.T, tl.ldA, nullptr, x.s);  // (region A)
+            sx_launch_gen_rows(sd[2], n, m, x.row0, x.rows, lo, hi, x.T, tl, nullptr, x.s);
             sx_launch_build_rows(x.T, x.rows, x.row0, tl, n, m, Ns1, nullptr, b_dev, x.s);
             sx_launch_init_vectors(x.d, N1, n, m, x.base, x.s);
         }
@@ -1409,7 +1440,7 @@ class Engine {
         out.assign(m, 0.0);
         for (auto &x : sh) {
             DevGuard g(x.dev);
-            sx_launch_gather_rhs(x.T, x.rows, tl.ldA, x.rhs_local, x.s);  // (column 0: region A)
+            sx_launch_gather_rhs(x.T, x.rows, tl, x.rhs_local, x.s);
         }
         if (xchg) {
             allgather_doubles(&Shard::rhs_local, &Shard::rhs_all, rpr);
@@ -1439,11 +1470,26 @@ class Engine {
             tmp.assign((size_t)x.rows * c.Ns, 0.0);
             const int wa = std::min(c.Ns, tl.jB);  // region A's columns, then region B's
             DevGuard g(x.dev);
-            SX_HIP(hipMemcpy2DAsync(tmp.data(), c.Ns * sizeof(double), x.T, tl.ldA * sizeof(double),
-                                    wa * sizeof(double), x.rows, hipMemcpyDeviceToHost, x.s));
-            if (wa < c.Ns)
-                SX_HIP(hipMemcpy2DAsync(tmp.data() + wa, c.Ns * sizeof(double), x.T + tl.offB, tl.ldB * sizeof(double),
-                                        (c.Ns - wa) * sizeof(double), x.rows, hipMemcpyDeviceToHost, x.s));
+            if (tl.blk) {
+                // blocked storage: rows converted to row-major on the device, a chunk at a time
+                const int chunk = (int)std::max<size_t>(16, std::min<size_t>((size_t)x.rows, (64u << 20) / (8 * (size_t)c.Ns)));
+                double *buf = dalloc<double>((size_t)chunk * c.Ns);
+                for (int i0 = 0; i0 < x.rows; i0 += chunk) {
+                    const int nr = std::min(chunk, x.rows - i0);
+                    sx_launch_rows_out(x.T, tl, i0, nr, c.Ns, buf, x.s);
+                    SX_HIP(hipMemcpyAsync(tmp.data() + (size_t)i0 * c.Ns, buf, sizeof(double) * nr * c.Ns,
+                                          hipMemcpyDeviceToHost, x.s));
+                }
+                SX_HIP(hipStreamSynchronize(x.s));
+                (void)hipFree(buf);
+            } else {
+                SX_HIP(hipMemcpy2DAsync(tmp.data(), c.Ns * sizeof(double), x.T, tl.ldA * sizeof(double),
+                                        wa * sizeof(double), x.rows, hipMemcpyDeviceToHost, x.s));
+                if (wa < c.Ns)
+                    SX_HIP(hipMemcpy2DAsync(tmp.data() + wa, c.Ns * sizeof(double), x.T + tl.offB,
+                                            tl.ldB * sizeof(double), (c.Ns - wa) * sizeof(double), x.rows,
+                                            hipMemcpyDeviceToHost, x.s));
+            }
             SX_HIP(hipStreamSynchronize(x.s));
             for (int i = 0; i < x.rows; ++i) {
                 double *dst = T_host + (size_t)((local_rows ? 0 : x.row0) + i) * ld_host;
@@ -1470,11 +1516,28 @@ class Engine {
             if (x.rows > 0) {
                 const double *src = T_host + (size_t)(local_rows ? 0 : x.row0) * ld_host;
                 const int wa = std::min(c.Ns, tl.jB);  // region A's columns, then region B's
-                SX_HIP(hipMemcpy2DAsync(x.T, tl.ldA * sizeof(double), src, ld_host * sizeof(double),
-                                        wa * sizeof(double), x.rows, hipMemcpyHostToDevice, x.s));
-                if (wa < c.Ns)
-                    SX_HIP(hipMemcpy2DAsync(x.T + tl.offB, tl.ldB * sizeof(double), src + wa, ld_host * sizeof(double),
-                                            (c.Ns - wa) * sizeof(double), x.rows, hipMemcpyHostToDevice, x.s));
+                if (tl.blk) {
+                    // blocked storage: row-major chunks to the device, placed by a kernel
+                    const int chunk =
+                        (int)std::max<size_t>(16, std::min<size_t>((size_t)x.rows, (64u << 20) / (8 * (size_t)c.Ns)));
+                    double *buf = dalloc<double>((size_t)chunk * c.Ns);
+                    for (int i0 = 0; i0 < x.rows; i0 += chunk) {
+                        const int nr = std::min(chunk, x.rows - i0);
+                        SX_HIP(hipMemcpy2DAsync(buf, c.Ns * sizeof(double), src + (size_t)i0 * ld_host,
+                                                ld_host * sizeof(double), c.Ns * sizeof(double), nr,
+                                                hipMemcpyHostToDevice, x.s));
+                        sx_launch_rows_in(x.T, tl, i0, nr, c.Ns, 0, buf, c.Ns, x.s);
+                    }
+                    SX_HIP(hipStreamSynchronize(x.s));
+                    (void)hipFree(buf);
+                } else {
+                    SX_HIP(hipMemcpy2DAsync(x.T, tl.ldA * sizeof(double), src, ld_host * sizeof(double),
+                                            wa * sizeof(double), x.rows, hipMemcpyHostToDevice, x.s));
+                    if (wa < c.Ns)
+                        SX_HIP(hipMemcpy2DAsync(x.T + tl.offB, tl.ldB * sizeof(double), src + wa,
+                                                ld_host * sizeof(double), (c.Ns - wa) * sizeof(double), x.rows,
+                                                hipMemcpyHostToDevice, x.s));
+                }
             }
             if (d_host) SX_HIP(hipMemcpyAsync(x.d, d_host, sizeof(double) * width, hipMemcpyHostToDevice, x.s));
             if (base_host) SX_HIP(hipMemcpyAsync(x.base, base_host, sizeof(int) * m, hipMemcpyHostToDevice, x.s));
@@ -1755,6 +1818,8 @@ void simplex_set_hang_inject(long long batches) { g_cfg.inject_hang = batches >=
 void simplex_set_hang_inject_slot(int slot) { g_cfg.inject_slot = slot >= 0 ? slot : -1; }
 long long simplex_hang_recoveries(void) { return g_cfg.hang_recoveries; }
 long long simplex_fused_batches(void) { return g_cfg.fused_batches; }
+void simplex_set_fine_pivot_rows(int mode) { g_cfg.fine_u = mode < 0 ? -1 : (mode ? 1 : 0); }
+void simplex_set_blocked(int mode) { g_cfg.blocked = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_first_batch_id(unsigned int id) { g_cfg.first_batch_id = (id >= 1 && id < SX_BATCH_IDS) ? id : 1; }
 
 void enableBenchmarkMode(void) { g_cfg.benchmark = true; }
@@ -2159,20 +2224,24 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     SX_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     uint32_t sd[3];
     sx_crt_seeds(seed, 0, sd);
-    double *T = dalloc<double>((size_t)rows * ld);
+    TLay btl;  // one region, the engine's storage (row-major, or 4x4 blocks in whole 16-row strips)
+    btl.ldA = ld;
+    btl.jB = cols;
+    btl.blk = use_blocked() ? 1 : 0;
+    const size_t rows_alloc = btl.blk ? round_up((size_t)rows, 16) : (size_t)rows;
+    double *T = dalloc<double>(rows_alloc * ld);
     double *U = dalloc<double>((size_t)SX_KMAX * ld);
     double *F = dalloc<double>(round_up((size_t)rows, 16) * SX_KMAX);
     PivRec *recs = dalloc<PivRec>(SX_KMAX);
     unsigned long long *PM = dalloc<unsigned long long>(rows);
     unsigned long long *PM2 = dalloc<unsigned long long>(rows);
     DevState *st = dalloc<DevState>(1);
-    SX_HIP(hipMemsetAsync(T, 0, sizeof(double) * (size_t)rows * ld, s));
+    SX_HIP(hipMemsetAsync(T, 0, sizeof(double) * rows_alloc * ld, s));
     // column 0 = b (first CRT seed), columns 1.. = A's rows (third), as generateRandomProblem
     double *b_dev = dalloc<double>(rows);
     sx_launch_gen_vector(sd[0], 0, rows, lo, hi, b_dev, s);
-    sx_launch_gen_rows(sd[2], cols - 1, rows, 0, rows, lo, hi, T, ld, nullptr, s);
-    SX_HIP(hipMemcpy2DAsync(T, ld * sizeof(double), b_dev, sizeof(double), sizeof(double), rows,
-                            hipMemcpyDeviceToDevice, s));
+    sx_launch_gen_rows(sd[2], cols - 1, rows, 0, rows, lo, hi, T, btl, nullptr, s);
+    sx_launch_rows_in(T, btl, 0, rows, 1, 0, b_dev, 1, s);
     SX_HIP(hipStreamSynchronize(s));
     (void)hipFree(b_dev);
     SX_HIP(hipMemsetAsync(U, 0, sizeof(double) * SX_KMAX * ld, s));
@@ -2205,9 +2274,6 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     pd.PM2 = PM2;
     pd.batch = B;
     pd.q = pivots;
-    TLay btl;  // one region: rows of ld doubles
-    btl.ldA = ld;
-    btl.jB = cols;
     SweepCfg cfg;
     cfg.batch = pivots;
     cfg.mfma = pivots > SX_HMAX ? 1 : (g_cfg.sweep_mfma >= 0 ? g_cfg.sweep_mfma : 1);
@@ -2292,7 +2358,7 @@ problem_t *simplex_generate_problem_device(int n, int m, unsigned int seed, int 
     double *A = dalloc<double>((size_t)n * m), *b = dalloc<double>(m), *c = dalloc<double>(n);
     sx_launch_gen_vector(sd[0], 0, m, lo, hi, b, s);
     sx_launch_gen_vector(sd[1], 0, n, lo, hi, c, s);
-    sx_launch_gen_rows(sd[2], n, m, 0, m, lo, hi, nullptr, 0, A, s);
+    sx_launch_gen_rows(sd[2], n, m, 0, m, lo, hi, nullptr, TLay(), A, s);
     if (n > 0 && m > 0)
         SX_HIP(hipMemcpyAsync(p->constraintsMatrix, A, sizeof(double) * (size_t)n * m, hipMemcpyDeviceToHost, s));
     if (m > 0) SX_HIP(hipMemcpyAsync(p->knownTermsVector, b, sizeof(double) * m, hipMemcpyDeviceToHost, s));

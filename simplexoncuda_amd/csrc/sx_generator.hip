@@ -114,10 +114,11 @@ __device__ __forceinline__ double value_of(uint32_t x, double lo, double span) {
 }
 
 // A for rows [row0, row0+rows) of an n-column problem: chunk c of row i covers columns
-// [c*CH, c*CH+CH).  Output either the tableau (T[i*ld + 1 + j]) or column-major A_cm[j*m + row0+i].
+// [c*CH, c*CH+CH).  Output either the tableau (element (i, 1 + j) in the layout tl, region A) or
+// column-major A_cm[j*m + row0+i].
 template <int CH>
 __global__ __launch_bounds__(256) void k_gen_A(uint32_t seed, int n, int m, int row0, int rows, double lo, double span,
-                                               const uint32_t *__restrict__ jumps, double *T, size_t ld,
+                                               const uint32_t *__restrict__ jumps, double *T, TLay tl,
                                                double *A_cm) {
     const int chunks = (n + CH - 1) / CH;
     const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -128,8 +129,7 @@ __global__ __launch_bounds__(256) void k_gen_A(uint32_t seed, int n, int m, int 
     xw_init(s, seed);
     xw_skip(s, (uint64_t)(row0 + i) * (uint64_t)n + (uint64_t)j0, jumps);
     if (T) {
-        double *row = T + (size_t)i * ld + 1;
-        for (int j = j0; j < j1; ++j) row[j] = value_of(xw_next(s), lo, span);
+        for (int j = j0; j < j1; ++j) T[tl.idx(i, 1 + j)] = value_of(xw_next(s), lo, span);
     } else {
         for (int j = j0; j < j1; ++j) A_cm[(size_t)j * m + row0 + i] = value_of(xw_next(s), lo, span);
     }
@@ -158,13 +158,13 @@ const uint32_t *sx_jump_tables() {
     return g_jump_dev;
 }
 
-void sx_launch_gen_rows(uint32_t seedA, int n, int m, int row0, int rows, double lo, double hi, double *T, size_t ld,
+void sx_launch_gen_rows(uint32_t seedA, int n, int m, int row0, int rows, double lo, double hi, double *T, TLay tl,
                         double *A_cm, hipStream_t s) {
     if (rows <= 0 || n <= 0) return;
     constexpr int CH = 128;
     const long long threads = (long long)rows * ((n + CH - 1) / CH);
     const int blocks = (int)((threads + 255) / 256);
-    k_gen_A<CH><<<blocks, 256, 0, s>>>(seedA, n, m, row0, rows, lo, hi - lo, sx_jump_tables(), T, ld, A_cm);
+    k_gen_A<CH><<<blocks, 256, 0, s>>>(seedA, n, m, row0, rows, lo, hi - lo, sx_jump_tables(), T, tl, A_cm);
 }
 
 void sx_launch_gen_vector(uint32_t seed, long long first, int count, double lo, double hi, double *out,

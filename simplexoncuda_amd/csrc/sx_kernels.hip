@@ -726,11 +726,14 @@ __device__ __forceinline__ void poll_pause() { __builtin_amdgcn_s_sleep(1); }
 // barrier per poll; payf(k, payload) is called for every granule as it arrives.  Wave-uniform
 // result: false when the batch was aborted (or this wait timed out, which aborts it).  Only wave 0
 // may call it.
+// presleep (100 MHz ticks): the wave first sleeps that long -- a consumer that knows its records
+// cannot land sooner keeps its polls off the memory system meanwhile.
 template <typename OFF, bool SYS, int PL, typename PAYF>
 __device__ __forceinline__ int poll_wave_f(const u64 *base, int n, OFF off, unsigned tag, unsigned *out, unsigned *abort_w,
-                           unsigned long long timeout, PAYF payf) {
+                           unsigned long long timeout, PAYF payf, unsigned presleep = 0u) {
     const int t = threadIdx.x;
     const u64 t0 = __builtin_amdgcn_s_memrealtime();
+    while (presleep && __builtin_amdgcn_s_memrealtime() - t0 < presleep) __builtin_amdgcn_s_sleep(8);
     if (n <= 64) {
         bool have = t >= n;
         for (unsigned it = 0;; ++it) {
@@ -789,11 +792,22 @@ __device__ __forceinline__ int poll_wave_f(const u64 *base, int n, OFF off, unsi
 // granules come in pairs), or dropped (pay null).
 template <typename OFF, bool SYS = false>
 __device__ int poll_wave(const u64 *base, int n, OFF off, unsigned tag, unsigned *out, unsigned *abort_w,
-                         unsigned long long timeout, unsigned *pay) {
+                         unsigned long long timeout, unsigned *pay, unsigned presleep = 0u) {
     return poll_wave_f<OFF, SYS, SX_GATHER_PER_LANE>(base, n, off, tag, out, abort_w, timeout,
                                                      [pay](int k, unsigned pl) {
                                                          if (pay && !(k & 1)) pay[k >> 1] = pl;
-                                                     });
+                                                     },
+                                                     presleep);
+}
+
+// Adaptive poll back-off of a fused batch's waits: sleep for the previous pivot's wait less a
+// margin (SX_BACKOFF_MARGIN ticks of 10 ns), at most SX_BACKOFF_MAX; updated from each wait.
+#define SX_BACKOFF_MARGIN 120u
+#define SX_BACKOFF_MAX 800u
+__device__ __forceinline__ unsigned next_backoff(unsigned long long waited) {
+    if (waited <= SX_BACKOFF_MARGIN) return 0u;
+    const unsigned long long b = waited - SX_BACKOFF_MARGIN;
+    return b > SX_BACKOFF_MAX ? SX_BACKOFF_MAX : (unsigned)b;
 }
 
 // Pass 2 of the reference's argmin (deviceReduceKernel<false><<<1,1024>>>, reduction.cu:239-241)
@@ -1296,6 +1310,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
     int status = SX_NOT_ENDED, cnt = 0;
     bool aborted = false;
     const unsigned inj = ch->inject_q;  // (test hook, normally 0)
+    const bool backoff = ch->backoff != 0u;
     if (status0 == SX_NOT_ENDED) {
         // ratio block: its row; objective block: its logical column d[1 + ia]
         const int li = blockIdx.x * SX_TILE + t;
@@ -1347,6 +1362,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
             // of the current stage; wu1: U[s][e] of the first stage), loaded by every wave with the
             // column's stored values (the fresh slot from the objective record)
             double wu = 0.0, wu1 = 0.0;
+            unsigned pre_c = 0u;  // (wave 0) back-off before polling the objective records
             for (int q = 0; q < K; ++q) {
                 const unsigned tag = make_tag(B, q);
                 if (cap >= 0 && piv0 + q >= cap) {
@@ -1501,10 +1517,14 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 // winner's record (wave 0 polls; one block barrier)
                 if (t < 64) {
                     unsigned short *po = s_payo;
+                    const u64 ta = __builtin_amdgcn_s_memrealtime();
                     const int ok = poll_wave_f<Rec4All, false, SX_OBJ_PER_LANE>(
-                        gb, SX_GB4 * NB, Rec4All(), tag, s_g, &ch->abort_w, 20000000ull, [po](int k, unsigned pl) {
+                        gb, SX_GB4 * NB, Rec4All(), tag, s_g, &ch->abort_w, 20000000ull,
+                        [po](int k, unsigned pl) {
                             if ((k & 3) < 3) po[(k & 3) * SX_OBJ_TILES + (k >> 2)] = (unsigned short)pl;
-                        });
+                        },
+                        pre_c);
+                    if (backoff) pre_c = next_backoff(__builtin_amdgcn_s_memrealtime() - ta);
                     double ev = DBL_MAX;
                     int ei = -1, any = 0;
                     if (ok) wave_pass2<SX_GB4, unsigned short>(s_g, s_payo, NB, s_v, s_i, ev, ei, any);
@@ -1544,6 +1564,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 }
             }
         } else {
+            unsigned pre_a = 0u;  // (wave 0) back-off before polling the ratio records
             for (int q = 0; q < K; ++q) {
                 const unsigned tag = make_tag(B, q);
                 if (cap >= 0 && piv0 + q >= cap) {
@@ -1554,7 +1575,9 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 const int qq = q - hb;  // slot within the stage
                 // ---- selection: pass 2 over the ratio tiles (wave 0 polls and runs the tree)
                 if (t < 64) {
-                    const int ok = poll_wave(ga, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
+                    const u64 ta = __builtin_amdgcn_s_memrealtime();
+                    const int ok = poll_wave(ga, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, 20000000ull, s_pay, pre_a);
+                    if (backoff) pre_a = next_backoff(__builtin_amdgcn_s_memrealtime() - ta);
                     double tv = DBL_MAX;
                     int ti = -1, any = 0;
                     if (ok) wave_pass2(s_g, s_pay, NA, s_v, s_i, tv, ti, any);
@@ -2390,7 +2413,14 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, T
     for (int s = 0; s < KT; ++s)
         u[s] = s < cnt ? *reinterpret_cast<const double2 *>(U + (size_t)s * ld + j) : make_double2(0.0, 0.0);
     const int ng = (rows + RB - 1) / RB;
-    const int oob = (int)(ldr * 8);
+    // a row's buffer resource: its first element (row-major), or its first 4-column block row inside
+    // the 16-row strip (blocked layout, TLay); the thread's column pair at a fixed offset from it
+    const int oob = (int)(tl.blk ? ldr * 16 * 8 : ldr * 8);
+    const int jo = tl.blk ? ((jr >> 2) * 64 + (jr & 3)) * 8 : jr * 8;
+    auto row_base = [&](int i) {
+        return tl.blk ? Tr + (size_t)(i >> 4) * 16 * ldr + (size_t)(((i & 15) >> 2) * 16 + (i & 3) * 4)
+                      : Tr + (size_t)i * ldr;
+    };
     for (int g = gy; g < ng; g += G) {
         const int i0 = (rev ? ng - 1 - g : g) * RB;
         double2 x[RB];
@@ -2400,9 +2430,8 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, T
 #pragma unroll
         for (int k = 0; k < RB; ++k) {
             const int i = i0 + k < rows ? i0 + k : i0;
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                Tr + (size_t)i * ldr, 0, oob, 0x00020000);
-            x[k] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, i0 + k < rows ? jr * 8 : oob,
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row_base(i), 0, oob, 0x00020000);
+            x[k] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, i0 + k < rows ? jo : oob,
                                                                                       0, LAUX));
         }
 #pragma unroll
@@ -2450,10 +2479,9 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, T
                     }
                 }
             }
-            const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(Tr + (size_t)i * ldr, 0, oob, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row_base(i), 0, oob, 0x00020000);
             constexpr int SAUX = 16;
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, jr * 8, 0, SAUX);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rs, jo, 0, SAUX);
         }
     }
 }
@@ -2529,10 +2557,18 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
         // (wave-uniform) holding the strip's valid rows; rows past the end read 0 and drop their
         // stores
         auto strip_r0 = [&](int g) { return (rev ? nstrip - 1 - g : g) * 16; };
+        // (blocked layout, TLay: a strip's rows past the end exist -- rows are allocated in whole
+        // strips -- and hold values no row reads; row-major: they read 0 and their stores drop)
         auto strip_rsrc = [&](const double *base, int r0) {
-            const int nr = rows - r0 < 16 ? rows - r0 : 16;
+            const int nr = tl.blk ? 16 : (rows - r0 < 16 ? rows - r0 : 16);
             return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(base) + (size_t)r0 * ldr, 0,
                                                      (int)((size_t)nr * ldr * 8), 0x00020000);
+        };
+        // byte offset in the strip of the lane's column pair (c0 + 32 p + 2 jl, + 1) in row rg + 4 v
+        auto tile_off = [&](int p, int v) {
+            const int jr = cr + 32 * p + 2 * jl;
+            return tl.blk ? (int)((size_t)((jr >> 2) * 64 + v * 16 + rg * 4 + (jr & 3)) * 8)
+                          : (int)(((size_t)(rg + 4 * v) * ldr + jr) * 8);
         };
         auto load_tiles = [&](double2 (&cx)[2][4], int r0) {
             const __amdgpu_buffer_rsrc_t rsl = strip_rsrc(Tr, r0);
@@ -2541,9 +2577,8 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
                     const int j = c0 + 32 * p + 2 * jl;
-                    const int off = (int)(((size_t)(rg + 4 * v) * ldr + cr + 32 * p + 2 * jl) * 8);
                     cx[p][v] = __builtin_bit_cast(
-                        double2, __builtin_amdgcn_raw_buffer_load_b128(rsl, j < Ns ? off : OOB, 0, 2));
+                        double2, __builtin_amdgcn_raw_buffer_load_b128(rsl, j < Ns ? tile_off(p, v) : OOB, 0, 2));
                 }
         };
         for (int g = gy; g < nstrip; g += G) {
@@ -2572,7 +2607,7 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
             unsigned skip = 0u;  // bit v: row r0 + rg + 4v is a leaving row (not stored here)
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
-                const int j = c0 + 32 * p + 2 * jl, jr = cr + 32 * p + 2 * jl;
+                const int j = c0 + 32 * p + 2 * jl;
                 d4_t ax = {cx[p][0].x, cx[p][1].x, cx[p][2].x, cx[p][3].x};
                 d4_t ay = {cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
                 if (nkb == NKB) {
@@ -2603,7 +2638,7 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
                 const bool pair = j + 1 < Ns;
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
-                    const int off = (int)(((size_t)(rg + 4 * v) * ldr + jr) * 8);
+                    const int off = tile_off(p, v);
                     const bool keep = j < Ns && !((skip >> v) & 1u);
                     if (pair) {
                         const double2 y = make_double2(ax[v], ay[v]);
@@ -2663,7 +2698,7 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
         double x[NR], fl[NR];
 #pragma unroll
         for (int q1 = 0; q1 < NR; ++q1) {
-            x[q1] = (live[q1] && j < Ns) ? Tr[(size_t)r[q1] * ldr + cr + l] : 0.0;
+            x[q1] = (live[q1] && j < Ns) ? Tr[tl.blk ? TLay::b4(r[q1], cr + l, ldr) : (size_t)r[q1] * ldr + cr + l] : 0.0;
             fl[q1] = (live[q1] && l < cnt) ? F[sx_fidx(r[q1], l)] : 0.0;  // lane s: F[r][s]
         }
         // (32 slots of the column's pivot-row values at a time: registers)
@@ -2689,11 +2724,15 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
 #pragma unroll
         for (int q1 = 0; q1 < NR; ++q1) {
             if (!live[q1]) continue;
+            // (the row's strip through one resource: its element of column cr + l at b4 within it)
+            const int rr = r[q1];
             const __amdgpu_buffer_rsrc_t rsr =
-                __builtin_amdgcn_make_buffer_rsrc(Tw + (size_t)r[q1] * ldr, 0, (int)(ldr * 8), 0x00020000);
+                tl.blk ? __builtin_amdgcn_make_buffer_rsrc(Tw + (size_t)(rr >> 4) * 16 * ldr, 0, (int)(ldr * 16 * 8), 0x00020000)
+                       : __builtin_amdgcn_make_buffer_rsrc(Tw + (size_t)rr * ldr, 0, (int)(ldr * 8), 0x00020000);
+            const int eo = tl.blk ? (int)(TLay::b4(rr & 15, cr + l, ldr) * 8) : (cr + l) * 8;
             const unsigned long long xb = (unsigned long long)__double_as_longlong(x[q1]);
             const u32x2 w = {(unsigned)xb, (unsigned)(xb >> 32)};
-            __builtin_amdgcn_raw_buffer_store_b64(w, rsr, j < Ns ? (cr + l) * 8 : OOB, 0, 16);  // (write-through, as the strips)
+            __builtin_amdgcn_raw_buffer_store_b64(w, rsr, j < Ns ? eo : OOB, 0, 16);  // (write-through, as the strips)
         }
     }
 }
@@ -2851,18 +2890,16 @@ __global__ __launch_bounds__(256) void k_gemv_partials(const double *__restrict_
     if (j >= N) return;
     const int i1 = (k + 1) * SX_TILE < rows ? (k + 1) * SX_TILE : rows;
     double s = 0.0;
-    const double *col = T + tl.idx(0, j);  // column j: stride ldA in region A, ldB in region B
-    const size_t ld = j < tl.jB ? tl.ldA : tl.ldB;
     int i = k * SX_TILE;
     for (; i + 4 <= i1; i += 4) {
-        const double t0 = col[(size_t)i * ld], t1 = col[(size_t)(i + 1) * ld];
-        const double t2 = col[(size_t)(i + 2) * ld], t3 = col[(size_t)(i + 3) * ld];
+        const double t0 = T[tl.idx(i, j)], t1 = T[tl.idx(i + 1, j)];
+        const double t2 = T[tl.idx(i + 2, j)], t3 = T[tl.idx(i + 3, j)];
         s = fma(t0, coef[i], s);
         s = fma(t1, coef[i + 1], s);
         s = fma(t2, coef[i + 2], s);
         s = fma(t3, coef[i + 3], s);
     }
-    for (; i < i1; ++i) s = fma(col[(size_t)i * ld], coef[i], s);
+    for (; i < i1; ++i) s = fma(T[tl.idx(i, j)], coef[i], s);
     partials[(size_t)k * N + j] = s;
 }
 
@@ -2879,7 +2916,7 @@ __global__ void k_gemv_apply(double *d, Cols c, const double *__restrict__ parti
 // Tableau construction (fillTableu + checkColumns, twoPhaseMethod.cu:145-200, 86-111).
 // A_local is the shard's slice of the column-major A: A_local[j*rows + i] = A(row0+i, j).
 // 32x32 LDS transpose so both the read (along i) and the write (along j) are coalesced.
-__global__ __launch_bounds__(256) void k_fill_structural(double *T, int rows, size_t ld, int n,
+__global__ __launch_bounds__(256) void k_fill_structural(double *T, int rows, TLay tl, int n,
                                                          const double *__restrict__ A_local) {
     __shared__ double tile[32][33];
     const int i_base = blockIdx.x * 32, j_base = blockIdx.y * 32;
@@ -2890,7 +2927,7 @@ __global__ __launch_bounds__(256) void k_fill_structural(double *T, int rows, si
     __syncthreads();
     for (int ii = threadIdx.y; ii < 32; ii += 8) {
         const int i = i_base + ii, j = j_base + threadIdx.x;
-        if (i < rows && j < n) T[(size_t)i * ld + 1 + j] = tile[threadIdx.x][ii];
+        if (i < rows && j < n) T[tl.idx(i, 1 + j)] = tile[threadIdx.x][ii];
     }
 }
 
@@ -2930,9 +2967,25 @@ __global__ void k_phase2_costs(double *d, int n, int m, const double *c) {
     if (t < m) d[1 + n + t] = 0.0;
 }
 
-__global__ void k_gather_rhs(const double *T, int rows, size_t ld, double *out) {
+// rows [i0, i0 + nr) of the tableau, stored columns [0, Ns), to / from a row-major buffer (the
+// host's view of a blocked tableau: download, upload, and the synthetic sweep bench's column 0)
+__global__ void k_rows_out(const double *__restrict__ T, TLay tl, int i0, int nr, int Ns, double *__restrict__ out) {
+    const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= (long long)nr * Ns) return;
+    const int r = (int)(k / Ns), j = (int)(k % Ns);
+    out[k] = T[tl.idx(i0 + r, j)];
+}
+__global__ void k_rows_in(double *__restrict__ T, TLay tl, int i0, int nr, int Ns, int j0, const double *__restrict__ in,
+                          size_t ld_in) {
+    const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= (long long)nr * Ns) return;
+    const int r = (int)(k / Ns), j = (int)(k % Ns);
+    T[tl.idx(i0 + r, j0 + j)] = in[(size_t)r * ld_in + j];
+}
+
+__global__ void k_gather_rhs(const double *T, int rows, TLay tl, double *out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < rows) out[i] = T[(size_t)i * ld];
+    if (i < rows) out[i] = T[tl.idx(i, 0)];
 }
 
 }  // namespace
@@ -3251,7 +3304,7 @@ void sx_launch_build_rows(double *T, int rows, int row0, TLay tl, int n, int m, 
     dim3 tb(32, 8);
     dim3 tg((rows + 31) / 32, (n + 31) / 32);
     // A_local == nullptr: the structural columns are already in T (device generator)
-    if (n > 0 && A_local != nullptr) k_fill_structural<<<tg, tb, 0, s>>>(T, rows, tl.ldA, n, A_local);  // (columns 1..n: region A)
+    if (n > 0 && A_local != nullptr) k_fill_structural<<<tg, tb, 0, s>>>(T, rows, tl, n, A_local);
     int gx = (Ns + 255) / 256;
     if (gx > 64) gx = 64;
     dim3 rg(gx, rows);
@@ -3269,9 +3322,21 @@ void sx_launch_phase2_costs(double *d, int n, int m, const double *c, hipStream_
     k_phase2_costs<<<(t + 255) / 256, 256, 0, s>>>(d, n, m, c);
 }
 
-void sx_launch_gather_rhs(const double *T, int rows, size_t ld, double *out, hipStream_t s) {
+void sx_launch_rows_out(const double *T, TLay tl, int i0, int nr, int Ns, double *out, hipStream_t s) {
+    const long long n = (long long)nr * Ns;
+    if (n <= 0) return;
+    k_rows_out<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(T, tl, i0, nr, Ns, out);
+}
+void sx_launch_rows_in(double *T, TLay tl, int i0, int nr, int Ns, int j0, const double *in, size_t ld_in,
+                       hipStream_t s) {
+    const long long n = (long long)nr * Ns;
+    if (n <= 0) return;
+    k_rows_in<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(T, tl, i0, nr, Ns, j0, in, ld_in);
+}
+
+void sx_launch_gather_rhs(const double *T, int rows, TLay tl, double *out, hipStream_t s) {
     if (rows <= 0) return;
-    k_gather_rhs<<<(rows + 255) / 256, 256, 0, s>>>(T, rows, ld, out);
+    k_gather_rhs<<<(rows + 255) / 256, 256, 0, s>>>(T, rows, tl, out);
 }
 
 void sx_launch_argmin_vector(const double *v, long long L, TilePart *parts, int *out_idx, double *out_v,

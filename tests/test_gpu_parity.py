@@ -678,3 +678,61 @@ def test_slack_compaction_generated_session_width(gpu):
     assert t.update_launches == (96 + K - 1) // K and t.swept_pivots == 96
     assert t.update_bytes <= 16.0 * m * (1 + n + active) + 1e-6
     assert t.update_bytes < 16.0 * m * t.stored_width
+
+
+# ------------------------------------------------------------------ round 4
+@pytest.mark.parametrize("batch", [32, 64])
+@pytest.mark.parametrize("W", [2, 8])
+def test_p2p_fused_fine_pivot_rows(gpu, batch, W):
+    """the pending pivot rows U in fine-grained memory -- what the engine allocates when the shards
+    span devices (peer ranks write U over xGMI) -- forced on one GPU: the multi-rank
+    batch and its sweeps stay bit-exact"""
+    lib = sx.load()
+    T, d, base = _phase1_state(300, 1100, 11)
+    try:
+        lib.simplex_set_fine_pivot_rows(1)
+        Tg, dg, bg, st, done = _pivots_with({"batch": batch, "W": W, "p2p": 1}, T, d, base, 150)
+    finally:
+        lib.simplex_set_fine_pivot_rows(-1)
+    st_o, done_o = oracle.solve(T, d, base, max_pivots=150)
+    assert done == done_o
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+def _subnormal_state(seed):
+    """a phase-1 state whose structural block holds IEEE edge values the pivot decisions do not
+    depend on: subnormals, entries of 1e-300 scale (their products with the row factors underflow
+    to subnormals or zero) and signed zeros, ~12 % of the structural entries"""
+    n, m = 300, 1100
+    T, d, base = _phase1_state(n, m, seed)
+    rng = np.random.default_rng(seed)
+    blk = T[:, 1:1 + n]
+    pick = rng.random(blk.shape)
+    sub = rng.integers(1, 1 << 52, size=blk.shape, dtype=np.uint64).view(np.float64)
+    tiny = rng.uniform(-1.0, 1.0, size=blk.shape) * 1e-300
+    blk[pick < 0.04] = sub[pick < 0.04] * np.where(rng.random(blk.shape) < 0.5, -1.0, 1.0)[pick < 0.04]
+    blk[(pick >= 0.04) & (pick < 0.08)] = tiny[(pick >= 0.04) & (pick < 0.08)]
+    blk[(pick >= 0.08) & (pick < 0.10)] = -0.0
+    blk[(pick >= 0.10) & (pick < 0.12)] = 0.0
+    # ~5 % of the rows scaled into the subnormal range (RHS included): their entering entries stay
+    # below the 1e-9 eligibility bound, so they never leave, and their factors and updates stay
+    # subnormal pivot after pivot
+    rows = rng.random(m) < 0.05
+    T[rows, :1 + n] *= 2.0 ** -1040
+    return T, d, base
+
+
+@pytest.mark.parametrize("batch,mfma", [(64, 1), (32, 1), (17, 1), (32, 0)])
+def test_subnormal_tableau_bit_exact(gpu, batch, mfma):
+    """the sweep on a tableau holding subnormal, underflowing and signed-zero entries: the matrix
+    cores (v_mfma_f64_16x16x4f64: 64- and 32-slot sweeps, a partial batch) and the vector units
+    give the oracle's per-element fma chain bit for bit -- the edge semantics the matrix-core sweep
+    depends on (profiles/r04_mfma_edge_probe.txt), here through the engine"""
+    T, d, base = _subnormal_state(11)
+    sub0 = np.count_nonzero((T != 0) & (np.abs(T) < 2.2250738585072014e-308))
+    assert sub0 > 1000
+    Tg, dg, bg, st, done = _pivots_with({"batch": batch, "mfma": mfma}, T, d, base, 130)
+    st_o, done_o = oracle.solve(T, d, base, max_pivots=130)
+    assert done == done_o
+    assert np.count_nonzero((T != 0) & (np.abs(T) < 2.2250738585072014e-308)) > 1000  # (subnormal results too)
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
