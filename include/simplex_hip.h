@@ -83,6 +83,11 @@ void simplex_set_fused(int mode);
 void simplex_set_p2p(int mode);
 /* 1 when the peer-memory fused path passed simplex_dist_init's self-check on every rank */
 int simplex_p2p_ready(void);
+/* how the shards of this process (RCCL ranks, or the SIMPLEX_GPUS device list) passed their
+ * start-up self-check against a one-shard solve of the same instance: 2 peer-memory fused batches,
+ * 1 the per-pivot exchange, 0 neither (every solve then runs on one device: RCCL ranks each solve
+ * alone, a device list on its first device), -1 not checked (yet) or one shard */
+int simplex_multi_gpu_mode(void);
 /* wall time (s) of the last twoPhaseMethod call's two pivot loops (solve calls): out[0] phase 1,
  * out[1] phase 2 -- the reference's TIMER CSV reports the two phases separately */
 void simplex_last_phase_seconds(double *out);

@@ -102,6 +102,7 @@ SIGNATURES = {
     "simplex_last_objective_row": (ctypes.c_longlong, [ctypes.POINTER(ctypes.c_double), ctypes.c_longlong]),
     "simplex_set_p2p": (None, [ctypes.c_int]),
     "simplex_p2p_ready": (ctypes.c_int, []),
+    "simplex_multi_gpu_mode": (ctypes.c_int, []),
     "simplex_set_update_waves": (None, [ctypes.c_double]),
     "simplex_set_regions": (None, [ctypes.c_int]),
     "simplex_set_mr_single_launch": (None, [ctypes.c_int]),

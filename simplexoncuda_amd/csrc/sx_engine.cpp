@@ -70,7 +70,9 @@ struct Config {
     int fused = -1;          // whole batches in one resident launch: -1 auto (one shard), 0 off
     int p2p = -1;            // several shards: fused batches exchanging over peer memory: -1 auto, 0 off, 1 force
     bool p2p_ready = false;  // RCCL ranks: the peer-memory path passed the start-up self-check
-    std::map<std::vector<int>, bool> p2p_checked;  // one process, several GPUs: self-check result per device list
+    std::map<std::vector<int>, int> gpus_checked;  // one process, several GPUs: self-check result per device list
+    bool single_shard = false;  // every engine one shard on its own device (self-check reference; the
+                                // fallback when the shards' exchange failed the self-check)
     int debug = -1;          // -1: from SIMPLEX_DEBUG; 1: print the tableau after every step
     bool benchmark = false;
     bool no_timer = false;         // the multi-GPU self-check: never write TIMER CSVs
@@ -222,6 +224,7 @@ std::vector<int> shard_devices() {
 }
 
 bool gpus_selftest(const std::vector<int> &devs);  // (below two_phase)
+int gpus_check(const std::vector<int> &devs);
 
 // the engine's own tableaux in 4x4 blocks (TLay::blk) unless SIMPLEX_BLOCKED=0 or
 // simplex_set_blocked(0)
@@ -338,15 +341,21 @@ class Engine {
         ld = round_up((size_t)Ns1, 16);
         batch_id = (g_cfg.first_batch_id >= 1 && g_cfg.first_batch_id < SX_BATCH_IDS) ? g_cfg.first_batch_id : 1;
         std::vector<int> devs;  // one process, several GPUs: the device of every shard
-        if (g_cfg.ipc_world > 1) {
+        if (g_cfg.single_shard) {
+            // one shard on this device
+        } else if (g_cfg.ipc_world > 1) {
             rccl = ipc = true;
             W = g_cfg.ipc_world;
         } else if (g_cfg.dist && g_cfg.comm) {
             rccl = true;
             W = g_cfg.world;
         } else if ((devs = shard_devices()).size() > 1) {
-            W = (int)devs.size();
-            gpus_mode = true;
+            if (gpus_check(devs) != 0) {
+                W = (int)devs.size();
+                gpus_mode = true;
+            } else {
+                g_cfg.device = devs[0];  // (the list failed its self-check: its first device alone)
+            }
         } else if (g_cfg.virtual_ranks > 1) {
             W = g_cfg.virtual_ranks;
         }
@@ -1704,17 +1713,19 @@ int two_phase(problem_t *P, double *solution, double *opt, int *base_out, long l
 }
 
 // A small instance solved with the multi-rank fused batch over peer memory -- in one-stage (32) and
-// two-stage (64-pivot) batches -- and with the per-pivot exchange: true when the fused path ran (no
-// hand-off timed out) and every answer is bit-identical.  The instance gives each of the W shards
-// 512 rows (m = 512 W, rows per shard round_up(m / W, 512) = 512), so every rank sweeps, owns
-// leaving rows and writes and reads peer pivot rows during the check (W = 2: m = 1100 -- 1318 + 23
-// pivots, phases ending mid-batch -- as before).
-bool selftest_solves(int W) {
+// two-stage (64-pivot) batches -- with the per-pivot exchange, and on one shard of this device
+// alone (the reference answer).  The instance gives each of the W shards 512 rows (m = 512 W, rows
+// per shard round_up(m / W, 512) = 512), so every rank sweeps, owns leaving rows and writes and
+// reads peer pivot rows during the check (W = 2: m = 1100 -- 1318 + 23 pivots, phases ending
+// mid-batch -- as before).  Returns 2 when both multi-shard paths give the one-shard answer bit for
+// bit (and the fused path ran without a hand-off timing out), 1 when only the per-pivot exchange
+// does, 0 when the per-pivot exchange does not either (the shards must not be used: one device).
+int selftest_solves(int W) {
     const int sm = W > 2 ? 512 * W : 1100;
     problem_t *P = generateRandomProblem(300, sm, 300 * 100 + sm, 1, 100);
     const int n = P->vars, m = P->constraints;
     const int save = g_cfg.p2p, save_batch = g_cfg.batch;
-    const bool save_nt = g_cfg.no_timer;
+    const bool save_nt = g_cfg.no_timer, save_single = g_cfg.single_shard;
     g_cfg.no_timer = true;  // (timing would switch the solves to the per-pivot path; no CSVs either)
     struct Answer {
         std::vector<double> x;
@@ -1740,28 +1751,37 @@ bool selftest_solves(int W) {
     const long long fb0 = g_cfg.fused_batches, hr0 = g_cfg.hang_recoveries;
     const Answer a32 = solve(1, SX_HMAX), a64 = solve(1, SX_KMAX);
     const bool went_fused = g_cfg.fused_batches > fb0 && g_cfg.hang_recoveries == hr0;
-    const Answer ref = solve(0, 0);
+    const Answer xch = solve(0, 0);
+    g_cfg.single_shard = true;  // the reference: one shard of this device
+    const Answer one = solve(-1, 0);
+    g_cfg.single_shard = save_single;
     g_cfg.p2p = save;
     g_cfg.batch = save_batch;
     g_cfg.no_timer = save_nt;
-    const bool ok = went_fused && same(a32, ref) && same(a64, ref);
+    const int code = !same(xch, one) ? 0 : (went_fused && same(a32, one) && same(a64, one)) ? 2 : 1;
     freeProblem(P);
     free(P);
-    return ok;
+    return code;
 }
 
-// One process, several GPUs (SIMPLEX_GPUS): the peer-memory batch is used on a device list only
-// when selftest_solves passes on it (once per list and process).
-bool gpus_selftest(const std::vector<int> &devs) {
-    auto it = g_cfg.p2p_checked.find(devs);
-    if (it != g_cfg.p2p_checked.end()) return it->second;
-    g_cfg.p2p_checked[devs] = false;  // (while the check runs)
-    const bool ok = selftest_solves((int)devs.size());
-    g_cfg.p2p_checked[devs] = ok;
-    if (!ok) fprintf(stderr, "simplex: peer-memory fused batches disagree with the per-pivot exchange on these GPUs; "
-                             "using the per-pivot exchange\n");
-    return ok;
+// One process, several GPUs (SIMPLEX_GPUS): once per device list and process, selftest_solves
+// decides how the list is used: 2 peer-memory fused batches, 1 the per-pivot
+// exchange, 0 not at all (every solve on the list's first device).  -1 while the check runs.
+int gpus_check(const std::vector<int> &devs) {
+    auto it = g_cfg.gpus_checked.find(devs);
+    if (it != g_cfg.gpus_checked.end()) return it->second;
+    g_cfg.gpus_checked[devs] = -1;  // (the check's own engines run the list)
+    const int code = selftest_solves((int)devs.size());
+    g_cfg.gpus_checked[devs] = code;
+    if (code == 1)
+        fprintf(stderr, "simplex: peer-memory fused batches disagree with the one-shard answer on these GPUs; "
+                        "using the per-pivot exchange\n");
+    if (code == 0)
+        fprintf(stderr, "simplex: the GPUs of this device list disagree with the one-shard answer; solving on "
+                        "device %d alone\n", devs[0]);
+    return code;
 }
+bool gpus_selftest(const std::vector<int> &devs) { return gpus_check(devs) == 2; }
 
 }  // namespace
 
@@ -1796,10 +1816,19 @@ void simplex_set_p2p(int mode) { g_cfg.p2p = mode < 0 ? -1 : (mode ? 1 : 0); }
 int simplex_p2p_ready(void) {
     const std::vector<int> v = g_cfg.dist ? std::vector<int>() : shard_devices();
     if (v.size() > 1) {  // one process, several GPUs: the self-check of this device list
-        auto it = g_cfg.p2p_checked.find(v);
-        return it != g_cfg.p2p_checked.end() && it->second ? 1 : 0;
+        auto it = g_cfg.gpus_checked.find(v);
+        return it != g_cfg.gpus_checked.end() && it->second == 2 ? 1 : 0;
     }
     return g_cfg.p2p_ready ? 1 : 0;
+}
+int simplex_multi_gpu_mode(void) {
+    const std::vector<int> v = g_cfg.dist ? std::vector<int>() : shard_devices();
+    if (v.size() > 1) {
+        auto it = g_cfg.gpus_checked.find(v);
+        return it == g_cfg.gpus_checked.end() ? -1 : it->second;
+    }
+    if (!g_cfg.dist) return -1;
+    return g_cfg.single_shard ? 0 : g_cfg.p2p_ready ? 2 : 1;
 }
 void simplex_last_phase_seconds(double *out) {
     out[0] = g_phase_seconds[0];
@@ -1839,17 +1868,20 @@ int simplex_dist_get_unique_id(unsigned char *out) {
 // rank gets bit-identical answers from both.
 static void p2p_selftest() {
     g_cfg.p2p_ready = false;
-    if (g_cfg.world > SX_MAXW || g_cfg.p2p == 0) return;
-    int ok = selftest_solves(g_cfg.world) ? 1 : 0;
+    g_cfg.single_shard = false;
+    int code = selftest_solves(g_cfg.world);
     int *dv = nullptr;
     SX_HIP(hipMalloc(reinterpret_cast<void **>(&dv), sizeof(int)));
-    SX_HIP(hipMemcpy(dv, &ok, sizeof(int), hipMemcpyHostToDevice));
+    SX_HIP(hipMemcpy(dv, &code, sizeof(int), hipMemcpyHostToDevice));
     SX_NCCL(ncclAllReduce(dv, dv, 1, ncclInt, ncclMin, g_cfg.comm, nullptr));
-    SX_HIP(hipMemcpy(&ok, dv, sizeof(int), hipMemcpyDeviceToHost));
+    SX_HIP(hipMemcpy(&code, dv, sizeof(int), hipMemcpyDeviceToHost));
     (void)hipFree(dv);
-    g_cfg.p2p_ready = ok != 0;
-    if (!ok && g_cfg.rank == 0)
-        fprintf(stderr, "simplex: peer-memory fused batches disagree with the RCCL exchange; using RCCL\n");
+    g_cfg.p2p_ready = code == 2 && g_cfg.p2p != 0 && g_cfg.world <= SX_MAXW;
+    g_cfg.single_shard = code == 0;
+    if (code == 1 && g_cfg.rank == 0)
+        fprintf(stderr, "simplex: peer-memory fused batches disagree with the one-shard answer; using RCCL\n");
+    if (code == 0 && g_cfg.rank == 0)
+        fprintf(stderr, "simplex: the RCCL exchange disagrees with the one-shard answer; every rank solves alone\n");
 }
 
 int simplex_dist_init(int rank, int world, const unsigned char *unique_id, int device) {
