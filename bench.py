@@ -329,9 +329,9 @@ def main():
         # (uniform [1,100], seed 823296) with K random pending pivots, K = the pivot loop's batch
         # (three runs of 10 untimed + 50 timed sweeps each; the median run is reported -- the
         # first run on a box is often 5-10 % slower); the one-stage variants alongside
-        def sweep_bench(pivots, mfma):
+        def sweep_bench(pivots, mfma, rows=4096):
             sx.set_sweep_mfma(mfma)
-            runs = [sx.bench_sweep(4096, 8192, 823296, 1, 100, pivots, warmup=10, iters=50) for _ in range(3)]
+            runs = [sx.bench_sweep(rows, 8192, 823296, 1, 100, pivots, warmup=10, iters=50) for _ in range(3)]
             sx.set_sweep_mfma(-1)
             us, nbytes = sorted(runs)[1]
             gbs = nbytes / (us * 1e-6) / 1e9
@@ -346,10 +346,24 @@ def main():
         # peak: it is co-bound by the fp64 matrix rate)
         K3 = r["K"] if args.config == "config3" else (r2["K"] if args.secondary == "config3" else 32)
         variants = [sweep_bench(32, 1), sweep_bench(64, 1), sweep_bench(32, 0)]
+        # the same kernel on a matrix 8x the Infinity Cache (2.1 GB): every byte from HBM
+        big = sweep_bench(32, 1, rows=16384)
+        big["workload"] = "16384x8192 (2.1 GB, 8x the 256 MiB Infinity Cache), 32 pivots per sweep"
+        pmc_ub = os.path.join(args.pmc_dir, "pmc_update_bench.json") if args.pmc_dir else None
+        ub_traffic = None
+        if pmc_ub and os.path.exists(pmc_ub):
+            with open(pmc_ub) as f:
+                ub_traffic = json.load(f)
         out["update_bench"] = dict(variants[0], workload=(
             "config3': the 32-pivot sweep kernel on a synthetic 4096x8192 fp64 matrix (uniform [1,100], seed "
             "823296) with 32 random pending pivots, median of 3 runs of 50 timed sweeps (HIP events)"),
-            note="the matrix (268 MB) is about the size of the 256 MB Infinity Cache, so sweeps partly hit it",
+            note="the matrix (268 MB) is about the size of the 256 MB Infinity Cache, so sweeps partly hit it; "
+                 "out_of_cache is the same kernel on a 2.1 GB matrix (HBM rate)",
+            traffic=(ub_traffic or {}).get("4096x8192"),
+            traffic_source=("committed profile profiles/pmc_update_bench.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                            "passes of tools/update_bench_probe.py, (2*FETCH_SIZE+WRITE_SIZE)*1024 per launch; FETCH_SIZE "
+                            "counts Infinity-Cache hits too) -- not measured in this run") if ub_traffic else None,
+            out_of_cache=dict(big, traffic=(ub_traffic or {}).get("16384x8192")),
             loop_batch_on_4096_rows=K3, variants=variants)
     if args.full_solves:
         # the whole drop-in call, as main.cu -t times it: build + both phases + solution (problem

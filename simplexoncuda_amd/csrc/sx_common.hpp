@@ -96,7 +96,9 @@ struct BatchChan {
     alignas(128) unsigned inject_q;  // test hook: 1 + the slot at which ratio block 0 (of rank 0)
                                      // leaves with the batch aborted (0: off); the last block clears it
     alignas(128) unsigned backoff;   // k_batch: adaptive poll back-off on (1) / off (0)
+    alignas(128) unsigned copies;    // k_batch: copies of every hand-off record, 1..SX_REC_COPIES
 };
+#define SX_REC_COPIES 8
 
 // Multi-rank fused batch (k_batch_mr): every rank's buffers as seen from this rank (peer
 // memory over xGMI, or the other virtual shards on one GPU).

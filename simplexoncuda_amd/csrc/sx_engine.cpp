@@ -97,12 +97,13 @@ Config g_cfg;
 std::mutex g_mu;
 
 // The granule records of the RCCL ranks' peer-memory batch are polled inside a launch while
-// other GPUs write them, so they are uncached.  Uncached and cached allocations must not
-// trade pages within a process: after virtual-shard runs had allocated and freed uncached
-// records, later single-GPU batches diverged from the oracle (tests/test_gpu_parity.py run
-// in order).  So the uncached records are allocated once per process (after an
-// L2 write-back, so no dirty line of the pages' earlier cached use lands on them later) and
-// never freed; everything else, virtual shards included, uses plain device memory.
+// other GPUs write them, so they are uncached.  In round 2, single-GPU batches that ran after
+// virtual-shard runs had allocated and freed uncached records diverged from the oracle; the
+// round-4 reuse probe (profiles/r04_uncached_bisect_and_reuse.txt) found no stale word on a
+// freed-and-reused page either way, so that divergence is unexplained.  As a
+// precaution the uncached records are still allocated once per process, after an L2
+// write-back, and never freed; everything else, virtual shards included, uses plain device
+// memory.
 // A pool of such sets, one per (device, concurrent engine): a second engine alive at the same
 // time (or a second shard on the device) takes another set instead of falling back to cached
 // memory.
@@ -741,6 +742,10 @@ class Engine {
             const char *e = getenv("SIMPLEX_BACKOFF");
             const unsigned bo = (e && atoi(e) == 0) ? 0u : 1u;
             SX_HIP(hipMemcpyAsync(&x.chan->backoff, &bo, sizeof(unsigned), hipMemcpyHostToDevice, x.s));
+            // copies of every hand-off record (SIMPLEX_REC_COPIES, 1..SX_REC_COPIES)
+            const char *rc = getenv("SIMPLEX_REC_COPIES");
+            const unsigned cp = rc ? (unsigned)std::min(std::max(atoi(rc), 1), SX_REC_COPIES) : 1u;
+            SX_HIP(hipMemcpyAsync(&x.chan->copies, &cp, sizeof(unsigned), hipMemcpyHostToDevice, x.s));
             SX_HIP(hipStreamSynchronize(x.s));
         }
         SX_HIP(hipMemsetAsync(x.ga, 0, sx_batch_granules_a() * sizeof(unsigned long long), x.s));

@@ -1311,6 +1311,12 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
     bool aborted = false;
     const unsigned inj = ch->inject_q;  // (test hook, normally 0)
     const bool backoff = ch->backoff != 0u;
+    // copies of every record (SIMPLEX_REC_COPIES): a producer writes each of its records into
+    // all of them, a block polls copy blockIdx % copies -- one per XCD at 8, since workgroups
+    // are dispatched to the XCDs round-robin
+    const int rcn = ch->copies < 1u ? 1 : ch->copies > SX_REC_COPIES ? SX_REC_COPIES : (int)ch->copies;
+    u64 *const gam = ga + (size_t)(blockIdx.x % rcn) * sx_ga_size();
+    u64 *const gbm = gb + (size_t)(blockIdx.x % rcn) * sx_gb_size();
     if (status0 == SX_NOT_ENDED) {
         // ratio block: its row; objective block: its logical column d[1 + ia]
         const int li = blockIdx.x * SX_TILE + t;
@@ -1437,7 +1443,9 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                             const u64 bits64 = (u64)__double_as_longlong(val);
                             data = (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64;
                         }
-                        put_g(ga + (size_t)blockIdx.x * SX_GA_STRIDE + k, data, k < kRD ? (tag | pl) : tag);
+                        for (int c = 0; c < rcn; ++c)
+                            put_g(ga + c * sx_ga_size() + (size_t)blockIdx.x * SX_GA_STRIDE + k, data,
+                                  k < kRD ? (tag | pl) : tag);
                     }
                 }
                 if (blockIdx.x == 0) SX_STAMP(1);
@@ -1450,14 +1458,14 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 // the objective blocks run, reduction.cu:116-140, and takes p and the RHS from the
                 // winner's record): the objective side answers much later, so this is off the chain
                 if (t < 64) {
-                    int ok = poll_wave(ga, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
+                    int ok = poll_wave(gam, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
                     double tv = DBL_MAX;
                     int ti = -1, any = 0;
                     if (ok) wave_pass2(s_g, s_pay, NA, s_v, s_i, tv, ti, any);
                     ti = __builtin_amdgcn_readfirstlane(ti);
                     if (ok && ti >= 0) {
                         const int wt = ti / SX_TILE;
-                        ok = poll_wave(ga + (size_t)wt * SX_GA_STRIDE + kRA, 4, IdOff(), tag, s_g + 2048 - 64,
+                        ok = poll_wave(gam + (size_t)wt * SX_GA_STRIDE + kRA, 4, IdOff(), tag, s_g + 2048 - 64,
                                        &ch->abort_w, 20000000ull, (unsigned *)nullptr);
                     }
                     if (t == 0) {
@@ -1519,7 +1527,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     unsigned short *po = s_payo;
                     const u64 ta = __builtin_amdgcn_s_memrealtime();
                     const int ok = poll_wave_f<Rec4All, false, SX_OBJ_PER_LANE>(
-                        gb, SX_GB4 * NB, Rec4All(), tag, s_g, &ch->abort_w, 20000000ull,
+                        gbm, SX_GB4 * NB, Rec4All(), tag, s_g, &ch->abort_w, 20000000ull,
                         [po](int k, unsigned pl) {
                             if ((k & 3) < 3) po[(k & 3) * SX_OBJ_TILES + (k >> 2)] = (unsigned short)pl;
                         },
@@ -1576,7 +1584,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 // ---- selection: pass 2 over the ratio tiles (wave 0 polls and runs the tree)
                 if (t < 64) {
                     const u64 ta = __builtin_amdgcn_s_memrealtime();
-                    const int ok = poll_wave(ga, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, 20000000ull, s_pay, pre_a);
+                    const int ok = poll_wave(gam, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, 20000000ull, s_pay, pre_a);
                     if (backoff) pre_a = next_backoff(__builtin_amdgcn_s_memrealtime() - ta);
                     double tv = DBL_MAX;
                     int ti = -1, any = 0;
@@ -1606,7 +1614,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     u64 fr1 = 0ull;
                     if (hb && t < SX_HMAX)
                         fr1 = ld_sc1(reinterpret_cast<const u64 *>(F + sx_fidx(r >= 0 ? r : 0, t)));
-                    const int ok = poll_wave(ga + (size_t)wt * SX_GA_STRIDE + kRD, (kRF - kRD) + 2 * qq,
+                    const int ok = poll_wave(gam + (size_t)wt * SX_GA_STRIDE + kRD, (kRF - kRD) + 2 * qq,
                                              [](int k) { return k; }, tag, s_g, &ch->abort_w, 20000000ull,
                                              (unsigned *)nullptr);
                     if (hb && t < SX_HMAX) s_fr1[t] = __longlong_as_double((long long)fr1);
@@ -1686,15 +1694,16 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     // the record: the winner's d value (payload: its index in the tile) and its pivot-row
                     // value of this pivot U[q][w] (the ratio side's newest pending entry of the entering
                     // column if w enters), the winner's stored column in the payloads of granules 1, 2
-                    if (t < SX_GB4) {
+                    if (t < SX_GB4 * rcn) {
+                        const int k = t & (SX_GB4 - 1), c = t / SX_GB4;
                         const int mw = reinterpret_cast<const int *>(s_a)[win];
-                        const double val = t < 2 ? wv : s_hist[qq * SX_TILE + win];
+                        const double val = k < 2 ? wv : s_hist[qq * SX_TILE + win];
                         const u64 bits64 = (u64)__double_as_longlong(val);
-                        const unsigned data = (t & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64;
-                        const unsigned pl = t == 0 ? (wi >= 0 ? (unsigned)win : SX_NOIDX)
-                                          : t == 1 ? ((unsigned)mw & SX_PAYMASK)
-                                          : t == 2 ? (((unsigned)mw >> SX_PAYBITS) & SX_PAYMASK) : 0u;
-                        put_g(gb + (size_t)tb * SX_GBS + t, data, tag | pl);
+                        const unsigned data = (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64;
+                        const unsigned pl = k == 0 ? (wi >= 0 ? (unsigned)win : SX_NOIDX)
+                                          : k == 1 ? ((unsigned)mw & SX_PAYMASK)
+                                          : k == 2 ? (((unsigned)mw >> SX_PAYBITS) & SX_PAYMASK) : 0u;
+                        put_g(gb + c * sx_gb_size() + (size_t)tb * SX_GBS + k, data, tag | pl);
                     }
                 }
                 // the pivot row into U[q] (the sweep's input, and the ratio side's pending entries of
@@ -1714,7 +1723,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
         if (!isA && !aborted && (status == SX_NOT_ENDED || status == SX_PIVOT_CAP) && cnt > 0) {
             const unsigned tag = make_tag(B, cnt - 1);
             if (t < 64) {
-                const int ok = poll_wave(gb, 2 * NB, Rec4Val(), tag, s_g, &ch->abort_w, 20000000ull, s_pay);
+                const int ok = poll_wave(gbm, 2 * NB, Rec4Val(), tag, s_g, &ch->abort_w, 20000000ull, s_pay);
                 double ev = DBL_MAX;
                 int ei = -1, any = 0;
                 if (ok) wave_pass2(s_g, s_pay, NB, s_v, s_i, ev, ei, any);
@@ -3153,8 +3162,8 @@ void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, 
 // LDS history of a fused batch of k pivots: one stage
 static size_t batch_lds(int k) { return (size_t)(k < SX_HMAX ? k : SX_HMAX) * SX_TILE * sizeof(double); }
 
-size_t sx_batch_granules_a() { return sx_ga_size(); }
-size_t sx_batch_granules_b() { return sx_gb_size(); }
+size_t sx_batch_granules_a() { return SX_REC_COPIES * sx_ga_size(); }
+size_t sx_batch_granules_b() { return SX_REC_COPIES * sx_gb_size(); }
 
 bool sx_batch_fits(int rows, Cols c, int k) {
     if (k < 1 || k > SX_KMAX || rows <= 0) return false;

@@ -89,3 +89,32 @@ def test_config5_degenerate_variant_pivots_match_oracle(gpu, W, mode, p2p):
 def test_simplex_gpus_mode_on_one_device(gpu, name, W):
     """SIMPLEX_GPUS mapped onto one GPU: the multi-GPU splits of configs 4 and 5 bit-exact"""
     run(name, gpus=[0] * W)
+
+
+with open(os.path.join(GOLDEN, "variant_solves.json")) as _f:
+    VARIANT = json.load(_f)
+
+
+@pytest.mark.parametrize("W,p2p", [(1, -1), (8, 1)])
+def test_config5_degenerate_variant_trajectory(gpu, W, p2p):
+    """config 5's [-100, 100] variant (SURVEY.md §8d's "degenerate" case, main.cu:7-8): its phase 1
+    does not end within 2,000,000 pivots on MI355X (the reference has no anti-cycling and no
+    iteration cap, solver.cu:139-140; the phase-1 objective d[0] still rises slowly, -1.57e6 at 20k
+    pivots to -1.48e6 at 2M, so it is not a cycle).  The recorded GPU trajectory (d[0] bits after
+    every 20,000 pivots, tests/golden/variant_solves.json) is reproduced up to 100,000 pivots on one
+    shard and on 8 peer-memory virtual shards -- a regression pin: the oracle pins only the first
+    48 pivots (test_config5_degenerate_variant_pivots_match_oracle)"""
+    v = VARIANT
+    sx.set_virtual_ranks(W)
+    sx.set_p2p(p2p)
+    try:
+        sess = sx.Session(generated=(v["n"], v["m"], v["seed"], v["lo"], v["hi"]))
+        for rec in v["phase1_trace"][:5]:
+            tim = sess.pivots(rec["pivots"] - sess.total_pivots())
+            assert tim.status == sx.NOT_ENDED
+            assert sess.total_pivots() == rec["pivots"]
+            assert float(sess.objective()).hex() == rec["d0_hex"], rec
+        sess.close()
+    finally:
+        sx.set_virtual_ranks(1)
+        sx.set_p2p(-1)

@@ -27,14 +27,16 @@ pytestmark = pytest.mark.gpu
 
 
 def _load(name):
+    # a missing fixture fails the collection (it must not parametrize zero tests and pass)
     path = os.path.join(GOLDEN, name)
     if not os.path.exists(path):
-        return {}
+        raise FileNotFoundError(f"golden fixture missing: {path}")
     with open(path) as f:
         return json.load(f)
 
 
 PUBLISHED = [r for r in _load("published_pivots.json") if r["gpu"] == "rtx2070super"]
+assert len(PUBLISHED) == 36, f"published_pivots.json: {len(PUBLISHED)} RTX 2070 Super instances, expected 36"
 ORACLE = _load("oracle_solves.json")
 HIGHS = _load("highs_objectives.json")
 
