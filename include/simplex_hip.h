@@ -114,6 +114,9 @@ void simplex_set_fine_pivot_rows(int mode);
  * SIMPLEX_BLOCKED=0), 1 blocks of 4 rows x 4 columns in 16-row strips, 0 plain row-major (DESIGN.md §2;
  * callers' tableaux, tabular.h, are always row-major) */
 void simplex_set_blocked(int mode);
+/* The matrix-core sweep with each strip's tableau tiles and factors staged through LDS by LDS-DMA
+   (1; SIMPLEX_SWEEP_LDS=1) or loaded to registers (0, default).  Same results bit for bit. */
+void simplex_set_sweep_lds(int on);
 
 /* ---- fault handling and test hooks ---- */
 /* a fused batch whose in-kernel hand-off wait times out (SIMPLEX_HANG, never expected) is

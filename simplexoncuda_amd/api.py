@@ -403,6 +403,12 @@ def set_sweep_mfma(mode):
     _lib.load().simplex_set_sweep_mfma(int(mode))
 
 
+def set_sweep_lds(on):
+    """The matrix-core sweep with its strips staged through LDS by LDS-DMA (1) or loaded to
+    registers (0, default); the same results bit for bit."""
+    _lib.load().simplex_set_sweep_lds(int(on))
+
+
 def set_batch(p):
     """Pivots per tableau sweep (1..64; <= 0: auto -- 64 when the tableau has >= 4096 rows, else 32).
     Batches above 32 run only in the fused batches (one shard's and the peer-memory multi-rank

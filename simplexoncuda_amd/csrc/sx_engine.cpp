@@ -1854,6 +1854,7 @@ long long simplex_hang_recoveries(void) { return g_cfg.hang_recoveries; }
 long long simplex_fused_batches(void) { return g_cfg.fused_batches; }
 void simplex_set_fine_pivot_rows(int mode) { g_cfg.fine_u = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_blocked(int mode) { g_cfg.blocked = mode < 0 ? -1 : (mode ? 1 : 0); }
+void simplex_set_sweep_lds(int on) { sx_set_sweep_lds(on); }
 void simplex_set_first_batch_id(unsigned int id) { g_cfg.first_batch_id = (id >= 1 && id < SX_BATCH_IDS) ? id : 1; }
 
 void enableBenchmarkMode(void) { g_cfg.benchmark = true; }

@@ -2495,6 +2495,97 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, T
     }
 }
 
+// The rows that left the basis in a batch (k_msweep, k_msweep_lds): row r_s (first slot s where
+// it left) by the row slot s % G, one column per lane, the guarded chain from its stored values
+// (the strips left them unwritten).  The row slot's rows are found in one round trip (lane k:
+// slot gy + G k), and each row's operands -- its stored values, the column's pivot-row values (32
+// slots at a time), the row's factors and the pivots (lane s: slot s, read by v_readlane) -- are
+// loaded together: one or two round trips per row instead of one per 16 slots.
+template <int NKB>
+__device__ __forceinline__ void msweep_fixup(const double *Tr, double *Tw, size_t ldr, int cr, int c0, int Ns, int rows,
+                                             int row0, TLay tl, int gy, int G, int cnt,
+                                             const double *__restrict__ F, const double *__restrict__ U, size_t ld,
+                                             const PivRec *__restrict__ recs,
+                                             const unsigned long long *__restrict__ PM,
+                                             const unsigned long long *__restrict__ PM2, unsigned B, unsigned mask,
+                                             unsigned mask2) {
+    const int OOB = 0x7fffffff;
+    const int l = (int)threadIdx.x & 63;
+    const int j = c0 + l;
+    int rk = -1;                // lane k: the row of slot gy + G k, if this is its first slot
+    unsigned long long bk = 0;  // ... and its leaving slots
+    {
+        const int sk = gy + G * l;
+        if (sk < cnt) {
+            const int r = recs[sk].r - row0;
+            if (r >= 0 && r < rows) {
+                bk = (unsigned long long)pend_bits(PM, r, B, mask) |
+                     ((unsigned long long)(mask2 ? pend_bits(PM2, r, B, mask2) : 0u) << SX_HMAX);
+                if (bk != 0ull && (int)__builtin_ctzll(bk) == sk) rk = r;
+            }
+        }
+    }
+    const double pl = l < cnt ? recs[l].p : 1.0;  // lane s: p_s
+    unsigned long long todo = __ballot(rk >= 0);
+    // NR rows at a time (independent chains; within each kernel's register budget: the
+    // two-stage kernel's pivot-row registers are free here, the one-stage kernel keeps its 3
+    // waves per SIMD)
+    constexpr int NR = NKB == SX_KMAX / 4 ? 4 : 2;
+    while (todo) {
+        int r[NR];
+        unsigned long long bits[NR];
+        bool live[NR];
+#pragma unroll
+        for (int q1 = 0; q1 < NR; ++q1) {
+            live[q1] = todo != 0ull;
+            const int k = live[q1] ? __builtin_ctzll(todo) : 0;
+            if (live[q1]) todo &= todo - 1ull;
+            r[q1] = __builtin_amdgcn_readlane(rk, k);
+            bits[q1] = ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(bk >> 32), k) << 32) |
+                       (unsigned)__builtin_amdgcn_readlane((int)bk, k);
+        }
+        double x[NR], fl[NR];
+#pragma unroll
+        for (int q1 = 0; q1 < NR; ++q1) {
+            x[q1] = (live[q1] && j < Ns) ? Tr[tl.blk ? TLay::b4(r[q1], cr + l, ldr) : (size_t)r[q1] * ldr + cr + l] : 0.0;
+            fl[q1] = (live[q1] && l < cnt) ? F[sx_fidx(r[q1], l)] : 0.0;  // lane s: F[r][s]
+        }
+        // (32 slots of the column's pivot-row values at a time: registers)
+        for (int c1 = 0; c1 < cnt; c1 += SX_HMAX) {
+            double uu[SX_HMAX];
+#pragma unroll
+            for (int k1 = 0; k1 < SX_HMAX; ++k1)
+                uu[k1] = (c1 + k1 < cnt && j < Ns) ? U[(size_t)(c1 + k1) * ld + j] : 0.0;
+#pragma unroll
+            for (int k1 = 0; k1 < SX_HMAX; ++k1) {
+                const int s1 = c1 + k1;
+                if (s1 < cnt) {
+#pragma unroll
+                    for (int q1 = 0; q1 < NR; ++q1) {
+                        if ((bits[q1] >> s1) & 1ull)
+                            x[q1] = x[q1] / rdlane(pl, s1);
+                        else
+                            x[q1] = fma(rdlane(fl[q1], s1), uu[k1], x[q1]);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int q1 = 0; q1 < NR; ++q1) {
+            if (!live[q1]) continue;
+            // (the row's strip through one resource: its element of column cr + l at b4 within it)
+            const int rr = r[q1];
+            const __amdgpu_buffer_rsrc_t rsr =
+                tl.blk ? __builtin_amdgcn_make_buffer_rsrc(Tw + (size_t)(rr >> 4) * 16 * ldr, 0, (int)(ldr * 16 * 8), 0x00020000)
+                       : __builtin_amdgcn_make_buffer_rsrc(Tw + (size_t)rr * ldr, 0, (int)(ldr * 8), 0x00020000);
+            const int eo = tl.blk ? (int)(TLay::b4(rr & 15, cr + l, ldr) * 8) : (cr + l) * 8;
+            const unsigned long long xb = (unsigned long long)__double_as_longlong(x[q1]);
+            const u32x2 w = {(unsigned)xb, (unsigned)(xb >> 32)};
+            __builtin_amdgcn_raw_buffer_store_b64(w, rsr, j < Ns ? eo : OOB, 0, 16);  // (write-through, as the strips)
+        }
+    }
+}
+
 // K5': the same sweep on the matrix cores.  v_mfma_f64_16x16x4f64 computes a 16x16 tile's
 // D = A B + C as the slot-ordered chain of fused multiply-adds, bit for bit
 // (tools/mfma_f64_probe.hip: every element equals fma(a3, b3, fma(a2, b2, fma(a1, b1,
@@ -2664,86 +2755,222 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
             }
         }
     }
-    // the leaving rows: row r_s (first slot s where it left) by the row slot s % G, one column
-    // per lane, the guarded chain from its stored values (the strips left them unwritten).
-    // The row slot's rows are found in one round trip (lane k: slot gy + G k), and each row's
-    // operands -- its stored values, the column's pivot-row values (32 slots at a time), the row's
-    // factors and the pivots (lane s: slot s, read by v_readlane) -- are loaded together: one or
-    // two round trips per row instead of one per 16 slots.
     if (cnt <= 0) return;
-    const int j = c0 + l;
-    int rk = -1;                // lane k: the row of slot gy + G k, if this is its first slot
-    unsigned long long bk = 0;  // ... and its leaving slots
-    {
-        const int sk = gy + G * l;
-        if (sk < cnt) {
-            const int r = recs[sk].r - row0;
-            if (r >= 0 && r < rows) {
-                bk = (unsigned long long)pend_bits(PM, r, B, mask) |
-                     ((unsigned long long)(mask2 ? pend_bits(PM2, r, B, mask2) : 0u) << SX_HMAX);
-                if (bk != 0ull && (int)__builtin_ctzll(bk) == sk) rk = r;
-            }
+    msweep_fixup<NKB>(Tr, Tw, ldr, cr, c0, Ns, rows, row0, tl, gy, G, cnt, F, U, ld, recs, PM, PM2, B, mask, mask2);
+}
+
+// K5'' (option, simplex_set_sweep_lds): k_msweep with each strip's tableau tiles and factors
+// staged through LDS by LDS-DMA (buffer_load ... lds), one strip ahead: a block's 4 waves walk the
+// same strips, so a strip's factors (SX_KMAX / 4 steps x 64 lanes) are loaded once per block, a
+// quarter by each wave, and each wave loads its own tiles -- 8 KB, one 1-KB LDS-DMA instruction per
+// (pair, row group) fragment, placed lane-linear so every fragment read is one conflict-free
+// ds_read_b128.  Per strip: wait for this strip's DMA (the stores of the previous strip may stay
+// in flight: vmcnt counts loads, stores and LDS-DMA together, in issue order), one block barrier,
+// issue the next strip's DMA into the other buffer, then the matrix steps as k_msweep.  No
+// VGPR-destination global load is issued inside the strip loop (the leaving rows of the batch
+// come from recs, one register per lane), so nothing makes the compiler drain the DMA early.
+// Same operations in the same order as k_msweep: bit-identical results.
+// one LDS-DMA instruction: 16 bytes per lane from the buffer (rs: wave-uniform descriptor) at byte
+// voff into LDS at byte lds + 16 * lane.  Inline asm, so that hipcc ties none of its own waits to
+// it (the builtin made it wait vmcnt(0) before every LDS read of the staged tiles, draining the
+// next strip's DMA): the kernel waits for these loads itself, with counted vmcnt.
+template <bool NT>
+__device__ __forceinline__ void lds_dma16(u32x4 rs, unsigned lds, int voff) {
+    unsigned keep;
+    lds = __builtin_amdgcn_readfirstlane(lds);
+    if constexpr (NT)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(voff), "s"(rs), "s"(lds)
+                     : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(voff), "s"(rs), "s"(lds)
+                     : "memory");
+}
+// a raw buffer descriptor (as __builtin_amdgcn_make_buffer_rsrc(p, 0, bytes, 0x00020000)) in
+// scalar registers
+__device__ __forceinline__ u32x4 sgpr_rsrc(const void *p, unsigned bytes) {
+    const unsigned long long a = (unsigned long long)p;
+    u32x4 r;
+    r.x = __builtin_amdgcn_readfirstlane((unsigned)a);
+    r.y = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32) & 0xffffu);
+    r.z = __builtin_amdgcn_readfirstlane(bytes);
+    r.w = 0x00020000u;
+    return r;
+}
+
+template <int NKB>
+__global__ __launch_bounds__(256, 2) void k_msweep_lds(double *T, int rows, int row0, size_t ld, TLay tl, int Ns,
+                                                       const int *__restrict__ nact, int s0,
+                                                       const double *__restrict__ F, const double *__restrict__ U,
+                                                       const PivRec *__restrict__ recs,
+                                                       const unsigned long long *__restrict__ PM,
+                                                       const unsigned long long *__restrict__ PM2,
+                                                       const DevState *__restrict__ st, unsigned B, int rev,
+                                                       int *__restrict__ rec) {
+    constexpr int FBY = NKB * 64 * 8;  // a strip's factors, bytes
+    constexpr int TBY = 8 * 1024;      // a wave's tiles of a strip, bytes
+    constexpr int BUF = 4 * TBY + FBY; // one stage buffer of the block
+    constexpr int NF = FBY / 4 / 1024; // factor DMA instructions per wave
+    __shared__ __attribute__((aligned(16))) char s_buf[2 * BUF];
+    sweep_record(rec, st, nact);
+    const int cnt = st->batch_tag == B ? st->batch_count : 0;
+    if (cnt <= 0) return;
+    if (nact && s0 + *nact < Ns) Ns = s0 + *nact;
+    const int cb = (Ns + 255) / 256;
+    const int lin = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    const int G = (int)(gridDim.x * gridDim.y) / cb;
+    const int tile = lin % cb, gy = lin / cb;
+    if (gy >= G) return;
+    const int bx = rev ? cb - 1 - tile : tile;
+    const int l = (int)threadIdx.x & 63, jl = l & 15, rg = l >> 4, wv = (int)threadIdx.x >> 6;
+    const int c0 = (bx * 4 + wv) * 64;  // the wave's first column
+    const bool act = c0 < Ns;           // (a wave past the last column still loads its share of the factors)
+    const bool inB = bx * 256 >= tl.jB;
+    double *const Tb = inB ? T + tl.offB : T;
+    const size_t ldr = inB ? tl.ldB : tl.ldA;
+    const int cr = inB ? c0 - tl.jB : c0;
+    const unsigned mask = slot_mask(cnt);
+    const unsigned mask2 = cnt > SX_HMAX ? slot_mask(cnt - SX_HMAX) : 0u;
+    const int nkb = (cnt + 3) >> 2;
+    const int OOB = 0x7fffffff;
+    const int nstrip = (rows + 15) >> 4;
+    const int niter = gy < nstrip ? (nstrip - 1 - gy) / G + 1 : 0;
+    auto strip_r0 = [&](int it) {
+        const int g = gy + it * G;
+        return (rev ? nstrip - 1 - g : g) * 16;
+    };
+    auto strip_rsrc = [&](const double *base, int r0) {
+        const int nr = tl.blk ? 16 : (rows - r0 < 16 ? rows - r0 : 16);
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(base) + (size_t)r0 * ldr, 0,
+                                                 (int)((size_t)nr * ldr * 8), 0x00020000);
+    };
+    auto tile_off = [&](int p, int v) {
+        const int jr = cr + 32 * p + 2 * jl;
+        return tl.blk ? (int)((size_t)((jr >> 2) * 64 + v * 16 + rg * 4 + (jr & 3)) * 8)
+                      : (int)(((size_t)(rg + 4 * v) * ldr + jr) * 8);
+    };
+    // (LDS byte address of the staging buffers; the wave index as a scalar)
+    const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) char *)s_buf;
+    const int wvu = __builtin_amdgcn_readfirstlane(wv);
+    auto issue = [&](int it) {
+        const unsigned bf = lds0 + (unsigned)((it & 1) * BUF);
+        const int r0 = strip_r0(it);
+        if (act) {
+            const int nr = tl.blk ? 16 : (rows - r0 < 16 ? rows - r0 : 16);
+            const u32x4 rsl = sgpr_rsrc(Tb + (size_t)r0 * ldr, (unsigned)((size_t)nr * ldr * 8));
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int j = c0 + 32 * p + 2 * jl;
+                    lds_dma16<true>(rsl, bf + (unsigned)(wvu * TBY + (p * 4 + v) * 1024), j < Ns ? tile_off(p, v) : OOB);
+                }
         }
+        // (the strip's factors: sx_fidx keeps a strip's 64 slots x 16 rows contiguous)
+        const u32x4 rsf = sgpr_rsrc(F + sx_fidx(r0, 0), (unsigned)FBY);
+#pragma unroll
+        for (int n = 0; n < NF; ++n) {
+            const int off = (wvu * NF + n) * 1024;
+            lds_dma16<false>(rsf, bf + (unsigned)(4 * TBY + off), off + l * 16);
+        }
+    };
+    // the lane's columns: c0 + 32p + 2jl and the next, p = 0, 1
+    double2 uf[NKB][2];
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int sl = 4 * kb + rg, j = c0 + 32 * p + 2 * jl;
+            uf[kb][p] = (act && sl < cnt && j < Ns) ? *reinterpret_cast<const double2 *>(U + (size_t)sl * ld + j)
+                                                    : make_double2(0.0, 0.0);
+        }
+    // lane s: the shard row that left at slot s (-1: none, or another shard's)
+    int lrow = -1;
+    if (l < cnt) {
+        const int r = recs[l].r - row0;
+        lrow = r >= 0 && r < rows ? r : -1;
     }
-    const double pl = l < cnt ? recs[l].p : 1.0;  // lane s: p_s
-    unsigned long long todo = __ballot(rk >= 0);
-    // NR rows at a time (independent chains; within each kernel's register budget: the
-    // two-stage kernel's pivot-row registers are free here, the one-stage kernel keeps its 3
-    // waves per SIMD)
-    constexpr int NR = NKB == SX_KMAX / 4 ? 4 : 2;
-    while (todo) {
-        int r[NR];
-        unsigned long long bits[NR];
-        bool live[NR];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (nothing of the above outstanding behind the DMA)
+    if (niter > 0) issue(0);
+    for (int it = 0; it < niter; ++it) {
+        // this strip's DMA done (younger: the previous strip's stores, at least 8 instructions)
+        if (act && it > 0)
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // (every wave's share of the factors has landed; the other buffer is free)
+        asm volatile("" ::: "memory");  // (no LDS read moves above the barrier)
+        if (it + 1 < niter) issue(it + 1);
+        const char *const bf = s_buf + (it & 1) * BUF;
+        double ff[NKB];
 #pragma unroll
-        for (int q1 = 0; q1 < NR; ++q1) {
-            live[q1] = todo != 0ull;
-            const int k = live[q1] ? __builtin_ctzll(todo) : 0;
-            if (live[q1]) todo &= todo - 1ull;
-            r[q1] = __builtin_amdgcn_readlane(rk, k);
-            bits[q1] = ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(bk >> 32), k) << 32) |
-                       (unsigned)__builtin_amdgcn_readlane((int)bk, k);
+        for (int kb = 0; kb < NKB; ++kb) {
+            ff[kb] = *reinterpret_cast<const double *>(bf + 4 * TBY + kb * 512 + l * 8);
+            if (4 * kb + rg >= cnt) ff[kb] = -0.0;
         }
-        double x[NR], fl[NR];
+        if (!act) continue;
+        const int r0 = strip_r0(it);
+        double2 cx[2][4];
 #pragma unroll
-        for (int q1 = 0; q1 < NR; ++q1) {
-            x[q1] = (live[q1] && j < Ns) ? Tr[tl.blk ? TLay::b4(r[q1], cr + l, ldr) : (size_t)r[q1] * ldr + cr + l] : 0.0;
-            fl[q1] = (live[q1] && l < cnt) ? F[sx_fidx(r[q1], l)] : 0.0;  // lane s: F[r][s]
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+                cx[p][v] = *reinterpret_cast<const double2 *>(bf + wv * TBY + (p * 4 + v) * 1024 + l * 16);
+        // the strip's leaving rows (not stored here: bit v of skip, row r0 + rg + 4v)
+        unsigned skip = 0u;
+        const unsigned long long hit = __ballot(lrow >= r0 && lrow < r0 + 16);
+        if (hit) {
+            unsigned m16 = 0u;
+            for (unsigned long long h = hit; h; h &= h - 1ull)
+                m16 |= 1u << (__builtin_amdgcn_readlane(lrow, (int)__builtin_ctzll(h)) - r0);
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+                if ((m16 >> (rg + 4 * v)) & 1u) skip |= 1u << v;
         }
-        // (32 slots of the column's pivot-row values at a time: registers)
-        for (int c1 = 0; c1 < cnt; c1 += SX_HMAX) {
-            double uu[SX_HMAX];
+        const __amdgpu_buffer_rsrc_t rss = strip_rsrc(Tb, r0);
 #pragma unroll
-            for (int k1 = 0; k1 < SX_HMAX; ++k1)
-                uu[k1] = (c1 + k1 < cnt && j < Ns) ? U[(size_t)(c1 + k1) * ld + j] : 0.0;
+        for (int p = 0; p < 2; ++p) {
+            const int j = c0 + 32 * p + 2 * jl;
+            d4_t ax = {cx[p][0].x, cx[p][1].x, cx[p][2].x, cx[p][3].x};
+            d4_t ay = {cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
+            if (nkb == NKB) {
 #pragma unroll
-            for (int k1 = 0; k1 < SX_HMAX; ++k1) {
-                const int s1 = c1 + k1;
-                if (s1 < cnt) {
+                for (int kb = 0; kb < NKB; ++kb) {
+                    ax = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].x, ax, 0, 0, 0);
+                    ay = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].y, ay, 0, 0, 0);
+                }
+            } else {
 #pragma unroll
-                    for (int q1 = 0; q1 < NR; ++q1) {
-                        if ((bits[q1] >> s1) & 1ull)
-                            x[q1] = x[q1] / rdlane(pl, s1);
-                        else
-                            x[q1] = fma(rdlane(fl[q1], s1), uu[k1], x[q1]);
+                for (int kb = 0; kb < NKB; ++kb)
+                    if (kb < nkb) {
+                        ax = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].x, ax, 0, 0, 0);
+                        ay = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].y, ay, 0, 0, 0);
                     }
+            }
+            const bool pair = j + 1 < Ns;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int off = tile_off(p, v);
+                const bool keep = j < Ns && !((skip >> v) & 1u);
+                if (pair) {
+                    const double2 y = make_double2(ax[v], ay[v]);
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rss, keep ? off : OOB, 0, 16);
+                } else {
+                    const unsigned long long xb = (unsigned long long)__double_as_longlong(ax[v]);
+                    const u32x2 w = {(unsigned)xb, (unsigned)(xb >> 32)};
+                    __builtin_amdgcn_raw_buffer_store_b64(w, rss, keep ? off : OOB, 0, 16);
                 }
             }
         }
-#pragma unroll
-        for (int q1 = 0; q1 < NR; ++q1) {
-            if (!live[q1]) continue;
-            // (the row's strip through one resource: its element of column cr + l at b4 within it)
-            const int rr = r[q1];
-            const __amdgpu_buffer_rsrc_t rsr =
-                tl.blk ? __builtin_amdgcn_make_buffer_rsrc(Tw + (size_t)(rr >> 4) * 16 * ldr, 0, (int)(ldr * 16 * 8), 0x00020000)
-                       : __builtin_amdgcn_make_buffer_rsrc(Tw + (size_t)rr * ldr, 0, (int)(ldr * 8), 0x00020000);
-            const int eo = tl.blk ? (int)(TLay::b4(rr & 15, cr + l, ldr) * 8) : (cr + l) * 8;
-            const unsigned long long xb = (unsigned long long)__double_as_longlong(x[q1]);
-            const u32x2 w = {(unsigned)xb, (unsigned)(xb >> 32)};
-            __builtin_amdgcn_raw_buffer_store_b64(w, rsr, j < Ns ? eo : OOB, 0, 16);  // (write-through, as the strips)
-        }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!act) return;
+    msweep_fixup<NKB>(Tb, Tb, ldr, cr, c0, Ns, rows, row0, tl, gy, G, cnt, F, U, ld, recs, PM, PM2, B, mask, mask2);
 }
 
 // Slack compaction (sx_common.hpp Cols), between a batch's selections and its
@@ -3111,6 +3338,13 @@ static void launch_sweep_k(double *T, int rows, size_t ld, TLay tl, int Ns, cons
 // 32768 rows); the two-stage kernel with twice its resident grid when each block would walk 64
 // strips or more (32768 x 9216: 974 vs 1006 us; at 4096 rows the resident grid stays best).  An
 // explicit simplex_set_update_waves overrides both.
+// the matrix-core sweep with LDS-DMA staging (k_msweep_lds): SIMPLEX_SWEEP_LDS=1 or sx_set_sweep_lds
+static int g_sweep_lds = [] {
+    const char *e = getenv("SIMPLEX_SWEEP_LDS");
+    return e && atoi(e) != 0 ? 1 : 0;
+}();
+void sx_set_sweep_lds(int on) { g_sweep_lds = on ? 1 : 0; }
+
 static int msweep_slots(int capacity, int cb, int rows, bool two_stage) {
     if (g_sweep_waves != 1.0f) return row_slots(capacity, cb, rows, 16);
     if (!two_stage) return row_slots(capacity, cb, rows, 16, 2.0f / 3.0f);
@@ -3133,6 +3367,18 @@ void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, 
         if (ld % 2 != 0 || tl.ldA % 2 != 0 || (tl.jB < Ns && (tl.jB % 256 != 0 || tl.ldB % 2 != 0 || tl.offB % 2 != 0)))
             SX_FATAL("matrix-core sweep: 16-byte rows and 256-aligned regions required");
         const int cb = (Ns + 255) / 256;
+        if (g_sweep_lds) {
+            if (cfg.batch > SX_HMAX) {
+                dim3 grid(cb, msweep_slots(sweep_capacity<k_msweep_lds<SX_KMAX / 4>>(), cb, rows, true));
+                k_msweep_lds<SX_KMAX / 4><<<grid, 256, 0, s>>>(T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs,
+                                                               pd.PM, pd.PM2, st, pd.batch, rev, g_sweep_rec);
+            } else {
+                dim3 grid(cb, msweep_slots(sweep_capacity<k_msweep_lds<SX_HMAX / 4>>(), cb, rows, false));
+                k_msweep_lds<SX_HMAX / 4><<<grid, 256, 0, s>>>(T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs,
+                                                               pd.PM, pd.PM2, st, pd.batch, rev, g_sweep_rec);
+            }
+            return;
+        }
         if (cfg.batch > SX_HMAX) {
             dim3 grid(cb, msweep_slots(sweep_capacity<k_msweep<SX_KMAX / 4>>(), cb, rows, true));
             k_msweep<SX_KMAX / 4><<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM,

@@ -231,7 +231,7 @@ def _pivots_with(cfg, T, d, base, k):
     setters = {"batch": (sx.set_batch, 0),
                "fused": (sx.set_fused, -1), "p2p": (sx.set_p2p, -1),
                "waves": (sx.set_update_waves, 0), "W": (sx.set_virtual_ranks, 1),
-               "mfma": (sx.set_sweep_mfma, -1)}
+               "mfma": (sx.set_sweep_mfma, -1), "lds": (sx.set_sweep_lds, 0)}
     try:
         for key, val in cfg.items():
             setters[key][0](val)
@@ -394,6 +394,39 @@ def test_p2p_fused_two_phase_two_stages(gpu, W, n, m, seed, lo, hi):
         sx.set_virtual_ranks(1)
 
 
+@pytest.mark.parametrize("batch,inst,W", [(5, (333, 1025, 7), 1), (31, (333, 1025, 7), 1), (32, (300, 1100, 11), 1),
+                                         (40, (333, 1025, 7), 1), (64, (300, 1100, 11), 1), (64, (333, 1025, 7), 1),
+                                         (64, (300, 1100, 11), 4), (32, (300, 1100, 11), 8)])
+def test_lds_staged_sweep_bit_exact(gpu, batch, inst, W):
+    """the matrix-core sweep with each strip's tiles and factors staged through LDS by LDS-DMA
+    (k_msweep_lds, simplex_set_sweep_lds): one- and two-stage batches, partial last batches and a
+    partial last strip, leaving rows skipped per strip from the batch's records, virtual shards
+    (rows of other shards in the records): the oracle's bits"""
+    T, d, base = _phase1_state(*inst)
+    cfg = {"batch": batch, "lds": 1, "mfma": 1}
+    if W > 1:
+        cfg.update({"W": W, "p2p": 1})
+    Tg, dg, bg, st, done = _pivots_with(cfg, T, d, base, 150)
+    st_o, done_o = oracle.solve(T, d, base, max_pivots=150)
+    assert done == done_o
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+@pytest.mark.parametrize("n,m,seed,lo,hi", [(300, 1100, 41100, 1, 100), (129, 1513, 77, -100, 100),
+                                            (40, 700, 4070, 1, 100)])
+def test_lds_staged_sweep_whole_phase(gpu, n, m, seed, lo, hi):
+    """whole two-phase solves with the LDS-staged sweep (generated tableaux: blocked layout,
+    aliased artificials, slack compaction)"""
+    p = sx.generateRandomProblem(n, m, seed, lo, hi)
+    try:
+        sx.set_sweep_lds(1)
+        sx.set_batch(64)
+        _check_two_phase(p)
+    finally:
+        sx.set_batch(0)
+        sx.set_sweep_lds(0)
+
+
 @pytest.mark.parametrize("mfma", [1, 0])
 @pytest.mark.parametrize("waves", [1e-4, 0.3, 1, 4])
 def test_sweep_grid_bit_exact(gpu, mfma, waves):
@@ -401,6 +434,17 @@ def test_sweep_grid_bit_exact(gpu, mfma, waves):
     than row groups; both sweeps"""
     T, d, base = _phase1_state(210, 1700, 3)
     Tg, dg, bg, st, done = _pivots_with({"mfma": mfma, "waves": waves, "batch": 16}, T, d, base, 90)
+    oracle.solve(T, d, base, max_pivots=90)
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+@pytest.mark.parametrize("batch", [16, 64])
+@pytest.mark.parametrize("waves", [1e-4, 0.3, 4])
+def test_lds_staged_sweep_grid(gpu, batch, waves):
+    """the LDS-staged sweep from one block per column tile (every strip through the two
+    buffers) to more blocks than strips (blocks with no strip meet no barrier): bit-exact"""
+    T, d, base = _phase1_state(210, 1700, 3)
+    Tg, dg, bg, st, done = _pivots_with({"mfma": 1, "lds": 1, "waves": waves, "batch": batch}, T, d, base, 90)
     oracle.solve(T, d, base, max_pivots=90)
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
