@@ -687,7 +687,12 @@ class Engine {
         // (coherent with the peers' system-scope writes by construction, not through this device's
         // L2: DESIGN.md §5); on one device, or when forced off, plain device memory.
         x.d = dalloc<double>(round_up((size_t)N1, 16));
-        x.fineU = g_cfg.fine_u > 0 || (g_cfg.fine_u < 0 && ((rccl && !ipc) || multidev));
+        int fu = g_cfg.fine_u;
+        if (fu < 0) {  // (SIMPLEX_FINE_PIVOT_ROWS=0/1 overrides the default, as simplex_set_fine_pivot_rows)
+            const char *e = getenv("SIMPLEX_FINE_PIVOT_ROWS");
+            if (e) fu = atoi(e) != 0 ? 1 : 0;
+        }
+        x.fineU = fu > 0 || (fu < 0 && ((rccl && !ipc) || multidev));
         if (x.fineU)
             SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&x.U), (size_t)SX_KMAX * ld * sizeof(double),
                                          hipDeviceMallocFinegrained));

@@ -2495,6 +2495,60 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, T
     }
 }
 
+// A strip's matrix steps (k_msweep, k_msweep_lds): acc[p][0] / acc[p][1] = tile X / Y of pair p; all
+// four chains advance one 4-slot step at a time (each element's fmas stay in slot order)
+template <int NKB>
+__device__ __forceinline__ void msweep_steps(d4_t (&acc)[2][2], const double (&ff)[NKB], const double2 (&uf)[NKB][2],
+                                             int nkb) {
+    if (nkb == NKB) {
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                acc[p][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].x, acc[p][0], 0, 0, 0);
+                acc[p][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].y, acc[p][1], 0, 0, 0);
+            }
+    } else {
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+            if (kb < nkb)
+#pragma unroll
+                for (int p = 0; p < 2; ++p) {
+                    acc[p][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].x, acc[p][0], 0, 0, 0);
+                    acc[p][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].y, acc[p][1], 0, 0, 0);
+                }
+    }
+}
+
+// ... and its stores: the lane's column pair of rows rg + 4v, write-through; a leaving row (bit v of
+// skip) and columns past Ns are not written; an odd last column's neighbour is an untouched
+// column: only the even one is written
+template <typename OFF>
+__device__ __forceinline__ void msweep_store(const d4_t (&acc)[2][2], __amdgpu_buffer_rsrc_t rss, int c0, int jl, int Ns,
+                                             unsigned skip, OFF tile_off) {
+    const int OOB = 0x7fffffff;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const int j = c0 + 32 * p + 2 * jl;
+        const bool pair = j + 1 < Ns;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int off = tile_off(p, v);
+            const bool keep = j < Ns && !((skip >> v) & 1u);
+            if (pair) {
+                const double2 y = make_double2(acc[p][0][v], acc[p][1][v]);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rss, keep ? off : OOB, 0, 16);
+            } else {
+                // (built from the 64-bit integer: a bit_cast of acc[p][0][v] straight to u32x2 compiled
+                // to a store of element 0 for every v -- ROCm 7.2 clang, checked in the ISA)
+                const unsigned long long xb = (unsigned long long)__double_as_longlong(acc[p][0][v]);
+                const u32x2 w = {(unsigned)xb, (unsigned)(xb >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b64(w, rss, keep ? off : OOB, 0, 16);
+            }
+        }
+    }
+}
+
 // The rows that left the basis in a batch (k_msweep, k_msweep_lds): row r_s (first slot s where
 // it left) by the row slot s % G, one column per lane, the guarded chain from its stored values
 // (the strips left them unwritten).  The row slot's rows are found in one round trip (lane k:
@@ -2686,8 +2740,8 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
             const int fr = r0 + jl;  // the A-operand row of this lane
             const __amdgpu_buffer_rsrc_t rss = strip_rsrc(Tw, r0);
             // issue order: both pairs' tableau tiles, the strip's factors, its leaving-row bits --
-            // one memory round trip per strip (the bits are only needed after the first pair's
-            // matrix steps, and the counter waits are in issue order)
+            // one memory round trip per strip (the bits are only needed after the matrix steps,
+            // and the counter waits are in issue order)
             double2 cx[2][4];
             load_tiles(cx, r0);
             double ff[NKB];
@@ -2703,56 +2757,28 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb)
                 if (4 * kb + rg >= cnt) ff[kb] = -0.0;
-            bool fix = false;
-            unsigned skip = 0u;  // bit v: row r0 + rg + 4v is a leaving row (not stored here)
+            // both pairs' four accumulators advance together: four independent MFMA chains per wave
+            // (two chains at a time left the matrix pipe waiting on each step's result)
+            d4_t acc[2][2];
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
-                const int j = c0 + 32 * p + 2 * jl;
-                d4_t ax = {cx[p][0].x, cx[p][1].x, cx[p][2].x, cx[p][3].x};
-                d4_t ay = {cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
-                if (nkb == NKB) {
-#pragma unroll
-                    for (int kb = 0; kb < NKB; ++kb) {
-                        ax = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].x, ax, 0, 0, 0);
-                        ay = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].y, ay, 0, 0, 0);
-                    }
-                } else {
-#pragma unroll
-                    for (int kb = 0; kb < NKB; ++kb)
-                        if (kb < nkb) {
-                            ax = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].x, ax, 0, 0, 0);
-                            ay = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].y, ay, 0, 0, 0);
-                        }
-                }
-                if (p == 0) {
-                    // row fr's slots as a leaving row (both stages)
-                    const unsigned lb = fr < rows ? ((((unsigned)(pm1 >> 32) == B) ? ((unsigned)pm1 & mask) : 0u) |
-                                                     (((unsigned)(pm2 >> 32) == B) ? ((unsigned)pm2 & mask2) : 0u))
-                                                  : 0u;
-                    fix = __ballot(lb != 0u) != 0ull;
-                    if (fix)
-#pragma unroll
-                        for (int v = 0; v < 4; ++v)
-                            if (__shfl(lb, rg + 4 * v) != 0u) skip |= 1u << v;  // (lane rg + 4v: that row's bits)
-                }
-                const bool pair = j + 1 < Ns;
-#pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    const int off = tile_off(p, v);
-                    const bool keep = j < Ns && !((skip >> v) & 1u);
-                    if (pair) {
-                        const double2 y = make_double2(ax[v], ay[v]);
-                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rss, keep ? off : OOB, 0,
-                                                               16);
-                    } else {
-                        // (built from the 64-bit integer: a bit_cast of ax[v] straight to u32x2 compiled
-                        // to a store of ax[0] for every v -- ROCm 7.2 clang, checked in the ISA)
-                        const unsigned long long xb = (unsigned long long)__double_as_longlong(ax[v]);
-                        const u32x2 w = {(unsigned)xb, (unsigned)(xb >> 32)};
-                        __builtin_amdgcn_raw_buffer_store_b64(w, rss, keep ? off : OOB, 0, 16);
-                    }
-                }
+                acc[p][0] = d4_t{cx[p][0].x, cx[p][1].x, cx[p][2].x, cx[p][3].x};
+                acc[p][1] = d4_t{cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
             }
+            msweep_steps<NKB>(acc, ff, uf, nkb);
+            // row fr's slots as a leaving row (both stages); bit v of skip: row r0 + rg + 4v leaves (not
+            // stored here)
+            unsigned skip = 0u;
+            {
+                const unsigned lb = fr < rows ? ((((unsigned)(pm1 >> 32) == B) ? ((unsigned)pm1 & mask) : 0u) |
+                                                 (((unsigned)(pm2 >> 32) == B) ? ((unsigned)pm2 & mask2) : 0u))
+                                              : 0u;
+                if (__ballot(lb != 0u) != 0ull)
+#pragma unroll
+                    for (int v = 0; v < 4; ++v)
+                        if (__shfl(lb, rg + 4 * v) != 0u) skip |= 1u << v;  // (lane rg + 4v: that row's bits)
+            }
+            msweep_store(acc, rss, c0, jl, Ns, skip, tile_off);
         }
     }
     if (cnt <= 0) return;
@@ -2933,40 +2959,14 @@ __global__ __launch_bounds__(256, 2) void k_msweep_lds(double *T, int rows, int 
                 if ((m16 >> (rg + 4 * v)) & 1u) skip |= 1u << v;
         }
         const __amdgpu_buffer_rsrc_t rss = strip_rsrc(Tb, r0);
+        d4_t acc[2][2];
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
-            const int j = c0 + 32 * p + 2 * jl;
-            d4_t ax = {cx[p][0].x, cx[p][1].x, cx[p][2].x, cx[p][3].x};
-            d4_t ay = {cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
-            if (nkb == NKB) {
-#pragma unroll
-                for (int kb = 0; kb < NKB; ++kb) {
-                    ax = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].x, ax, 0, 0, 0);
-                    ay = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].y, ay, 0, 0, 0);
-                }
-            } else {
-#pragma unroll
-                for (int kb = 0; kb < NKB; ++kb)
-                    if (kb < nkb) {
-                        ax = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].x, ax, 0, 0, 0);
-                        ay = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].y, ay, 0, 0, 0);
-                    }
-            }
-            const bool pair = j + 1 < Ns;
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                const int off = tile_off(p, v);
-                const bool keep = j < Ns && !((skip >> v) & 1u);
-                if (pair) {
-                    const double2 y = make_double2(ax[v], ay[v]);
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rss, keep ? off : OOB, 0, 16);
-                } else {
-                    const unsigned long long xb = (unsigned long long)__double_as_longlong(ax[v]);
-                    const u32x2 w = {(unsigned)xb, (unsigned)(xb >> 32)};
-                    __builtin_amdgcn_raw_buffer_store_b64(w, rss, keep ? off : OOB, 0, 16);
-                }
-            }
+            acc[p][0] = d4_t{cx[p][0].x, cx[p][1].x, cx[p][2].x, cx[p][3].x};
+            acc[p][1] = d4_t{cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
         }
+        msweep_steps<NKB>(acc, ff, uf, nkb);
+        msweep_store(acc, rss, c0, jl, Ns, skip, tile_off);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!act) return;
