@@ -266,11 +266,14 @@ def main():
     def exchange_name():
         if n_gpus == 1:
             return "none (one shard)"
-        if world > 1:
-            return ("peer-memory fused batch (xGMI)" if sx.p2p_ready() else
-                    "per-pivot RCCL collectives (FALLBACK: the peer-memory self-check failed; slower than 1 GPU)")
-        return ("peer-memory fused batch, one launch per GPU (xGMI)" if sx.load().simplex_p2p_ready() else
-                "per-pivot device copies (FALLBACK: the peer-memory self-check failed)")
+        # the start-up self-check's verdict on these devices (simplex_multi_gpu_mode)
+        mode = sx.load().simplex_multi_gpu_mode()
+        form = "" if world > 1 else ", one launch per GPU"
+        return {2: f"peer-memory fused batch{form} (xGMI)",
+                1: ("per-pivot exchange (FALLBACK: the peer-memory batches failed the self-check against a "
+                    "one-shard solve; slower than 1 GPU)"),
+                0: ("none: every solve on one device (FALLBACK: the shards' exchange failed the self-check "
+                    "against a one-shard solve)")}.get(mode, f"unknown (self-check not run, mode {mode})")
 
     def workload(cfg, r):
         return (f"{cfg}: phase-1 pivots, {r['m']}x{1 + r['n'] + 2 * r['m']} fp64 tableau "
