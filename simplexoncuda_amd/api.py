@@ -382,6 +382,18 @@ def set_update_waves(w):
     _lib.load().simplex_set_update_waves(float(w))
 
 
+def set_blocked(mode):
+    """New engines' tableau storage: -1 default (row-major unless SIMPLEX_BLOCKED=1), 1 the blocked
+    layout (4x4 blocks in 16-row strips), 0 row-major."""
+    _lib.load().simplex_set_blocked(int(mode))
+
+
+def set_fine_pivot_rows(mode):
+    """Pending pivot rows U in fine-grained memory: -1 default (when shards sit on different
+    devices), 1 always, 0 never."""
+    _lib.load().simplex_set_fine_pivot_rows(int(mode))
+
+
 def set_regions(mode):
     """New engines' tableau layout: 0 plain rows, 1 auto two-region layout (default), >= 2 region A
     forced to that many slack positions (test hook)."""
@@ -407,6 +419,12 @@ def set_sweep_lds(on):
     """The matrix-core sweep with its strips staged through LDS by LDS-DMA (1) or loaded to
     registers (0, default); the same results bit for bit."""
     _lib.load().simplex_set_sweep_lds(int(on))
+
+
+def set_sweep_interleave(on):
+    """The matrix-core sweep with both tile pairs' four MFMA chains interleaved (1) or pair by pair
+    (0, default); the same results bit for bit."""
+    _lib.load().simplex_set_sweep_interleave(int(on))
 
 
 def set_batch(p):

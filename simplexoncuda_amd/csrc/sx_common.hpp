@@ -237,6 +237,7 @@ void sx_launch_batch_mr_multi(const MrLaunchRank *ranks, int nloc, int W, int rp
                               int k, int slots, const PeerView &pv, unsigned long long timeout, hipStream_t s);
 void sx_set_update_waves(float w);  // resident-grid multiple of the sweep (default 1)
 void sx_set_sweep_lds(int on);      // the matrix-core sweep staged through LDS by LDS-DMA (k_msweep_lds)
+void sx_set_sweep_interleave(int on);  // the matrix-core sweep's four interleaved MFMA chains per wave
 void sx_set_sweep_record(int *rec);  // next sweeps write (batch tag, count, nact) to rec[0..2] (null: off)
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s);
 void sx_launch_l2_writeback(hipStream_t s);  // every XCD's L2 writes back its dirty lines

@@ -81,8 +81,8 @@ struct Config {
     int mr_two_stage = -1;         // peer-memory multi-rank batches of two stages (-1: unless SIMPLEX_MR_STAGES=1)
     unsigned first_batch_id = 1;   // test hook: batch id of a new engine's first batch
     int fine_u = -1;               // U in fine-grained memory: -1 across devices, 1 always, 0 never
-    int blocked = -1;              // the engine's tableaux in 4x4 blocks (TLay::blk): -1 default (on unless
-                                   // SIMPLEX_BLOCKED=0), 0 row-major, 1 blocked
+    int blocked = -1;              // the engine's tableaux in 4x4 blocks (TLay::blk): -1 default (off unless
+                                   // SIMPLEX_BLOCKED=1), 0 row-major, 1 blocked
     int ipc_rank = -1, ipc_world = 0;  // test hook: one shard per process, peers through IPC handles, no RCCL
     long long hang_recoveries = 0; // fused batches aborted and re-run on the per-pivot path
     long long fused_batches = 0;   // fused batch launches (every shard's counted once)
@@ -229,10 +229,12 @@ int gpus_check(const std::vector<int> &devs);
 
 // the engine's own tableaux in 4x4 blocks (TLay::blk) unless SIMPLEX_BLOCKED=0 or
 // simplex_set_blocked(0)
+// (off by default until the blocked layout has run on the GPU: SIMPLEX_BLOCKED=1 or
+// simplex_set_blocked(1) opts in)
 bool use_blocked() {
     if (g_cfg.blocked < 0) {
         const char *e = getenv("SIMPLEX_BLOCKED");
-        return !(e && atoi(e) == 0);
+        return e && atoi(e) != 0;
     }
     return g_cfg.blocked != 0;
 }
@@ -743,9 +745,9 @@ class Engine {
         }
         if (x.gdone) SX_HIP(hipMemsetAsync(x.gdone, 0, SX_MAXW * 8, x.s));
         SX_HIP(hipMemsetAsync(x.chan, 0, sizeof(BatchChan), x.s));
-        {  // the fused batch's adaptive poll back-off (SIMPLEX_BACKOFF=0 turns it off)
+        {  // the fused batch's adaptive poll back-off (opt-in, SIMPLEX_BACKOFF=1: not yet run on the GPU)
             const char *e = getenv("SIMPLEX_BACKOFF");
-            const unsigned bo = (e && atoi(e) == 0) ? 0u : 1u;
+            const unsigned bo = (e && atoi(e) != 0) ? 1u : 0u;
             SX_HIP(hipMemcpyAsync(&x.chan->backoff, &bo, sizeof(unsigned), hipMemcpyHostToDevice, x.s));
             // copies of every hand-off record (SIMPLEX_REC_COPIES, 1..SX_REC_COPIES)
             const char *rc = getenv("SIMPLEX_REC_COPIES");
@@ -1860,6 +1862,7 @@ long long simplex_fused_batches(void) { return g_cfg.fused_batches; }
 void simplex_set_fine_pivot_rows(int mode) { g_cfg.fine_u = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_blocked(int mode) { g_cfg.blocked = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_sweep_lds(int on) { sx_set_sweep_lds(on); }
+void simplex_set_sweep_interleave(int on) { sx_set_sweep_interleave(on); }
 void simplex_set_first_batch_id(unsigned int id) { g_cfg.first_batch_id = (id >= 1 && id < SX_BATCH_IDS) ? id : 1; }
 
 void enableBenchmarkMode(void) { g_cfg.benchmark = true; }

@@ -2661,8 +2661,10 @@ __device__ __forceinline__ void msweep_fixup(const double *Tr, double *Tw, size_
 // Grid, column order, regions, compaction and cache policy as k_sweep (POL 1), with 256-column
 // tiles.  In place (Tsrc == Tdst: the strips read through one pointer and write through the other).
 // NKB: 4-slot steps held (SX_HMAX / 4: one stage, 3 waves per SIMD; SX_KMAX / 4: two stages,
-// 2 waves per SIMD).
-template <int NKB>
+// 2 waves per SIMD).  ILV (opt-in, SIMPLEX_SWEEP_ILV=1, not yet run on the GPU): both pairs' four
+// accumulators advance together (msweep_steps) instead of pair 0's two chains, its stores, then
+// pair 1's -- the same fmas per element in the same order.
+template <int NKB, bool ILV>
 __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *Tdst, int rows, int row0, size_t ld,
                                                    TLay tl, int Ns, const int *__restrict__ nact, int s0,
                                                    const double *__restrict__ F, const double *__restrict__ U,
@@ -2740,8 +2742,8 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
             const int fr = r0 + jl;  // the A-operand row of this lane
             const __amdgpu_buffer_rsrc_t rss = strip_rsrc(Tw, r0);
             // issue order: both pairs' tableau tiles, the strip's factors, its leaving-row bits --
-            // one memory round trip per strip (the bits are only needed after the matrix steps,
-            // and the counter waits are in issue order)
+            // one memory round trip per strip (the bits are only needed after the first pair's
+            // matrix steps, and the counter waits are in issue order)
             double2 cx[2][4];
             load_tiles(cx, r0);
             double ff[NKB];
@@ -2757,28 +2759,81 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb)
                 if (4 * kb + rg >= cnt) ff[kb] = -0.0;
-            // both pairs' four accumulators advance together: four independent MFMA chains per wave
-            // (two chains at a time left the matrix pipe waiting on each step's result)
-            d4_t acc[2][2];
+            if constexpr (ILV) {
+                // both pairs' four accumulators advance together: four independent MFMA chains per
+                // wave (two chains at a time leave the matrix pipe waiting on each step's result)
+                d4_t acc[2][2];
 #pragma unroll
-            for (int p = 0; p < 2; ++p) {
-                acc[p][0] = d4_t{cx[p][0].x, cx[p][1].x, cx[p][2].x, cx[p][3].x};
-                acc[p][1] = d4_t{cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
-            }
-            msweep_steps<NKB>(acc, ff, uf, nkb);
-            // row fr's slots as a leaving row (both stages); bit v of skip: row r0 + rg + 4v leaves (not
-            // stored here)
-            unsigned skip = 0u;
-            {
-                const unsigned lb = fr < rows ? ((((unsigned)(pm1 >> 32) == B) ? ((unsigned)pm1 & mask) : 0u) |
-                                                 (((unsigned)(pm2 >> 32) == B) ? ((unsigned)pm2 & mask2) : 0u))
-                                              : 0u;
-                if (__ballot(lb != 0u) != 0ull)
+                for (int p = 0; p < 2; ++p) {
+                    acc[p][0] = d4_t{cx[p][0].x, cx[p][1].x, cx[p][2].x, cx[p][3].x};
+                    acc[p][1] = d4_t{cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
+                }
+                msweep_steps<NKB>(acc, ff, uf, nkb);
+                // row fr's slots as a leaving row (both stages); bit v of skip: row r0 + rg + 4v
+                // leaves (not stored here)
+                unsigned skip = 0u;
+                {
+                    const unsigned lb = fr < rows ? ((((unsigned)(pm1 >> 32) == B) ? ((unsigned)pm1 & mask) : 0u) |
+                                                     (((unsigned)(pm2 >> 32) == B) ? ((unsigned)pm2 & mask2) : 0u))
+                                                  : 0u;
+                    if (__ballot(lb != 0u) != 0ull)
 #pragma unroll
-                    for (int v = 0; v < 4; ++v)
-                        if (__shfl(lb, rg + 4 * v) != 0u) skip |= 1u << v;  // (lane rg + 4v: that row's bits)
+                        for (int v = 0; v < 4; ++v)
+                            if (__shfl(lb, rg + 4 * v) != 0u) skip |= 1u << v;  // (lane rg + 4v: that row's bits)
+                }
+                msweep_store(acc, rss, c0, jl, Ns, skip, tile_off);
+            } else {
+                bool fix = false;
+                unsigned skip = 0u;  // bit v: row r0 + rg + 4v is a leaving row (not stored here)
+#pragma unroll
+                for (int p = 0; p < 2; ++p) {
+                    const int j = c0 + 32 * p + 2 * jl;
+                    d4_t ax = {cx[p][0].x, cx[p][1].x, cx[p][2].x, cx[p][3].x};
+                    d4_t ay = {cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
+                    if (nkb == NKB) {
+#pragma unroll
+                        for (int kb = 0; kb < NKB; ++kb) {
+                            ax = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].x, ax, 0, 0, 0);
+                            ay = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].y, ay, 0, 0, 0);
+                        }
+                    } else {
+#pragma unroll
+                        for (int kb = 0; kb < NKB; ++kb)
+                            if (kb < nkb) {
+                                ax = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].x, ax, 0, 0, 0);
+                                ay = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].y, ay, 0, 0, 0);
+                            }
+                    }
+                    if (p == 0) {
+                        // row fr's slots as a leaving row (both stages)
+                        const unsigned lb = fr < rows ? ((((unsigned)(pm1 >> 32) == B) ? ((unsigned)pm1 & mask) : 0u) |
+                                                         (((unsigned)(pm2 >> 32) == B) ? ((unsigned)pm2 & mask2) : 0u))
+                                                      : 0u;
+                        fix = __ballot(lb != 0u) != 0ull;
+                        if (fix)
+#pragma unroll
+                            for (int v = 0; v < 4; ++v)
+                                if (__shfl(lb, rg + 4 * v) != 0u) skip |= 1u << v;  // (lane rg + 4v: that row's bits)
+                    }
+                    const bool pair = j + 1 < Ns;
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        const int off = tile_off(p, v);
+                        const bool keep = j < Ns && !((skip >> v) & 1u);
+                        if (pair) {
+                            const double2 y = make_double2(ax[v], ay[v]);
+                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rss, keep ? off : OOB, 0,
+                                                                   16);
+                        } else {
+                            // (built from the 64-bit integer: a bit_cast of ax[v] straight to u32x2 compiled
+                            // to a store of ax[0] for every v -- ROCm 7.2 clang, checked in the ISA)
+                            const unsigned long long xb = (unsigned long long)__double_as_longlong(ax[v]);
+                            const u32x2 w = {(unsigned)xb, (unsigned)(xb >> 32)};
+                            __builtin_amdgcn_raw_buffer_store_b64(w, rss, keep ? off : OOB, 0, 16);
+                        }
+                    }
+                }
             }
-            msweep_store(acc, rss, c0, jl, Ns, skip, tile_off);
         }
     }
     if (cnt <= 0) return;
@@ -3344,12 +3399,32 @@ static int g_sweep_lds = [] {
     return e && atoi(e) != 0 ? 1 : 0;
 }();
 void sx_set_sweep_lds(int on) { g_sweep_lds = on ? 1 : 0; }
+// the matrix-core sweep's four interleaved MFMA chains (k_msweep<, true>): SIMPLEX_SWEEP_ILV=1
+static int g_sweep_ilv = [] {
+    const char *e = getenv("SIMPLEX_SWEEP_ILV");
+    return e && atoi(e) != 0 ? 1 : 0;
+}();
+void sx_set_sweep_interleave(int on) { g_sweep_ilv = on ? 1 : 0; }
 
 static int msweep_slots(int capacity, int cb, int rows, bool two_stage) {
     if (g_sweep_waves != 1.0f) return row_slots(capacity, cb, rows, 16);
     if (!two_stage) return row_slots(capacity, cb, rows, 16, 2.0f / 3.0f);
     const long long nstrip = (rows + 15) / 16, g0 = std::max(1, capacity / std::max(cb, 1));
     return row_slots(capacity, cb, rows, 16, nstrip / g0 >= 64 ? 2.0f : 1.0f);
+}
+
+template <bool ILV>
+static void launch_msweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, const int *nact, int s0,
+                          const Pending &pd, const DevState *st, int rev, SweepCfg cfg, int cb, hipStream_t s) {
+    if (cfg.batch > SX_HMAX) {
+        dim3 grid(cb, msweep_slots(sweep_capacity<k_msweep<SX_KMAX / 4, ILV>>(), cb, rows, true));
+        k_msweep<SX_KMAX / 4, ILV><<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs,
+                                                        pd.PM, pd.PM2, st, pd.batch, rev, g_sweep_rec);
+    } else {
+        dim3 grid(cb, msweep_slots(sweep_capacity<k_msweep<SX_HMAX / 4, ILV>>(), cb, rows, false));
+        k_msweep<SX_HMAX / 4, ILV><<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs,
+                                                        pd.PM, pd.PM2, st, pd.batch, rev, g_sweep_rec);
+    }
 }
 
 void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, int m, double *T, int rows, int row0,
@@ -3379,15 +3454,10 @@ void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, 
             }
             return;
         }
-        if (cfg.batch > SX_HMAX) {
-            dim3 grid(cb, msweep_slots(sweep_capacity<k_msweep<SX_KMAX / 4>>(), cb, rows, true));
-            k_msweep<SX_KMAX / 4><<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM,
-                                                       pd.PM2, st, pd.batch, rev, g_sweep_rec);
-        } else {
-            dim3 grid(cb, msweep_slots(sweep_capacity<k_msweep<SX_HMAX / 4>>(), cb, rows, false));
-            k_msweep<SX_HMAX / 4><<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs, pd.PM,
-                                                       pd.PM2, st, pd.batch, rev, g_sweep_rec);
-        }
+        if (g_sweep_ilv)
+            launch_msweep<true>(T, rows, row0, ld, tl, Ns, nact, s0, pd, st, rev, cfg, cb, s);
+        else
+            launch_msweep<false>(T, rows, row0, ld, tl, Ns, nact, s0, pd, st, rev, cfg, cb, s);
         return;
     }
     const int k = cfg.batch;  // pivots the sweep may have to apply (register slots)

@@ -91,6 +91,19 @@ def test_simplex_gpus_mode_on_one_device(gpu, name, W):
     run(name, gpus=[0] * W)
 
 
+@pytest.mark.parametrize("name,W,p2p", [("config4", 1, -1), ("config5", 1, -1), ("config5", 8, 1),
+                                        ("config5_degenerate", 1, -1)])
+def test_blocked_layout_pins(gpu, unverified, name, W, p2p):
+    """the full-size pins with the engine's tableaux in 4x4 blocks (simplex_set_blocked(1)): the
+    oracle's tableau, objective row and basis after the pinned pivots, read back through the
+    layout's row transfers"""
+    sx.set_blocked(1)
+    try:
+        run(name, W, 0, p2p)
+    finally:
+        sx.set_blocked(-1)
+
+
 with open(os.path.join(GOLDEN, "variant_solves.json")) as _f:
     VARIANT = json.load(_f)
 
