@@ -45,6 +45,7 @@ def load():
         "orc_pivot": (ctypes.c_int, [_dp, i64, i64, i64, _dp, _ip, _lp, _lp]),
         "orc_solve": (ctypes.c_int, [_dp, i64, i64, i64, _dp, _ip, i64, _lp]),
         "orc_two_phase": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _dp, _dp, _dp, i64, _dp, _dp, _ip, _lp, _dp]),
+        "orc_last_objective_row": (i64, [_dp, i64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -89,6 +90,15 @@ def two_phase(A, b, c, max_pivots=-1):
                            piv.ctypes.data_as(_lp), ctypes.byref(p1v))
     return {"status": st, "x": x[:n], "opt": opt.value, "base": base[:m], "pivots": (int(piv[0]), int(piv[1])),
             "phase1_value": p1v.value}
+
+
+def last_objective_row():
+    """The last two_phase call's final objective row (as simplex_last_objective_row)."""
+    lib = load()
+    n = lib.orc_last_objective_row(None, 0)
+    d = np.zeros(max(n, 1))
+    lib.orc_last_objective_row(p(d), n)
+    return d[:n]
 
 
 def argmin(v):

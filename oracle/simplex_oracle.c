@@ -370,6 +370,21 @@ int orc_solve(double *T, int64_t m, int64_t N, int64_t ld, double *d, int *base,
     return st;
 }
 
+/* the last orc_two_phase call's final objective row: phase 2's (width 1+n+m) when phase 1 ended
+   feasible, else phase 1's (width 1+n+2m) -- what simplex_last_objective_row returns */
+static double *g_last_d = NULL;
+static int64_t g_last_n = 0;
+static void keep_last_d(const double *d, int64_t n) {
+    free(g_last_d);
+    g_last_d = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    memcpy(g_last_d, d, sizeof(double) * (size_t)n);
+    g_last_n = n;
+}
+int64_t orc_last_objective_row(double *out, int64_t cap) {
+    for (int64_t j = 0; out && j < g_last_n && j < cap; ++j) out[j] = g_last_d[j];
+    return g_last_n;
+}
+
 /* twoPhaseMethod (twoPhaseMethod.cu:225-435) */
 int orc_two_phase(int n, int m, const double *A_colmajor, const double *b, const double *c,
                   int64_t max_pivots, double *x, double *opt, int *base_out, int64_t *pivots,
@@ -396,6 +411,7 @@ int orc_two_phase(int n, int m, const double *A_colmajor, const double *b, const
         for (int i = 0; i < m; ++i) /* checkDegeneracy :206-223 */
             if (base[i] >= n + m && base[i] < n + 2 * m) status = ORC_DEGENERATE;
     }
+    if (status != ORC_FEASIBLE) keep_last_d(d, N1);
     if (status == ORC_FEASIBLE) {
         /* phase2 (:285-356): drop artificial columns, d[1..n] = -c, slacks 0, d[0] kept */
         for (int j = 0; j < n; ++j) d[1 + j] = -c[j];
@@ -403,6 +419,7 @@ int orc_two_phase(int n, int m, const double *A_colmajor, const double *b, const
         orc_update_objective(T, m, N2, ld, base, d); /* gauss2, :337 */
         int64_t cap2 = max_pivots < 0 ? -1 : max_pivots;
         status = orc_solve(T, m, N2, ld, d, base, cap2, &p2);
+        keep_last_d(d, N2);
         if (status == ORC_FEASIBLE) {
             /* getSolutionHost (:370-383) */
             if (opt) *opt = d[0];
