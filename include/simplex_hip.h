@@ -110,17 +110,10 @@ void simplex_set_mr_single_launch(int on);
  * -1 auto (when the shards span devices, default), 1 always (test hook: the one-GPU cost and
  * parity of that path), 0 never */
 void simplex_set_fine_pivot_rows(int mode);
-/* new engines' tableau storage inside each region: -1 default (row-major unless the environment sets
- * SIMPLEX_BLOCKED=1; the blocked layout has not yet run on the GPU), 1 blocks of 4 rows x 4 columns
- * in 16-row strips, 0 plain row-major (callers' tableaux, tabular.h, are always
- * row-major) */
+/* new engines' tableau storage inside each region: -1 default (blocks of 4 rows x 4 columns in
+ * 16-row strips, unless the environment sets SIMPLEX_BLOCKED=0), 1 blocked, 0 plain row-major
+ * (callers' tableaux, tabular.h, are always row-major) */
 void simplex_set_blocked(int mode);
-/* Opt-in kernel variants, bit-identical by construction, not yet run on the GPU:
-   the matrix-core sweep with each strip's tableau tiles and factors staged through LDS by LDS-DMA
-   (1; SIMPLEX_SWEEP_LDS=1) or loaded to registers (0, default); and with both tile pairs' four
-   MFMA chains interleaved (1; SIMPLEX_SWEEP_ILV=1) or pair by pair (0, default). */
-void simplex_set_sweep_lds(int on);
-void simplex_set_sweep_interleave(int on);
 
 /* ---- fault handling and test hooks ---- */
 /* a fused batch whose in-kernel hand-off wait times out (SIMPLEX_HANG, never expected) is

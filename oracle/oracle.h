@@ -69,6 +69,9 @@ double orc_ratio(double b, double a);
 /* rank-1 update of rows [0,rows) of a row block plus (optionally) d.
  * prow = pre-update pivot row, colE[i] = pre-update entering-column entry of local row i,
  * r_local = pivot row index inside this block or -1, p = pivot, d_e = entering reduced cost */
+/* host threads of orc_apply_update (default 1; the arithmetic is per element, so the result does
+   not depend on it) */
+void orc_set_threads(int n);
 void orc_apply_update(double *T, int64_t rows, int64_t N, int64_t ld, double *d, const double *prow,
                       const double *colE, int64_t r_local, double p, double d_e);
 

@@ -46,6 +46,7 @@ def load():
         "orc_solve": (ctypes.c_int, [_dp, i64, i64, i64, _dp, _ip, i64, _lp]),
         "orc_two_phase": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _dp, _dp, _dp, i64, _dp, _dp, _ip, _lp, _dp]),
         "orc_last_objective_row": (i64, [_dp, i64]),
+        "orc_set_threads": (None, [ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -16,6 +16,7 @@
 
 #include <float.h>
 #include <math.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -301,9 +302,9 @@ double orc_ratio(double b, double a) { return cmp_eps(a, 0.0) > 0 ? b / a : DBL_
  *   row r:      T[r][j] / p
  *   other rows: fma(-(a_ie/p), T_old[r][j], T[i][j])
  *   objective:  fma(-(d_e/p),  T_old[r][j], d[j]) */
-void orc_apply_update(double *T, int64_t rows, int64_t N, int64_t ld, double *d, const double *prow,
-                      const double *colE, int64_t r_local, double p, double d_e) {
-    for (int64_t i = 0; i < rows; ++i) {
+static void update_rows(double *T, int64_t i0, int64_t i1, int64_t N, int64_t ld, const double *prow,
+                        const double *colE, int64_t r_local, double p) {
+    for (int64_t i = i0; i < i1; ++i) {
         double *row = T + i * ld;
         if (i == r_local) {
             for (int64_t j = 0; j < N; ++j) row[j] = prow[j] / p;
@@ -311,6 +312,44 @@ void orc_apply_update(double *T, int64_t rows, int64_t N, int64_t ld, double *d,
             const double f = -colE[i] / p;
             for (int64_t j = 0; j < N; ++j) row[j] = fma(f, prow[j], row[j]);
         }
+    }
+}
+
+/* Rows may be updated by several host threads (orc_set_threads, default 1): every element still
+   receives exactly the one operation above, so the result does not depend on the thread count.
+   Used only to make the long full-size pins (tests/golden/scripts/make_long_pins.py) affordable;
+   the timed CPU baseline runs with one thread. */
+static int g_threads = 1;
+void orc_set_threads(int n) { g_threads = n < 1 ? 1 : n > 64 ? 64 : n; }
+
+struct upd_job {
+    double *T;
+    int64_t i0, i1, N, ld, r_local;
+    const double *prow, *colE;
+    double p;
+};
+static void *upd_thread(void *a) {
+    const struct upd_job *j = (const struct upd_job *)a;
+    update_rows(j->T, j->i0, j->i1, j->N, j->ld, j->prow, j->colE, j->r_local, j->p);
+    return NULL;
+}
+
+void orc_apply_update(double *T, int64_t rows, int64_t N, int64_t ld, double *d, const double *prow,
+                      const double *colE, int64_t r_local, double p, double d_e) {
+    const int nt = (rows * N >= ((int64_t)1 << 22)) ? g_threads : 1;
+    if (nt <= 1) {
+        update_rows(T, 0, rows, N, ld, prow, colE, r_local, p);
+    } else {
+        pthread_t th[64];
+        int started[64];
+        struct upd_job job[64];
+        for (int k = 0; k < nt; ++k) {
+            job[k] = (struct upd_job){T, rows * k / nt, rows * (k + 1) / nt, N, ld, r_local, prow, colE, p};
+            started[k] = pthread_create(&th[k], NULL, upd_thread, &job[k]) == 0;
+            if (!started[k]) upd_thread(&job[k]);
+        }
+        for (int k = 0; k < nt; ++k)
+            if (started[k]) pthread_join(th[k], NULL);
     }
     if (d) {
         const double f = -d_e / p;

@@ -383,8 +383,8 @@ def set_update_waves(w):
 
 
 def set_blocked(mode):
-    """New engines' tableau storage: -1 default (row-major unless SIMPLEX_BLOCKED=1), 1 the blocked
-    layout (4x4 blocks in 16-row strips), 0 row-major."""
+    """New engines' tableau storage: -1 default (the blocked layout unless SIMPLEX_BLOCKED=0), 1 the
+    blocked layout (4x4 blocks in 16-row strips), 0 row-major."""
     _lib.load().simplex_set_blocked(int(mode))
 
 
@@ -413,18 +413,6 @@ def set_verbose(on):
 def set_sweep_mfma(mode):
     """The tableau sweep on the matrix cores (1), the vector sweep (0) or auto (-1)."""
     _lib.load().simplex_set_sweep_mfma(int(mode))
-
-
-def set_sweep_lds(on):
-    """The matrix-core sweep with its strips staged through LDS by LDS-DMA (1) or loaded to
-    registers (0, default); the same results bit for bit."""
-    _lib.load().simplex_set_sweep_lds(int(on))
-
-
-def set_sweep_interleave(on):
-    """The matrix-core sweep with both tile pairs' four MFMA chains interleaved (1) or pair by pair
-    (0, default); the same results bit for bit."""
-    _lib.load().simplex_set_sweep_interleave(int(on))
 
 
 def set_batch(p):

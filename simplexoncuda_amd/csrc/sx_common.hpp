@@ -95,10 +95,7 @@ struct BatchChan {
     alignas(128) unsigned abort_w;   // a wait timed out: every block leaves
     alignas(128) unsigned inject_q;  // test hook: 1 + the slot at which ratio block 0 (of rank 0)
                                      // leaves with the batch aborted (0: off); the last block clears it
-    alignas(128) unsigned backoff;   // k_batch: adaptive poll back-off on (1) / off (0)
-    alignas(128) unsigned copies;    // k_batch: copies of every hand-off record, 1..SX_REC_COPIES
 };
-#define SX_REC_COPIES 8
 
 // Multi-rank fused batch (k_batch_mr): every rank's buffers as seen from this rank (peer
 // memory over xGMI, or the other virtual shards on one GPU).
@@ -203,6 +200,7 @@ void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, in
 // fused batch of up to k pivots on one shard (ratio tiles + objective tiles in one resident
 // grid); returns false (nothing launched) when the grid cannot be resident at once
 bool sx_batch_fits(int rows, Cols c, int k);
+int sx_batch_obj_tile_limit();  // objective tiles a one-shard fused batch holds (logical width <= 512 x this + 1)
 // d_save: the objective row as the batch found it (restored by the host after SX_HANG); the
 // basis is written only by a batch that completed
 // perm / iperm / act / nact (slack compaction, or null): the batch's last block also activates
@@ -236,8 +234,6 @@ struct MrLaunchRank {
 void sx_launch_batch_mr_multi(const MrLaunchRank *ranks, int nloc, int W, int rpr, size_t ld, TLay tl, Cols c, unsigned B,
                               int k, int slots, const PeerView &pv, unsigned long long timeout, hipStream_t s);
 void sx_set_update_waves(float w);  // resident-grid multiple of the sweep (default 1)
-void sx_set_sweep_lds(int on);      // the matrix-core sweep staged through LDS by LDS-DMA (k_msweep_lds)
-void sx_set_sweep_interleave(int on);  // the matrix-core sweep's four interleaved MFMA chains per wave
 void sx_set_sweep_record(int *rec);  // next sweeps write (batch tag, count, nact) to rec[0..2] (null: off)
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s);
 void sx_launch_l2_writeback(hipStream_t s);  // every XCD's L2 writes back its dirty lines

@@ -228,13 +228,11 @@ bool gpus_selftest(const std::vector<int> &devs);  // (below two_phase)
 int gpus_check(const std::vector<int> &devs);
 
 // the engine's own tableaux in 4x4 blocks (TLay::blk) unless SIMPLEX_BLOCKED=0 or
-// simplex_set_blocked(0)
-// (off by default until the blocked layout has run on the GPU: SIMPLEX_BLOCKED=1 or
-// simplex_set_blocked(1) opts in)
+// simplex_set_blocked(0) selects row-major storage (the layout of callers' tableaux, tabular.h)
 bool use_blocked() {
     if (g_cfg.blocked < 0) {
         const char *e = getenv("SIMPLEX_BLOCKED");
-        return e && atoi(e) != 0;
+        return !(e && atoi(e) == 0);
     }
     return g_cfg.blocked != 0;
 }
@@ -331,6 +329,7 @@ class Engine {
     unsigned batch_id = 1;  // 1 .. 2^15 - 1 (the granule tags keep 15 bits; see enqueue_sweep)
     int q_host = 0;
     bool batch_activated = false;  // the pending batch's fused kernel already activated its slack columns
+    mutable bool wide_note = false;  // the verbose note "too wide for the fused batch" was printed
     unsigned long long *stamps = nullptr;  // diagnostic: in-kernel timestamps of the fused batch
     long long sweeps = 0;
     std::function<void(int)> on_pivot;  // DEBUG trace: called after every pivot (solver.cu:112-116)
@@ -344,6 +343,7 @@ class Engine {
         ld = round_up((size_t)Ns1, 16);
         batch_id = (g_cfg.first_batch_id >= 1 && g_cfg.first_batch_id < SX_BATCH_IDS) ? g_cfg.first_batch_id : 1;
         std::vector<int> devs;  // one process, several GPUs: the device of every shard
+        int alone_dev = -1;     // a device list that failed its self-check: every solve on its first device
         if (g_cfg.single_shard) {
             // one shard on this device
         } else if (g_cfg.ipc_world > 1) {
@@ -357,7 +357,7 @@ class Engine {
                 W = (int)devs.size();
                 gpus_mode = true;
             } else {
-                g_cfg.device = devs[0];  // (the list failed its self-check: its first device alone)
+                alone_dev = devs[0];  // (the list failed its self-check: its first device alone)
             }
         } else if (g_cfg.virtual_ranks > 1) {
             W = g_cfg.virtual_ranks;
@@ -367,6 +367,8 @@ class Engine {
         int dev = 0;
         if (gpus_mode)
             SX_HIP(hipSetDevice(devs[0]));
+        else if (alone_dev >= 0)
+            SX_HIP(hipSetDevice(alone_dev));
         else if (g_cfg.device >= 0)
             SX_HIP(hipSetDevice(g_cfg.device));
         SX_HIP(hipGetDevice(&dev));
@@ -398,6 +400,14 @@ class Engine {
                 tl.ldA = (size_t)jB;
                 tl.ldB = round_up((size_t)(Ns1 - jB), 16);
                 tl.offB = (size_t)rpr * tl.ldA;  // every shard allocates rpr rows (peers index alike)
+            }
+        }
+        if (alias) {  // (experiment: SIMPLEX_LDPAD extra doubles on T's row stride)
+            const char *e = getenv("SIMPLEX_LDPAD");
+            const int pad = e ? (int)round_up((size_t)std::max(atoi(e), 0), 16) : 0;
+            if (pad > 0) {
+                tl.ldA += (size_t)pad;
+                if (tl.jB < Ns1) tl.offB = (size_t)rpr * tl.ldA;
             }
         }
         // one allgather of (tile winner, row) beats two collectives while the rows are small
@@ -657,7 +667,7 @@ class Engine {
     // doubles of a shard's tableau allocation (the blocked layout: whole 16-row strips)
     size_t t_doubles(size_t rows_alloc) const {
         if (tl.blk) rows_alloc = round_up(rows_alloc, 16);
-        return tl.jB < Ns1 ? tl.offB + (size_t)rpr * tl.ldB : rows_alloc * ld;
+        return tl.jB < Ns1 ? tl.offB + (size_t)rpr * tl.ldB : rows_alloc * tl.ldA;
     }
 
     // a free uncached record set on `dev` (allocated, after an L2 write-back, the first time)
@@ -745,16 +755,6 @@ class Engine {
         }
         if (x.gdone) SX_HIP(hipMemsetAsync(x.gdone, 0, SX_MAXW * 8, x.s));
         SX_HIP(hipMemsetAsync(x.chan, 0, sizeof(BatchChan), x.s));
-        {  // the fused batch's adaptive poll back-off (opt-in, SIMPLEX_BACKOFF=1: not yet run on the GPU)
-            const char *e = getenv("SIMPLEX_BACKOFF");
-            const unsigned bo = (e && atoi(e) != 0) ? 1u : 0u;
-            SX_HIP(hipMemcpyAsync(&x.chan->backoff, &bo, sizeof(unsigned), hipMemcpyHostToDevice, x.s));
-            // copies of every hand-off record (SIMPLEX_REC_COPIES, 1..SX_REC_COPIES)
-            const char *rc = getenv("SIMPLEX_REC_COPIES");
-            const unsigned cp = rc ? (unsigned)std::min(std::max(atoi(rc), 1), SX_REC_COPIES) : 1u;
-            SX_HIP(hipMemcpyAsync(&x.chan->copies, &cp, sizeof(unsigned), hipMemcpyHostToDevice, x.s));
-            SX_HIP(hipStreamSynchronize(x.s));
-        }
         SX_HIP(hipMemsetAsync(x.ga, 0, sx_batch_granules_a() * sizeof(unsigned long long), x.s));
         SX_HIP(hipMemsetAsync(x.gb, 0, sx_batch_granules_b() * sizeof(unsigned long long), x.s));
         x.tiles_local = dalloc<TilePart>(slots);
@@ -1159,7 +1159,14 @@ class Engine {
     // a whole batch of up to k pivots in one resident launch (one shard, no exchange)
     bool fused_ok(int k) const {
         if (g_cfg.fused == 0 || on_pivot) return false;
-        if (!xchg) return sh.size() == 1 && sx_batch_fits(sh[0].rows, cols(N), k);
+        if (!xchg) {
+            if ((N - 1 + SX_TILE - 1) / SX_TILE > sx_batch_obj_tile_limit() && g_cfg.verbose && !wide_note) {
+                wide_note = true;  // (the width limit of the one-shard fused batch)
+                fprintf(stderr, "simplex: %d objective tiles exceed the fused batch's %d (N - 1 > %d): per-pivot path\n",
+                        (N - 1 + SX_TILE - 1) / SX_TILE, sx_batch_obj_tile_limit(), sx_batch_obj_tile_limit() * SX_TILE);
+            }
+            return sh.size() == 1 && sx_batch_fits(sh[0].rows, cols(N), k);
+        }
         if (!p2p) return false;
         const int NBg = (N - 1 + SX_TILE - 1) / SX_TILE;
         const int nbl = (NBg + W - 1) / W;
@@ -1732,11 +1739,15 @@ int two_phase(problem_t *P, double *solution, double *opt, int *base_out, long l
 // mid-batch -- as before).  Returns 2 when both multi-shard paths give the one-shard answer bit for
 // bit (and the fused path ran without a hand-off timing out), 1 when only the per-pivot exchange
 // does, 0 when the per-pivot exchange does not either (the shards must not be used: one device).
-int selftest_solves(int W) {
+// ref_dev: the device of the one-shard reference solve (-1: the current one; a SIMPLEX_GPUS list: its
+// first device).  With peer-memory batches switched off (simplex_set_p2p(0)) only the per-pivot
+// exchange is checked (2 solves instead of 4).
+int selftest_solves(int W, int ref_dev) {
     const int sm = W > 2 ? 512 * W : 1100;
     problem_t *P = generateRandomProblem(300, sm, 300 * 100 + sm, 1, 100);
     const int n = P->vars, m = P->constraints;
-    const int save = g_cfg.p2p, save_batch = g_cfg.batch;
+    const int save = g_cfg.p2p, save_batch = g_cfg.batch, save_dev = g_cfg.device;
+    const bool check_p2p = g_cfg.p2p != 0;
     const bool save_nt = g_cfg.no_timer, save_single = g_cfg.single_shard;
     g_cfg.no_timer = true;  // (timing would switch the solves to the per-pivot path; no CSVs either)
     struct Answer {
@@ -1761,11 +1772,20 @@ int selftest_solves(int W) {
                std::memcmp(a.x.data(), b.x.data(), sizeof(double) * n) == 0;
     };
     const long long fb0 = g_cfg.fused_batches, hr0 = g_cfg.hang_recoveries;
-    const Answer a32 = solve(1, SX_HMAX), a64 = solve(1, SX_KMAX);
-    const bool went_fused = g_cfg.fused_batches > fb0 && g_cfg.hang_recoveries == hr0;
+    Answer a32, a64;
+    if (check_p2p) {
+        a32 = solve(1, SX_HMAX);
+        a64 = solve(1, SX_KMAX);
+    }
+    const bool went_fused = check_p2p && g_cfg.fused_batches > fb0 && g_cfg.hang_recoveries == hr0;
     const Answer xch = solve(0, 0);
-    g_cfg.single_shard = true;  // the reference: one shard of this device
+    g_cfg.single_shard = true;  // the reference: one shard of the reference device
+    int cur_dev = 0;
+    SX_HIP(hipGetDevice(&cur_dev));
+    if (ref_dev >= 0) g_cfg.device = ref_dev;
     const Answer one = solve(-1, 0);
+    g_cfg.device = save_dev;
+    SX_HIP(hipSetDevice(cur_dev));
     g_cfg.single_shard = save_single;
     g_cfg.p2p = save;
     g_cfg.batch = save_batch;
@@ -1783,7 +1803,7 @@ int gpus_check(const std::vector<int> &devs) {
     auto it = g_cfg.gpus_checked.find(devs);
     if (it != g_cfg.gpus_checked.end()) return it->second;
     g_cfg.gpus_checked[devs] = -1;  // (the check's own engines run the list)
-    const int code = selftest_solves((int)devs.size());
+    const int code = selftest_solves((int)devs.size(), devs[0]);
     g_cfg.gpus_checked[devs] = code;
     if (code == 1)
         fprintf(stderr, "simplex: peer-memory fused batches disagree with the one-shard answer on these GPUs; "
@@ -1861,8 +1881,6 @@ long long simplex_hang_recoveries(void) { return g_cfg.hang_recoveries; }
 long long simplex_fused_batches(void) { return g_cfg.fused_batches; }
 void simplex_set_fine_pivot_rows(int mode) { g_cfg.fine_u = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_blocked(int mode) { g_cfg.blocked = mode < 0 ? -1 : (mode ? 1 : 0); }
-void simplex_set_sweep_lds(int on) { sx_set_sweep_lds(on); }
-void simplex_set_sweep_interleave(int on) { sx_set_sweep_interleave(on); }
 void simplex_set_first_batch_id(unsigned int id) { g_cfg.first_batch_id = (id >= 1 && id < SX_BATCH_IDS) ? id : 1; }
 
 void enableBenchmarkMode(void) { g_cfg.benchmark = true; }
@@ -1883,7 +1901,7 @@ int simplex_dist_get_unique_id(unsigned char *out) {
 static void p2p_selftest() {
     g_cfg.p2p_ready = false;
     g_cfg.single_shard = false;
-    int code = selftest_solves(g_cfg.world);
+    int code = selftest_solves(g_cfg.world, -1);
     int *dv = nullptr;
     SX_HIP(hipMalloc(reinterpret_cast<void **>(&dv), sizeof(int)));
     SX_HIP(hipMemcpy(dv, &code, sizeof(int), hipMemcpyHostToDevice));
@@ -2272,17 +2290,21 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     sx_crt_seeds(seed, 0, sd);
     TLay btl;  // one region, the engine's storage (row-major, or 4x4 blocks in whole 16-row strips)
     btl.ldA = ld;
+    {  // (experiment: SIMPLEX_LDPAD extra doubles on T's row stride)
+        const char *e = getenv("SIMPLEX_LDPAD");
+        if (e) btl.ldA += round_up((size_t)std::max(atoi(e), 0), 16);
+    }
     btl.jB = cols;
     btl.blk = use_blocked() ? 1 : 0;
     const size_t rows_alloc = btl.blk ? round_up((size_t)rows, 16) : (size_t)rows;
-    double *T = dalloc<double>(rows_alloc * ld);
+    double *T = dalloc<double>(rows_alloc * btl.ldA);
     double *U = dalloc<double>((size_t)SX_KMAX * ld);
     double *F = dalloc<double>(round_up((size_t)rows, 16) * SX_KMAX);
     PivRec *recs = dalloc<PivRec>(SX_KMAX);
     unsigned long long *PM = dalloc<unsigned long long>(rows);
     unsigned long long *PM2 = dalloc<unsigned long long>(rows);
     DevState *st = dalloc<DevState>(1);
-    SX_HIP(hipMemsetAsync(T, 0, sizeof(double) * rows_alloc * ld, s));
+    SX_HIP(hipMemsetAsync(T, 0, sizeof(double) * rows_alloc * btl.ldA, s));
     // column 0 = b (first CRT seed), columns 1.. = A's rows (third), as generateRandomProblem
     double *b_dev = dalloc<double>(rows);
     sx_launch_gen_vector(sd[0], 0, rows, lo, hi, b_dev, s);
@@ -2296,10 +2318,12 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     const unsigned B = 1;
     std::vector<PivRec> rc(SX_KMAX);
     std::vector<unsigned long long> pm((size_t)rows, 0ull), pm2((size_t)rows, 0ull);
+    const bool noleave = getenv("SIMPLEX_BENCH_NOLEAVE") != nullptr;  // (experiment: no leaving rows)
     for (int k = 0; k < SX_KMAX; ++k) {
         rc[k].r = (int)(((long long)k * rows) / pivots % rows);
         rc[k].e = k;
         rc[k].p = 1.0 + (double)(k % 97);
+        if (noleave) continue;
         if (k < pivots && k < SX_HMAX) pm[(size_t)rc[k].r] = ((unsigned long long)B << 32) | (1ull << k);
         if (k < pivots && k >= SX_HMAX) pm2[(size_t)rc[k].r] = ((unsigned long long)B << 32) | (1ull << (k - SX_HMAX));
     }

@@ -726,14 +726,11 @@ __device__ __forceinline__ void poll_pause() { __builtin_amdgcn_s_sleep(1); }
 // barrier per poll; payf(k, payload) is called for every granule as it arrives.  Wave-uniform
 // result: false when the batch was aborted (or this wait timed out, which aborts it).  Only wave 0
 // may call it.
-// presleep (100 MHz ticks): the wave first sleeps that long -- a consumer that knows its records
-// cannot land sooner keeps its polls off the memory system meanwhile.
 template <typename OFF, bool SYS, int PL, typename PAYF>
 __device__ __forceinline__ int poll_wave_f(const u64 *base, int n, OFF off, unsigned tag, unsigned *out, unsigned *abort_w,
-                           unsigned long long timeout, PAYF payf, unsigned presleep = 0u) {
+                           unsigned long long timeout, PAYF payf) {
     const int t = threadIdx.x;
     const u64 t0 = __builtin_amdgcn_s_memrealtime();
-    while (presleep && __builtin_amdgcn_s_memrealtime() - t0 < presleep) __builtin_amdgcn_s_sleep(8);
     if (n <= 64) {
         bool have = t >= n;
         for (unsigned it = 0;; ++it) {
@@ -792,22 +789,11 @@ __device__ __forceinline__ int poll_wave_f(const u64 *base, int n, OFF off, unsi
 // granules come in pairs), or dropped (pay null).
 template <typename OFF, bool SYS = false>
 __device__ int poll_wave(const u64 *base, int n, OFF off, unsigned tag, unsigned *out, unsigned *abort_w,
-                         unsigned long long timeout, unsigned *pay, unsigned presleep = 0u) {
+                         unsigned long long timeout, unsigned *pay) {
     return poll_wave_f<OFF, SYS, SX_GATHER_PER_LANE>(base, n, off, tag, out, abort_w, timeout,
                                                      [pay](int k, unsigned pl) {
                                                          if (pay && !(k & 1)) pay[k >> 1] = pl;
-                                                     },
-                                                     presleep);
-}
-
-// Adaptive poll back-off of a fused batch's waits: sleep for the previous pivot's wait less a
-// margin (SX_BACKOFF_MARGIN ticks of 10 ns), at most SX_BACKOFF_MAX; updated from each wait.
-#define SX_BACKOFF_MARGIN 120u
-#define SX_BACKOFF_MAX 800u
-__device__ __forceinline__ unsigned next_backoff(unsigned long long waited) {
-    if (waited <= SX_BACKOFF_MARGIN) return 0u;
-    const unsigned long long b = waited - SX_BACKOFF_MARGIN;
-    return b > SX_BACKOFF_MAX ? SX_BACKOFF_MAX : (unsigned)b;
+                                                     });
 }
 
 // Pass 2 of the reference's argmin (deviceReduceKernel<false><<<1,1024>>>, reduction.cu:239-241)
@@ -1310,13 +1296,6 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
     int status = SX_NOT_ENDED, cnt = 0;
     bool aborted = false;
     const unsigned inj = ch->inject_q;  // (test hook, normally 0)
-    const bool backoff = ch->backoff != 0u;
-    // copies of every record (SIMPLEX_REC_COPIES): a producer writes each of its records into
-    // all of them, a block polls copy blockIdx % copies -- one per XCD at 8, since workgroups
-    // are dispatched to the XCDs round-robin
-    const int rcn = ch->copies < 1u ? 1 : ch->copies > SX_REC_COPIES ? SX_REC_COPIES : (int)ch->copies;
-    u64 *const gam = ga + (size_t)(blockIdx.x % rcn) * sx_ga_size();
-    u64 *const gbm = gb + (size_t)(blockIdx.x % rcn) * sx_gb_size();
     if (status0 == SX_NOT_ENDED) {
         // ratio block: its row; objective block: its logical column d[1 + ia]
         const int li = blockIdx.x * SX_TILE + t;
@@ -1368,7 +1347,6 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
             // of the current stage; wu1: U[s][e] of the first stage), loaded by every wave with the
             // column's stored values (the fresh slot from the objective record)
             double wu = 0.0, wu1 = 0.0;
-            unsigned pre_c = 0u;  // (wave 0) back-off before polling the objective records
             for (int q = 0; q < K; ++q) {
                 const unsigned tag = make_tag(B, q);
                 if (cap >= 0 && piv0 + q >= cap) {
@@ -1443,9 +1421,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                             const u64 bits64 = (u64)__double_as_longlong(val);
                             data = (k & 1) ? (unsigned)(bits64 >> 32) : (unsigned)bits64;
                         }
-                        for (int c = 0; c < rcn; ++c)
-                            put_g(ga + c * sx_ga_size() + (size_t)blockIdx.x * SX_GA_STRIDE + k, data,
-                                  k < kRD ? (tag | pl) : tag);
+                        put_g(ga + (size_t)blockIdx.x * SX_GA_STRIDE + k, data, k < kRD ? (tag | pl) : tag);
                     }
                 }
                 if (blockIdx.x == 0) SX_STAMP(1);
@@ -1458,14 +1434,14 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 // the objective blocks run, reduction.cu:116-140, and takes p and the RHS from the
                 // winner's record): the objective side answers much later, so this is off the chain
                 if (t < 64) {
-                    int ok = poll_wave(gam, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
+                    int ok = poll_wave(ga, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
                     double tv = DBL_MAX;
                     int ti = -1, any = 0;
                     if (ok) wave_pass2(s_g, s_pay, NA, s_v, s_i, tv, ti, any);
                     ti = __builtin_amdgcn_readfirstlane(ti);
                     if (ok && ti >= 0) {
                         const int wt = ti / SX_TILE;
-                        ok = poll_wave(gam + (size_t)wt * SX_GA_STRIDE + kRA, 4, IdOff(), tag, s_g + 2048 - 64,
+                        ok = poll_wave(ga + (size_t)wt * SX_GA_STRIDE + kRA, 4, IdOff(), tag, s_g + 2048 - 64,
                                        &ch->abort_w, 20000000ull, (unsigned *)nullptr);
                     }
                     if (t == 0) {
@@ -1525,14 +1501,11 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 // winner's record (wave 0 polls; one block barrier)
                 if (t < 64) {
                     unsigned short *po = s_payo;
-                    const u64 ta = __builtin_amdgcn_s_memrealtime();
                     const int ok = poll_wave_f<Rec4All, false, SX_OBJ_PER_LANE>(
-                        gbm, SX_GB4 * NB, Rec4All(), tag, s_g, &ch->abort_w, 20000000ull,
+                        gb, SX_GB4 * NB, Rec4All(), tag, s_g, &ch->abort_w, 20000000ull,
                         [po](int k, unsigned pl) {
                             if ((k & 3) < 3) po[(k & 3) * SX_OBJ_TILES + (k >> 2)] = (unsigned short)pl;
-                        },
-                        pre_c);
-                    if (backoff) pre_c = next_backoff(__builtin_amdgcn_s_memrealtime() - ta);
+                        });
                     double ev = DBL_MAX;
                     int ei = -1, any = 0;
                     if (ok) wave_pass2<SX_GB4, unsigned short>(s_g, s_payo, NB, s_v, s_i, ev, ei, any);
@@ -1572,7 +1545,6 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 }
             }
         } else {
-            unsigned pre_a = 0u;  // (wave 0) back-off before polling the ratio records
             for (int q = 0; q < K; ++q) {
                 const unsigned tag = make_tag(B, q);
                 if (cap >= 0 && piv0 + q >= cap) {
@@ -1583,9 +1555,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 const int qq = q - hb;  // slot within the stage
                 // ---- selection: pass 2 over the ratio tiles (wave 0 polls and runs the tree)
                 if (t < 64) {
-                    const u64 ta = __builtin_amdgcn_s_memrealtime();
-                    const int ok = poll_wave(gam, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, 20000000ull, s_pay, pre_a);
-                    if (backoff) pre_a = next_backoff(__builtin_amdgcn_s_memrealtime() - ta);
+                    const int ok = poll_wave(ga, 2 * NA, rec2_a, tag, s_g, &ch->abort_w, 20000000ull, s_pay);
                     double tv = DBL_MAX;
                     int ti = -1, any = 0;
                     if (ok) wave_pass2(s_g, s_pay, NA, s_v, s_i, tv, ti, any);
@@ -1614,7 +1584,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     u64 fr1 = 0ull;
                     if (hb && t < SX_HMAX)
                         fr1 = ld_sc1(reinterpret_cast<const u64 *>(F + sx_fidx(r >= 0 ? r : 0, t)));
-                    const int ok = poll_wave(gam + (size_t)wt * SX_GA_STRIDE + kRD, (kRF - kRD) + 2 * qq,
+                    const int ok = poll_wave(ga + (size_t)wt * SX_GA_STRIDE + kRD, (kRF - kRD) + 2 * qq,
                                              [](int k) { return k; }, tag, s_g, &ch->abort_w, 20000000ull,
                                              (unsigned *)nullptr);
                     if (hb && t < SX_HMAX) s_fr1[t] = __longlong_as_double((long long)fr1);
@@ -1694,8 +1664,8 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     // the record: the winner's d value (payload: its index in the tile) and its pivot-row
                     // value of this pivot U[q][w] (the ratio side's newest pending entry of the entering
                     // column if w enters), the winner's stored column in the payloads of granules 1, 2
-                    if (t < SX_GB4 * rcn) {
-                        const int k = t & (SX_GB4 - 1), c = t / SX_GB4;
+                    if (t < SX_GB4) {
+                        const int k = t;
                         const int mw = reinterpret_cast<const int *>(s_a)[win];
                         const double val = k < 2 ? wv : s_hist[qq * SX_TILE + win];
                         const u64 bits64 = (u64)__double_as_longlong(val);
@@ -1703,7 +1673,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                         const unsigned pl = k == 0 ? (wi >= 0 ? (unsigned)win : SX_NOIDX)
                                           : k == 1 ? ((unsigned)mw & SX_PAYMASK)
                                           : k == 2 ? (((unsigned)mw >> SX_PAYBITS) & SX_PAYMASK) : 0u;
-                        put_g(gb + c * sx_gb_size() + (size_t)tb * SX_GBS + k, data, tag | pl);
+                        put_g(gb + (size_t)tb * SX_GBS + k, data, tag | pl);
                     }
                 }
                 // the pivot row into U[q] (the sweep's input, and the ratio side's pending entries of
@@ -1723,7 +1693,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
         if (!isA && !aborted && (status == SX_NOT_ENDED || status == SX_PIVOT_CAP) && cnt > 0) {
             const unsigned tag = make_tag(B, cnt - 1);
             if (t < 64) {
-                const int ok = poll_wave(gbm, 2 * NB, Rec4Val(), tag, s_g, &ch->abort_w, 20000000ull, s_pay);
+                const int ok = poll_wave(gb, 2 * NB, Rec4Val(), tag, s_g, &ch->abort_w, 20000000ull, s_pay);
                 double ev = DBL_MAX;
                 int ei = -1, any = 0;
                 if (ok) wave_pass2(s_g, s_pay, NB, s_v, s_i, ev, ei, any);
@@ -2495,8 +2465,8 @@ __global__ __launch_bounds__(256) void k_sweep(double *T, int rows, size_t ld, T
     }
 }
 
-// A strip's matrix steps (k_msweep, k_msweep_lds): acc[p][0] / acc[p][1] = tile X / Y of pair p; all
-// four chains advance one 4-slot step at a time (each element's fmas stay in slot order)
+// A strip's matrix steps (k_msweep): acc[p][0] / acc[p][1] = tile X / Y of pair p; all four chains
+// advance one 4-slot step at a time (each element's fmas stay in slot order)
 template <int NKB>
 __device__ __forceinline__ void msweep_steps(d4_t (&acc)[2][2], const double (&ff)[NKB], const double2 (&uf)[NKB][2],
                                              int nkb) {
@@ -2549,7 +2519,7 @@ __device__ __forceinline__ void msweep_store(const d4_t (&acc)[2][2], __amdgpu_b
     }
 }
 
-// The rows that left the basis in a batch (k_msweep, k_msweep_lds): row r_s (first slot s where
+// The rows that left the basis in a batch (k_msweep): row r_s (first slot s where
 // it left) by the row slot s % G, one column per lane, the guarded chain from its stored values
 // (the strips left them unwritten).  The row slot's rows are found in one round trip (lane k:
 // slot gy + G k), and each row's operands -- its stored values, the column's pivot-row values (32
@@ -2661,10 +2631,11 @@ __device__ __forceinline__ void msweep_fixup(const double *Tr, double *Tw, size_
 // Grid, column order, regions, compaction and cache policy as k_sweep (POL 1), with 256-column
 // tiles.  In place (Tsrc == Tdst: the strips read through one pointer and write through the other).
 // NKB: 4-slot steps held (SX_HMAX / 4: one stage, 3 waves per SIMD; SX_KMAX / 4: two stages,
-// 2 waves per SIMD).  ILV (opt-in, SIMPLEX_SWEEP_ILV=1, not yet run on the GPU): both pairs' four
-// accumulators advance together (msweep_steps) instead of pair 0's two chains, its stores, then
-// pair 1's -- the same fmas per element in the same order.
-template <int NKB, bool ILV>
+// 2 waves per SIMD).  Both pairs' four accumulators advance one 4-slot step at a time (msweep_steps):
+// four independent MFMA chains per wave, eight per SIMD -- the f64 probe needs about eight to keep
+// the matrix pipe busy.  Pair by pair (two chains per wave) measured 2.5 % slower
+// at config 5, same box (profiles/r05_variants_ab.txt).
+template <int NKB>
 __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *Tdst, int rows, int row0, size_t ld,
                                                    TLay tl, int Ns, const int *__restrict__ nact, int s0,
                                                    const double *__restrict__ F, const double *__restrict__ U,
@@ -2742,8 +2713,8 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
             const int fr = r0 + jl;  // the A-operand row of this lane
             const __amdgpu_buffer_rsrc_t rss = strip_rsrc(Tw, r0);
             // issue order: both pairs' tableau tiles, the strip's factors, its leaving-row bits --
-            // one memory round trip per strip (the bits are only needed after the first pair's
-            // matrix steps, and the counter waits are in issue order)
+            // one memory round trip per strip (the bits are only needed after the matrix steps,
+            // and the counter waits are in issue order)
             double2 cx[2][4];
             load_tiles(cx, r0);
             double ff[NKB];
@@ -2759,273 +2730,32 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb)
                 if (4 * kb + rg >= cnt) ff[kb] = -0.0;
-            if constexpr (ILV) {
-                // both pairs' four accumulators advance together: four independent MFMA chains per
-                // wave (two chains at a time leave the matrix pipe waiting on each step's result)
-                d4_t acc[2][2];
+            // both pairs' four accumulators advance together: four independent MFMA chains per
+            // wave (two chains at a time leave the matrix pipe waiting on each step's result)
+            d4_t acc[2][2];
 #pragma unroll
-                for (int p = 0; p < 2; ++p) {
-                    acc[p][0] = d4_t{cx[p][0].x, cx[p][1].x, cx[p][2].x, cx[p][3].x};
-                    acc[p][1] = d4_t{cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
-                }
-                msweep_steps<NKB>(acc, ff, uf, nkb);
-                // row fr's slots as a leaving row (both stages); bit v of skip: row r0 + rg + 4v
-                // leaves (not stored here)
-                unsigned skip = 0u;
-                {
-                    const unsigned lb = fr < rows ? ((((unsigned)(pm1 >> 32) == B) ? ((unsigned)pm1 & mask) : 0u) |
-                                                     (((unsigned)(pm2 >> 32) == B) ? ((unsigned)pm2 & mask2) : 0u))
-                                                  : 0u;
-                    if (__ballot(lb != 0u) != 0ull)
-#pragma unroll
-                        for (int v = 0; v < 4; ++v)
-                            if (__shfl(lb, rg + 4 * v) != 0u) skip |= 1u << v;  // (lane rg + 4v: that row's bits)
-                }
-                msweep_store(acc, rss, c0, jl, Ns, skip, tile_off);
-            } else {
-                bool fix = false;
-                unsigned skip = 0u;  // bit v: row r0 + rg + 4v is a leaving row (not stored here)
-#pragma unroll
-                for (int p = 0; p < 2; ++p) {
-                    const int j = c0 + 32 * p + 2 * jl;
-                    d4_t ax = {cx[p][0].x, cx[p][1].x, cx[p][2].x, cx[p][3].x};
-                    d4_t ay = {cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
-                    if (nkb == NKB) {
-#pragma unroll
-                        for (int kb = 0; kb < NKB; ++kb) {
-                            ax = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].x, ax, 0, 0, 0);
-                            ay = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].y, ay, 0, 0, 0);
-                        }
-                    } else {
-#pragma unroll
-                        for (int kb = 0; kb < NKB; ++kb)
-                            if (kb < nkb) {
-                                ax = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].x, ax, 0, 0, 0);
-                                ay = __builtin_amdgcn_mfma_f64_16x16x4f64(ff[kb], uf[kb][p].y, ay, 0, 0, 0);
-                            }
-                    }
-                    if (p == 0) {
-                        // row fr's slots as a leaving row (both stages)
-                        const unsigned lb = fr < rows ? ((((unsigned)(pm1 >> 32) == B) ? ((unsigned)pm1 & mask) : 0u) |
-                                                         (((unsigned)(pm2 >> 32) == B) ? ((unsigned)pm2 & mask2) : 0u))
-                                                      : 0u;
-                        fix = __ballot(lb != 0u) != 0ull;
-                        if (fix)
-#pragma unroll
-                            for (int v = 0; v < 4; ++v)
-                                if (__shfl(lb, rg + 4 * v) != 0u) skip |= 1u << v;  // (lane rg + 4v: that row's bits)
-                    }
-                    const bool pair = j + 1 < Ns;
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) {
-                        const int off = tile_off(p, v);
-                        const bool keep = j < Ns && !((skip >> v) & 1u);
-                        if (pair) {
-                            const double2 y = make_double2(ax[v], ay[v]);
-                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y), rss, keep ? off : OOB, 0,
-                                                                   16);
-                        } else {
-                            // (built from the 64-bit integer: a bit_cast of ax[v] straight to u32x2 compiled
-                            // to a store of ax[0] for every v -- ROCm 7.2 clang, checked in the ISA)
-                            const unsigned long long xb = (unsigned long long)__double_as_longlong(ax[v]);
-                            const u32x2 w = {(unsigned)xb, (unsigned)(xb >> 32)};
-                            __builtin_amdgcn_raw_buffer_store_b64(w, rss, keep ? off : OOB, 0, 16);
-                        }
-                    }
-                }
+            for (int p = 0; p < 2; ++p) {
+                acc[p][0] = d4_t{cx[p][0].x, cx[p][1].x, cx[p][2].x, cx[p][3].x};
+                acc[p][1] = d4_t{cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
             }
+            msweep_steps<NKB>(acc, ff, uf, nkb);
+            // row fr's slots as a leaving row (both stages); bit v of skip: row r0 + rg + 4v
+            // leaves (not stored here)
+            unsigned skip = 0u;
+            {
+                const unsigned lb = fr < rows ? ((((unsigned)(pm1 >> 32) == B) ? ((unsigned)pm1 & mask) : 0u) |
+                                                 (((unsigned)(pm2 >> 32) == B) ? ((unsigned)pm2 & mask2) : 0u))
+                                              : 0u;
+                if (__ballot(lb != 0u) != 0ull)
+#pragma unroll
+                    for (int v = 0; v < 4; ++v)
+                        if (__shfl(lb, rg + 4 * v) != 0u) skip |= 1u << v;  // (lane rg + 4v: that row's bits)
+            }
+            msweep_store(acc, rss, c0, jl, Ns, skip, tile_off);
         }
     }
     if (cnt <= 0) return;
     msweep_fixup<NKB>(Tr, Tw, ldr, cr, c0, Ns, rows, row0, tl, gy, G, cnt, F, U, ld, recs, PM, PM2, B, mask, mask2);
-}
-
-// K5'' (option, simplex_set_sweep_lds): k_msweep with each strip's tableau tiles and factors
-// staged through LDS by LDS-DMA (buffer_load ... lds), one strip ahead: a block's 4 waves walk the
-// same strips, so a strip's factors (SX_KMAX / 4 steps x 64 lanes) are loaded once per block, a
-// quarter by each wave, and each wave loads its own tiles -- 8 KB, one 1-KB LDS-DMA instruction per
-// (pair, row group) fragment, placed lane-linear so every fragment read is one conflict-free
-// ds_read_b128.  Per strip: wait for this strip's DMA (the stores of the previous strip may stay
-// in flight: vmcnt counts loads, stores and LDS-DMA together, in issue order), one block barrier,
-// issue the next strip's DMA into the other buffer, then the matrix steps as k_msweep.  No
-// VGPR-destination global load is issued inside the strip loop (the leaving rows of the batch
-// come from recs, one register per lane), so nothing makes the compiler drain the DMA early.
-// Same operations in the same order as k_msweep: bit-identical results.
-// one LDS-DMA instruction: 16 bytes per lane from the buffer (rs: wave-uniform descriptor) at byte
-// voff into LDS at byte lds + 16 * lane.  Inline asm, so that hipcc ties none of its own waits to
-// it (the builtin made it wait vmcnt(0) before every LDS read of the staged tiles, draining the
-// next strip's DMA): the kernel waits for these loads itself, with counted vmcnt.
-template <bool NT>
-__device__ __forceinline__ void lds_dma16(u32x4 rs, unsigned lds, int voff) {
-    unsigned keep;
-    lds = __builtin_amdgcn_readfirstlane(lds);
-    if constexpr (NT)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds\n\t"
-                     "s_mov_b32 m0, %0"
-                     : "=&s"(keep)
-                     : "v"(voff), "s"(rs), "s"(lds)
-                     : "memory");
-    else
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-                     "s_mov_b32 m0, %0"
-                     : "=&s"(keep)
-                     : "v"(voff), "s"(rs), "s"(lds)
-                     : "memory");
-}
-// a raw buffer descriptor (as __builtin_amdgcn_make_buffer_rsrc(p, 0, bytes, 0x00020000)) in
-// scalar registers
-__device__ __forceinline__ u32x4 sgpr_rsrc(const void *p, unsigned bytes) {
-    const unsigned long long a = (unsigned long long)p;
-    u32x4 r;
-    r.x = __builtin_amdgcn_readfirstlane((unsigned)a);
-    r.y = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32) & 0xffffu);
-    r.z = __builtin_amdgcn_readfirstlane(bytes);
-    r.w = 0x00020000u;
-    return r;
-}
-
-template <int NKB>
-__global__ __launch_bounds__(256, 2) void k_msweep_lds(double *T, int rows, int row0, size_t ld, TLay tl, int Ns,
-                                                       const int *__restrict__ nact, int s0,
-                                                       const double *__restrict__ F, const double *__restrict__ U,
-                                                       const PivRec *__restrict__ recs,
-                                                       const unsigned long long *__restrict__ PM,
-                                                       const unsigned long long *__restrict__ PM2,
-                                                       const DevState *__restrict__ st, unsigned B, int rev,
-                                                       int *__restrict__ rec) {
-    constexpr int FBY = NKB * 64 * 8;  // a strip's factors, bytes
-    constexpr int TBY = 8 * 1024;      // a wave's tiles of a strip, bytes
-    constexpr int BUF = 4 * TBY + FBY; // one stage buffer of the block
-    constexpr int NF = FBY / 4 / 1024; // factor DMA instructions per wave
-    __shared__ __attribute__((aligned(16))) char s_buf[2 * BUF];
-    sweep_record(rec, st, nact);
-    const int cnt = st->batch_tag == B ? st->batch_count : 0;
-    if (cnt <= 0) return;
-    if (nact && s0 + *nact < Ns) Ns = s0 + *nact;
-    const int cb = (Ns + 255) / 256;
-    const int lin = (int)(blockIdx.y * gridDim.x + blockIdx.x);
-    const int G = (int)(gridDim.x * gridDim.y) / cb;
-    const int tile = lin % cb, gy = lin / cb;
-    if (gy >= G) return;
-    const int bx = rev ? cb - 1 - tile : tile;
-    const int l = (int)threadIdx.x & 63, jl = l & 15, rg = l >> 4, wv = (int)threadIdx.x >> 6;
-    const int c0 = (bx * 4 + wv) * 64;  // the wave's first column
-    const bool act = c0 < Ns;           // (a wave past the last column still loads its share of the factors)
-    const bool inB = bx * 256 >= tl.jB;
-    double *const Tb = inB ? T + tl.offB : T;
-    const size_t ldr = inB ? tl.ldB : tl.ldA;
-    const int cr = inB ? c0 - tl.jB : c0;
-    const unsigned mask = slot_mask(cnt);
-    const unsigned mask2 = cnt > SX_HMAX ? slot_mask(cnt - SX_HMAX) : 0u;
-    const int nkb = (cnt + 3) >> 2;
-    const int OOB = 0x7fffffff;
-    const int nstrip = (rows + 15) >> 4;
-    const int niter = gy < nstrip ? (nstrip - 1 - gy) / G + 1 : 0;
-    auto strip_r0 = [&](int it) {
-        const int g = gy + it * G;
-        return (rev ? nstrip - 1 - g : g) * 16;
-    };
-    auto strip_rsrc = [&](const double *base, int r0) {
-        const int nr = tl.blk ? 16 : (rows - r0 < 16 ? rows - r0 : 16);
-        return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(base) + (size_t)r0 * ldr, 0,
-                                                 (int)((size_t)nr * ldr * 8), 0x00020000);
-    };
-    auto tile_off = [&](int p, int v) {
-        const int jr = cr + 32 * p + 2 * jl;
-        return tl.blk ? (int)((size_t)((jr >> 2) * 64 + v * 16 + rg * 4 + (jr & 3)) * 8)
-                      : (int)(((size_t)(rg + 4 * v) * ldr + jr) * 8);
-    };
-    // (LDS byte address of the staging buffers; the wave index as a scalar)
-    const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) char *)s_buf;
-    const int wvu = __builtin_amdgcn_readfirstlane(wv);
-    auto issue = [&](int it) {
-        const unsigned bf = lds0 + (unsigned)((it & 1) * BUF);
-        const int r0 = strip_r0(it);
-        if (act) {
-            const int nr = tl.blk ? 16 : (rows - r0 < 16 ? rows - r0 : 16);
-            const u32x4 rsl = sgpr_rsrc(Tb + (size_t)r0 * ldr, (unsigned)((size_t)nr * ldr * 8));
-#pragma unroll
-            for (int p = 0; p < 2; ++p)
-#pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    const int j = c0 + 32 * p + 2 * jl;
-                    lds_dma16<true>(rsl, bf + (unsigned)(wvu * TBY + (p * 4 + v) * 1024), j < Ns ? tile_off(p, v) : OOB);
-                }
-        }
-        // (the strip's factors: sx_fidx keeps a strip's 64 slots x 16 rows contiguous)
-        const u32x4 rsf = sgpr_rsrc(F + sx_fidx(r0, 0), (unsigned)FBY);
-#pragma unroll
-        for (int n = 0; n < NF; ++n) {
-            const int off = (wvu * NF + n) * 1024;
-            lds_dma16<false>(rsf, bf + (unsigned)(4 * TBY + off), off + l * 16);
-        }
-    };
-    // the lane's columns: c0 + 32p + 2jl and the next, p = 0, 1
-    double2 uf[NKB][2];
-#pragma unroll
-    for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            const int sl = 4 * kb + rg, j = c0 + 32 * p + 2 * jl;
-            uf[kb][p] = (act && sl < cnt && j < Ns) ? *reinterpret_cast<const double2 *>(U + (size_t)sl * ld + j)
-                                                    : make_double2(0.0, 0.0);
-        }
-    // lane s: the shard row that left at slot s (-1: none, or another shard's)
-    int lrow = -1;
-    if (l < cnt) {
-        const int r = recs[l].r - row0;
-        lrow = r >= 0 && r < rows ? r : -1;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (nothing of the above outstanding behind the DMA)
-    if (niter > 0) issue(0);
-    for (int it = 0; it < niter; ++it) {
-        // this strip's DMA done (younger: the previous strip's stores, at least 8 instructions)
-        if (act && it > 0)
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // (every wave's share of the factors has landed; the other buffer is free)
-        asm volatile("" ::: "memory");  // (no LDS read moves above the barrier)
-        if (it + 1 < niter) issue(it + 1);
-        const char *const bf = s_buf + (it & 1) * BUF;
-        double ff[NKB];
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) {
-            ff[kb] = *reinterpret_cast<const double *>(bf + 4 * TBY + kb * 512 + l * 8);
-            if (4 * kb + rg >= cnt) ff[kb] = -0.0;
-        }
-        if (!act) continue;
-        const int r0 = strip_r0(it);
-        double2 cx[2][4];
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-#pragma unroll
-            for (int v = 0; v < 4; ++v)
-                cx[p][v] = *reinterpret_cast<const double2 *>(bf + wv * TBY + (p * 4 + v) * 1024 + l * 16);
-        // the strip's leaving rows (not stored here: bit v of skip, row r0 + rg + 4v)
-        unsigned skip = 0u;
-        const unsigned long long hit = __ballot(lrow >= r0 && lrow < r0 + 16);
-        if (hit) {
-            unsigned m16 = 0u;
-            for (unsigned long long h = hit; h; h &= h - 1ull)
-                m16 |= 1u << (__builtin_amdgcn_readlane(lrow, (int)__builtin_ctzll(h)) - r0);
-#pragma unroll
-            for (int v = 0; v < 4; ++v)
-                if ((m16 >> (rg + 4 * v)) & 1u) skip |= 1u << v;
-        }
-        const __amdgpu_buffer_rsrc_t rss = strip_rsrc(Tb, r0);
-        d4_t acc[2][2];
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            acc[p][0] = d4_t{cx[p][0].x, cx[p][1].x, cx[p][2].x, cx[p][3].x};
-            acc[p][1] = d4_t{cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
-        }
-        msweep_steps<NKB>(acc, ff, uf, nkb);
-        msweep_store(acc, rss, c0, jl, Ns, skip, tile_off);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!act) return;
-    msweep_fixup<NKB>(Tb, Tb, ldr, cr, c0, Ns, rows, row0, tl, gy, G, cnt, F, U, ld, recs, PM, PM2, B, mask, mask2);
 }
 
 // Slack compaction (sx_common.hpp Cols), between a batch's selections and its
@@ -3393,19 +3123,6 @@ static void launch_sweep_k(double *T, int rows, size_t ld, TLay tl, int Ns, cons
 // 32768 rows); the two-stage kernel with twice its resident grid when each block would walk 64
 // strips or more (32768 x 9216: 974 vs 1006 us; at 4096 rows the resident grid stays best).  An
 // explicit simplex_set_update_waves overrides both.
-// the matrix-core sweep with LDS-DMA staging (k_msweep_lds): SIMPLEX_SWEEP_LDS=1 or sx_set_sweep_lds
-static int g_sweep_lds = [] {
-    const char *e = getenv("SIMPLEX_SWEEP_LDS");
-    return e && atoi(e) != 0 ? 1 : 0;
-}();
-void sx_set_sweep_lds(int on) { g_sweep_lds = on ? 1 : 0; }
-// the matrix-core sweep's four interleaved MFMA chains (k_msweep<, true>): SIMPLEX_SWEEP_ILV=1
-static int g_sweep_ilv = [] {
-    const char *e = getenv("SIMPLEX_SWEEP_ILV");
-    return e && atoi(e) != 0 ? 1 : 0;
-}();
-void sx_set_sweep_interleave(int on) { g_sweep_ilv = on ? 1 : 0; }
-
 static int msweep_slots(int capacity, int cb, int rows, bool two_stage) {
     if (g_sweep_waves != 1.0f) return row_slots(capacity, cb, rows, 16);
     if (!two_stage) return row_slots(capacity, cb, rows, 16, 2.0f / 3.0f);
@@ -3413,16 +3130,15 @@ static int msweep_slots(int capacity, int cb, int rows, bool two_stage) {
     return row_slots(capacity, cb, rows, 16, nstrip / g0 >= 64 ? 2.0f : 1.0f);
 }
 
-template <bool ILV>
 static void launch_msweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, const int *nact, int s0,
                           const Pending &pd, const DevState *st, int rev, SweepCfg cfg, int cb, hipStream_t s) {
     if (cfg.batch > SX_HMAX) {
-        dim3 grid(cb, msweep_slots(sweep_capacity<k_msweep<SX_KMAX / 4, ILV>>(), cb, rows, true));
-        k_msweep<SX_KMAX / 4, ILV><<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs,
+        dim3 grid(cb, msweep_slots(sweep_capacity<k_msweep<SX_KMAX / 4>>(), cb, rows, true));
+        k_msweep<SX_KMAX / 4><<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs,
                                                         pd.PM, pd.PM2, st, pd.batch, rev, g_sweep_rec);
     } else {
-        dim3 grid(cb, msweep_slots(sweep_capacity<k_msweep<SX_HMAX / 4, ILV>>(), cb, rows, false));
-        k_msweep<SX_HMAX / 4, ILV><<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs,
+        dim3 grid(cb, msweep_slots(sweep_capacity<k_msweep<SX_HMAX / 4>>(), cb, rows, false));
+        k_msweep<SX_HMAX / 4><<<grid, 256, 0, s>>>(T, T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs,
                                                         pd.PM, pd.PM2, st, pd.batch, rev, g_sweep_rec);
     }
 }
@@ -3442,22 +3158,7 @@ void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, 
         if (ld % 2 != 0 || tl.ldA % 2 != 0 || (tl.jB < Ns && (tl.jB % 256 != 0 || tl.ldB % 2 != 0 || tl.offB % 2 != 0)))
             SX_FATAL("matrix-core sweep: 16-byte rows and 256-aligned regions required");
         const int cb = (Ns + 255) / 256;
-        if (g_sweep_lds) {
-            if (cfg.batch > SX_HMAX) {
-                dim3 grid(cb, msweep_slots(sweep_capacity<k_msweep_lds<SX_KMAX / 4>>(), cb, rows, true));
-                k_msweep_lds<SX_KMAX / 4><<<grid, 256, 0, s>>>(T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs,
-                                                               pd.PM, pd.PM2, st, pd.batch, rev, g_sweep_rec);
-            } else {
-                dim3 grid(cb, msweep_slots(sweep_capacity<k_msweep_lds<SX_HMAX / 4>>(), cb, rows, false));
-                k_msweep_lds<SX_HMAX / 4><<<grid, 256, 0, s>>>(T, rows, row0, ld, tl, Ns, nact, s0, pd.F, pd.U, pd.recs,
-                                                               pd.PM, pd.PM2, st, pd.batch, rev, g_sweep_rec);
-            }
-            return;
-        }
-        if (g_sweep_ilv)
-            launch_msweep<true>(T, rows, row0, ld, tl, Ns, nact, s0, pd, st, rev, cfg, cb, s);
-        else
-            launch_msweep<false>(T, rows, row0, ld, tl, Ns, nact, s0, pd, st, rev, cfg, cb, s);
+        launch_msweep(T, rows, row0, ld, tl, Ns, nact, s0, pd, st, rev, cfg, cb, s);
         return;
     }
     const int k = cfg.batch;  // pivots the sweep may have to apply (register slots)
@@ -3478,8 +3179,10 @@ void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, 
 // LDS history of a fused batch of k pivots: one stage
 static size_t batch_lds(int k) { return (size_t)(k < SX_HMAX ? k : SX_HMAX) * SX_TILE * sizeof(double); }
 
-size_t sx_batch_granules_a() { return SX_REC_COPIES * sx_ga_size(); }
-size_t sx_batch_granules_b() { return SX_REC_COPIES * sx_gb_size(); }
+size_t sx_batch_granules_a() { return sx_ga_size(); }
+size_t sx_batch_granules_b() { return sx_gb_size(); }
+
+int sx_batch_obj_tile_limit() { return SX_OBJ_TILES; }
 
 bool sx_batch_fits(int rows, Cols c, int k) {
     if (k < 1 || k > SX_KMAX || rows <= 0) return false;

@@ -48,13 +48,3 @@ def gpu():
         pytest.skip("no GPU")
     torch.cuda.set_device(0)
     return 0
-
-
-@pytest.fixture(scope="session")
-def unverified():
-    """Opt-in kernel variants and layouts implemented in round 4 that have not yet run on an
-    MI355X (the GPU pool was unavailable for the rest of the round): their parity tests run only
-    with SIMPLEX_TEST_UNVERIFIED=1, so that a fault in an untried kernel cannot take down the
-    default suite.  The library's defaults never use them."""
-    if os.environ.get("SIMPLEX_TEST_UNVERIFIED", "0") in ("", "0"):
-        pytest.skip("opt-in variant not yet run on the GPU (SIMPLEX_TEST_UNVERIFIED=1 runs it)")

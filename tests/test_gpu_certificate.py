@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("n,m,seed,lo,hi", CASES)
-def test_last_objective_row_matches_oracle(gpu, unverified, n, m, seed, lo, hi):
+def test_last_objective_row_matches_oracle(gpu, n, m, seed, lo, hi):
     p = sx.generateRandomProblem(n, m, seed, lo, hi)
     got = sx.twoPhaseMethodEx(p)
     d_gpu = sx.last_objective_row()

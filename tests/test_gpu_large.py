@@ -93,11 +93,11 @@ def test_simplex_gpus_mode_on_one_device(gpu, name, W):
 
 @pytest.mark.parametrize("name,W,p2p", [("config4", 1, -1), ("config5", 1, -1), ("config5", 8, 1),
                                         ("config5_degenerate", 1, -1)])
-def test_blocked_layout_pins(gpu, unverified, name, W, p2p):
-    """the full-size pins with the engine's tableaux in 4x4 blocks (simplex_set_blocked(1)): the
-    oracle's tableau, objective row and basis after the pinned pivots, read back through the
-    layout's row transfers"""
-    sx.set_blocked(1)
+def test_row_major_layout_pins(gpu, name, W, p2p):
+    """the full-size pins with the engine's tableaux row-major (simplex_set_blocked(0); the default
+    is the blocked layout, which every other test here runs): the oracle's tableau, objective row
+    and basis after the pinned pivots, read back through the layout's row transfers"""
+    sx.set_blocked(0)
     try:
         run(name, W, 0, p2p)
     finally:

@@ -231,8 +231,7 @@ def _pivots_with(cfg, T, d, base, k):
     setters = {"batch": (sx.set_batch, 0),
                "fused": (sx.set_fused, -1), "p2p": (sx.set_p2p, -1),
                "waves": (sx.set_update_waves, 0), "W": (sx.set_virtual_ranks, 1),
-               "mfma": (sx.set_sweep_mfma, -1), "lds": (sx.set_sweep_lds, 0),
-               "ilv": (sx.set_sweep_interleave, 0), "blocked": (sx.set_blocked, -1)}
+               "mfma": (sx.set_sweep_mfma, -1), "blocked": (sx.set_blocked, -1)}
     try:
         for key, val in cfg.items():
             setters[key][0](val)
@@ -395,39 +394,6 @@ def test_p2p_fused_two_phase_two_stages(gpu, W, n, m, seed, lo, hi):
         sx.set_virtual_ranks(1)
 
 
-@pytest.mark.parametrize("batch,inst,W", [(5, (333, 1025, 7), 1), (31, (333, 1025, 7), 1), (32, (300, 1100, 11), 1),
-                                         (40, (333, 1025, 7), 1), (64, (300, 1100, 11), 1), (64, (333, 1025, 7), 1),
-                                         (64, (300, 1100, 11), 4), (32, (300, 1100, 11), 8)])
-def test_lds_staged_sweep_bit_exact(gpu, unverified, batch, inst, W):
-    """the matrix-core sweep with each strip's tiles and factors staged through LDS by LDS-DMA
-    (k_msweep_lds, simplex_set_sweep_lds): one- and two-stage batches, partial last batches and a
-    partial last strip, leaving rows skipped per strip from the batch's records, virtual shards
-    (rows of other shards in the records): the oracle's bits"""
-    T, d, base = _phase1_state(*inst)
-    cfg = {"batch": batch, "lds": 1, "mfma": 1}
-    if W > 1:
-        cfg.update({"W": W, "p2p": 1})
-    Tg, dg, bg, st, done = _pivots_with(cfg, T, d, base, 150)
-    st_o, done_o = oracle.solve(T, d, base, max_pivots=150)
-    assert done == done_o
-    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
-
-
-@pytest.mark.parametrize("n,m,seed,lo,hi", [(300, 1100, 41100, 1, 100), (129, 1513, 77, -100, 100),
-                                            (40, 700, 4070, 1, 100)])
-def test_lds_staged_sweep_whole_phase(gpu, unverified, n, m, seed, lo, hi):
-    """whole two-phase solves with the LDS-staged sweep (generated tableaux: blocked layout,
-    aliased artificials, slack compaction)"""
-    p = sx.generateRandomProblem(n, m, seed, lo, hi)
-    try:
-        sx.set_sweep_lds(1)
-        sx.set_batch(64)
-        _check_two_phase(p)
-    finally:
-        sx.set_batch(0)
-        sx.set_sweep_lds(0)
-
-
 @pytest.mark.parametrize("mfma", [1, 0])
 @pytest.mark.parametrize("waves", [1e-4, 0.3, 1, 4])
 def test_sweep_grid_bit_exact(gpu, mfma, waves):
@@ -439,13 +405,15 @@ def test_sweep_grid_bit_exact(gpu, mfma, waves):
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 
+@pytest.mark.parametrize("blocked", [1, 0])
 @pytest.mark.parametrize("batch,inst,W", [(5, (333, 1025, 7), 1), (31, (333, 1025, 7), 1), (40, (333, 1025, 7), 1),
                                          (64, (300, 1100, 11), 1), (64, (300, 1100, 11), 4)])
-def test_interleaved_sweep_bit_exact(gpu, unverified, batch, inst, W):
-    """the matrix-core sweep with both tile pairs' four MFMA chains interleaved
-    (simplex_set_sweep_interleave): one- and two-stage batches, partial ones, virtual shards"""
+def test_matrix_core_sweep_layouts_bit_exact(gpu, batch, inst, W, blocked):
+    """the matrix-core sweep (both tile pairs' four MFMA chains interleaved) on the engine's blocked
+    tableau (default) and on row-major storage (simplex_set_blocked(0)): one- and two-stage
+    batches, partial ones, virtual shards"""
     T, d, base = _phase1_state(*inst)
-    cfg = {"batch": batch, "ilv": 1, "mfma": 1}
+    cfg = {"batch": batch, "blocked": blocked, "mfma": 1}
     if W > 1:
         cfg.update({"W": W, "p2p": 1})
     Tg, dg, bg, st, done = _pivots_with(cfg, T, d, base, 150)
@@ -454,16 +422,18 @@ def test_interleaved_sweep_bit_exact(gpu, unverified, batch, inst, W):
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 
+@pytest.mark.parametrize("blocked", [1, 0])
 @pytest.mark.parametrize("W", [1, 2, 4])
 @pytest.mark.parametrize("n,m,seed,lo,hi", [(300, 1100, 41100, 1, 100), (129, 1513, 77, -100, 100),
                                             (40, 700, 4070, 1, 100), (64, 128, 6528, 1, 100)])
-def test_blocked_layout_two_phase(gpu, unverified, W, n, m, seed, lo, hi):
-    """whole two-phase solves with the engine's tableaux in 4x4 blocks (simplex_set_blocked(1),
-    DESIGN.md §2): generator, build, GEMV, both batch kinds, sweeps, fix-ups, host transfers and
-    the phase-2 restart all address the blocked layout; one shard and virtual shards"""
+def test_layouts_two_phase(gpu, W, n, m, seed, lo, hi, blocked):
+    """whole two-phase solves with the engine's tableaux in 4x4 blocks (the default)
+    and row-major (simplex_set_blocked(0)): generator, build, GEMV, both batch kinds, sweeps,
+    fix-ups, host transfers and the phase-2 restart address the layout; one shard and virtual
+    shards"""
     p = sx.generateRandomProblem(n, m, seed, lo, hi)
     try:
-        sx.set_blocked(1)
+        sx.set_blocked(blocked)
         sx.set_batch(64)
         if W > 1:
             sx.set_virtual_ranks(W)
@@ -476,33 +446,18 @@ def test_blocked_layout_two_phase(gpu, unverified, W, n, m, seed, lo, hi):
         sx.set_blocked(-1)
 
 
-@pytest.mark.parametrize("ilv,lds", [(1, 0), (0, 1), (1, 1)])
-def test_blocked_layout_with_sweep_variants(gpu, unverified, ilv, lds):
-    """the blocked layout under the interleaved and the LDS-staged sweeps, the tableau split into
-    two storage regions (the test hook puts 300 slack positions in region A)"""
+@pytest.mark.parametrize("blocked", [1, 0])
+def test_layouts_two_regions(gpu, blocked):
+    """both layouts with the tableau split into two storage regions (the test hook puts 300 slack
+    positions in region A)"""
     p = sx.generateRandomProblem(300, 1100, 41100, 1, 100)
     try:
-        sx.set_blocked(1)
+        sx.set_blocked(blocked)
         sx.set_regions(300)
-        sx.set_sweep_interleave(ilv)
-        sx.set_sweep_lds(lds)
         _check_two_phase(p)
     finally:
-        sx.set_sweep_lds(0)
-        sx.set_sweep_interleave(0)
         sx.set_regions(1)
         sx.set_blocked(-1)
-
-
-@pytest.mark.parametrize("batch", [16, 64])
-@pytest.mark.parametrize("waves", [1e-4, 0.3, 4])
-def test_lds_staged_sweep_grid(gpu, unverified, batch, waves):
-    """the LDS-staged sweep from one block per column tile (every strip through the two
-    buffers) to more blocks than strips (blocks with no strip meet no barrier): bit-exact"""
-    T, d, base = _phase1_state(210, 1700, 3)
-    Tg, dg, bg, st, done = _pivots_with({"mfma": 1, "lds": 1, "waves": waves, "batch": batch}, T, d, base, 90)
-    oracle.solve(T, d, base, max_pivots=90)
-    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
 
 
 @pytest.mark.parametrize("fused", [-1, 0])
@@ -783,7 +738,7 @@ def test_slack_compaction_generated_session_width(gpu):
 # ------------------------------------------------------------------ round 4
 @pytest.mark.parametrize("batch", [32, 64])
 @pytest.mark.parametrize("W", [2, 8])
-def test_p2p_fused_fine_pivot_rows(gpu, unverified, batch, W):
+def test_p2p_fused_fine_pivot_rows(gpu, batch, W):
     """the pending pivot rows U in fine-grained memory -- what the engine allocates when the shards
     span devices (peer ranks write U over xGMI) -- forced on one GPU: the multi-rank
     batch and its sweeps stay bit-exact"""
