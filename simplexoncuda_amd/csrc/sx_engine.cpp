@@ -402,14 +402,6 @@ class Engine {
                 tl.offB = (size_t)rpr * tl.ldA;  // every shard allocates rpr rows (peers index alike)
             }
         }
-        if (alias) {  // (experiment: SIMPLEX_LDPAD extra doubles on T's row stride)
-            const char *e = getenv("SIMPLEX_LDPAD");
-            const int pad = e ? (int)round_up((size_t)std::max(atoi(e), 0), 16) : 0;
-            if (pad > 0) {
-                tl.ldA += (size_t)pad;
-                if (tl.jB < Ns1) tl.offB = (size_t)rpr * tl.ldA;
-            }
-        }
         // one allgather of (tile winner, row) beats two collectives while the rows are small
         const double slot_bytes = 8.0 * (double)slots * (double)slot_stride;
         rowgather = xchg && (g_cfg.exchange_mode == 2 || (g_cfg.exchange_mode == 0 && slot_bytes <= 1048576.0));
@@ -2290,10 +2282,6 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     sx_crt_seeds(seed, 0, sd);
     TLay btl;  // one region, the engine's storage (row-major, or 4x4 blocks in whole 16-row strips)
     btl.ldA = ld;
-    {  // (experiment: SIMPLEX_LDPAD extra doubles on T's row stride)
-        const char *e = getenv("SIMPLEX_LDPAD");
-        if (e) btl.ldA += round_up((size_t)std::max(atoi(e), 0), 16);
-    }
     btl.jB = cols;
     btl.blk = use_blocked() ? 1 : 0;
     const size_t rows_alloc = btl.blk ? round_up((size_t)rows, 16) : (size_t)rows;
@@ -2318,12 +2306,10 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     const unsigned B = 1;
     std::vector<PivRec> rc(SX_KMAX);
     std::vector<unsigned long long> pm((size_t)rows, 0ull), pm2((size_t)rows, 0ull);
-    const bool noleave = getenv("SIMPLEX_BENCH_NOLEAVE") != nullptr;  // (experiment: no leaving rows)
     for (int k = 0; k < SX_KMAX; ++k) {
         rc[k].r = (int)(((long long)k * rows) / pivots % rows);
         rc[k].e = k;
         rc[k].p = 1.0 + (double)(k % 97);
-        if (noleave) continue;
         if (k < pivots && k < SX_HMAX) pm[(size_t)rc[k].r] = ((unsigned long long)B << 32) | (1ull << k);
         if (k < pivots && k >= SX_HMAX) pm2[(size_t)rc[k].r] = ((unsigned long long)B << 32) | (1ull << (k - SX_HMAX));
     }

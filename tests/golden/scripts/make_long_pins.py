@@ -28,7 +28,7 @@ import numpy as np  # noqa: E402
 
 import oracle  # noqa: E402
 
-CHECKPOINTS = [48, 100, 250, 500, 1000]  # 48: cross-checked against large_pivots.json
+CHECKPOINTS = [48, 100, 250, 500, 1000, 2000, 3000]  # 48: cross-checked against large_pivots.json
 CASE = ("config5_degenerate", (8192, 32768, 851968, -100, 100))
 OUT = os.path.join(ROOT, "tests", "golden", "long_pivots.json")
 

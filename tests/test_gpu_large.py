@@ -131,3 +131,36 @@ def test_config5_degenerate_variant_trajectory(gpu, W, p2p):
     finally:
         sx.set_virtual_ranks(1)
         sx.set_p2p(-1)
+
+
+with open(os.path.join(GOLDEN, "long_pivots.json")) as _f:
+    LONG = json.load(_f)["config5_degenerate"]
+
+
+@pytest.mark.parametrize("W,p2p,stops", [(1, -1, (1000, 3000)), (8, 1, (3000,))])
+def test_config5_degenerate_variant_long_pins(gpu, W, p2p, stops):
+    """config 5's [-100, 100] variant (main.cu:7-8 range; 16,430 negated rows, so no slack
+    compaction) against the CPU oracle's long pins (tests/golden/long_pivots.json,
+    tests/golden/scripts/make_long_pins.py): after 1000 and 3000 phase-1 pivots the logical tableau,
+    objective row and basis are the oracle's bit for bit -- on one shard, and after 3000 pivots on
+    8 peer-memory virtual shards"""
+    pins = {c["pivots"]: c for c in LONG["checkpoints"]}
+    n, m, width = LONG["n"], LONG["m"], LONG["width"]
+    sx.set_virtual_ranks(W)
+    sx.set_p2p(p2p)
+    try:
+        sess = sx.Session(generated=(n, m, LONG["seed"], LONG["lo"], LONG["hi"]))
+        for k in stops:
+            pin = pins[k]
+            tim = sess.pivots(k - sess.total_pivots())
+            assert tim.status == sx.NOT_ENDED and sess.total_pivots() == k
+            T, d, base = sess.tableau(m, width)
+            assert float(d[0]).hex() == pin["d0_hex"]
+            assert sha(base) == pin["sha256_base"]
+            assert sha(d) == pin["sha256_d"]
+            assert sha(T) == pin["sha256_T"]
+            del T
+        sess.close()
+    finally:
+        sx.set_virtual_ranks(1)
+        sx.set_p2p(-1)
