@@ -51,7 +51,7 @@ CPU_SAMPLE = {"config2": 200, "config3": 50, "config4": 10, "config5": 5}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 F64_SPEC_TFLOPS = 78.6  # MI355X fp64 matrix (= vector) spec peak
 # the fp64 matrix rate this chip sustains: v_mfma_f64_16x16x4f64 alone on every SIMD, 2-4 waves each
-# (tools/f64_rate_probe.hip, profiles/r03_f64_rate_probe.txt: 46.8-47.6 TFLOP/s)
+# (experiments/f64_rate_probe.hip, profiles/r03_f64_rate_probe.txt: 46.8-47.6 TFLOP/s)
 F64_MFMA_MEASURED_TFLOPS = 47.6
 # reference: RTX 2070 Super, config 3 phase 1, mean 7607.5 us per pivot
 REF_PIVOTS_PER_S = {"config3": 1e6 / 7607.5}  # (no published number for configs 4-5)

@@ -3,7 +3,7 @@
 //   V  v_fma_f64 only: 8 independent chains per lane
 //   MV both in one wave: per step 4 MFMAs and NV vector fmas (the matrix and vector pipes in parallel?)
 // Every form runs on all CUs with WPS waves per SIMD; rates in TFLOP/s (MFMA 2048 flops, fma 2).
-//   build: hipcc --offload-arch=gfx950 -O3 tools/f64_rate_probe.hip -o tools/f64_rate_probe
+//   build: hipcc --offload-arch=gfx950 -O3 experiments/f64_rate_probe.hip -o tools/_ab/f64_rate_probe
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

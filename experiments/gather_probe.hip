@@ -19,8 +19,8 @@
 // meanwhile (the fused batch's idle side polling the next records).
 // Modes: G = column gather (block b: rows [512b, 512b+512), column c_k), R = row read (block b:
 // columns [512b, 512b+512) of row r_k).
-//   build: hipcc --offload-arch=gfx950 -O3 tools/gather_probe.hip -o tools/gather_probe
-//   run:   tools/gather_probe [rows ld blocks_G blocks_R rounds]
+//   build: hipcc --offload-arch=gfx950 -O3 experiments/gather_probe.hip -o tools/_ab/gather_probe
+//   run:   experiments/gather_probe [rows ld blocks_G blocks_R rounds]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -2,12 +2,12 @@
 //
 // The 64-slot sweep needs D = A B + C with every element the slot-ordered chain of fused
 // multiply-adds, fma(a3, b3, fma(a2, b2, fma(a1, b1, fma(a0, b0, c)))) -- the reference's
-// per-element operations (solver.cu:34-46).  tools/mfma_f64_probe.hip showed it for
+// per-element operations (solver.cu:34-46).  experiments/mfma_f64_probe.hip showed it for
 // v_mfma_f64_16x16x4f64; this probe checks it for the 4x4x4 (4-block) form -- 62-72 TFLOP/s on
 // MI355X against 43-48 for 16x16x4 (experiments/valu_sweep_probe.hip) -- with the lane layout below,
 // bit for bit on random operands and on edge-value pools (signed zeros, subnormals, overflow, inf,
 // NaN), at 1 and 16 chained steps.
-//   build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/mfma44_probe.hip -o tools/_ab/mfma44_probe
+//   build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off experiments/mfma44_probe.hip -o tools/_ab/mfma44_probe
 #include <hip/hip_runtime.h>
 
 #include <cmath>

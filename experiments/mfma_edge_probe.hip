@@ -3,14 +3,14 @@
 //
 // k_msweep computes each tableau element's batch update with v_mfma_f64_16x16x4f64, relying on
 // D[i][j] == fma(A[i][3], B[3][j], fma(A[i][2], B[2][j], fma(A[i][1], B[1][j], fma(A[i][0], B[0][j], C[i][j]))))
-// bit for bit (the reference's per-pivot fma order, solver.cu:34-46).  tools/mfma_f64_probe.hip
+// bit for bit (the reference's per-pivot fma order, solver.cu:34-46).  experiments/mfma_f64_probe.hip
 // showed it on normal random numbers.  This probe draws every operand from a pool of edge values
 // -- +-0, subnormals (the smallest, random ones, the largest), DBL_MIN, products that underflow
 // into the subnormal range or to zero, products and sums that overflow, +-DBL_MAX, +-inf, NaN --
 // mixed with normal values, and compares every element of D with the vector fma chain
 // (v_fma_f64, the default gfx950 float mode: fp64 denormals kept).  NaNs compare as "both NaN"
 // (payload bits reported separately).  Prints per class and an overall verdict.
-//   build: hipcc --offload-arch=gfx950 -O2 -ffp-contract=off tools/mfma_edge_probe.hip -o tools/mfma_edge_probe
+//   build: hipcc --offload-arch=gfx950 -O2 -ffp-contract=off experiments/mfma_edge_probe.hip -o tools/_ab/mfma_edge_probe
 #include <hip/hip_runtime.h>
 
 #include <cfloat>

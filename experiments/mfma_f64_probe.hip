@@ -2,7 +2,7 @@
 // bits of the sequential fused chain c = fma(a_k, b_k, c) for k = 0, 1, 2, 3 (the reference's
 // per-pivot update order, solver.cu:34-46, applied 4 pivots at a time)?  If it does, a batch
 // sweep can run on the matrix cores bit for bit.  Diagnostic only.
-//   build: hipcc --offload-arch=gfx950 -O2 -ffp-contract=off tools/mfma_f64_probe.hip -o tools/mfma_f64_probe
+//   build: hipcc --offload-arch=gfx950 -O2 -ffp-contract=off experiments/mfma_f64_probe.hip -o tools/_ab/mfma_f64_probe
 #include <hip/hip_runtime.h>
 
 #include <cmath>

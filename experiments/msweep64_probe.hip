@@ -9,7 +9,7 @@
 //   V6  V0 with the next strip's tiles loaded before this strip's matrix steps
 // Factors in the engine's strip-major layout (16-row strips, slot-major inside: sx_fidx).  Every
 // variant is checked against the vector fma chain, bit for bit.
-//   build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/msweep64_probe.hip -o tools/msweep64_probe
+//   build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off experiments/msweep64_probe.hip -o tools/_ab/msweep64_probe
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

@@ -3,7 +3,7 @@
 // The sweep applies K pending pivots to every element, in slot order (solver.cu:34-46):
 //   x = T[i][j];  for s < K:  x = fma(F[s][i], U[s][j], x)
 // v_mfma_f64_16x16x4f64 computes a 16x16 tile's D = A B + C as the k-ordered chain of fused
-// multiply-adds, bit for bit (tools/mfma_f64_probe.hip), so K/4 MFMAs per tile are exactly the
+// multiply-adds, bit for bit (experiments/mfma_f64_probe.hip), so K/4 MFMAs per tile are exactly the
 // reference's K updates.  Layout: A (16 rows x 4 slots) lane l = F^T[s0 + l/16][r0 + l%16];
 // B (4 slots x 16 columns) lane l = U[s0 + l/16][col(l%16)]; C/D lane l, register v =
 // T[r0 + l/16 + 4v][col(l%16)].  Two tiles share a lane's 16-byte access: tile X takes the even
@@ -13,7 +13,7 @@
 // [slot][row], so a fragment load is 4 rows of 128 contiguous bytes).
 // This probe measures the in-place bandwidth at K = 32 and 64 and checks every element against
 // the VALU chain.
-//   build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/msweep_probe.hip -o tools/msweep_probe
+//   build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off experiments/msweep_probe.hip -o tools/_ab/msweep_probe
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

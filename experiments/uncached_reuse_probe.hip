@@ -11,7 +11,7 @@
 // size, fill it with pattern B through uncached stores; then stream through a large unrelated
 // cached buffer (evicts the L2s); read the uncached buffer back and count words that hold
 // pattern A instead of B.  Diagnostic only.
-//   build: hipcc --offload-arch=gfx950 -O2 tools/uncached_reuse_probe.hip -o tools/uncached_reuse_probe
+//   build: hipcc --offload-arch=gfx950 -O2 experiments/uncached_reuse_probe.hip -o tools/_ab/uncached_reuse_probe
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

@@ -8,7 +8,7 @@
 //   V0     the engine's matrix-core shape (two tile pairs per wave), for comparison
 //   D<R>   R rows per step (R independent chains per lane), factors in the strip-major layout
 // Every variant is checked against the sequential fma chain, bit for bit.
-//   build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/vsweep_probe.hip -o tools/vsweep_probe
+//   build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off experiments/vsweep_probe.hip -o tools/_ab/vsweep_probe
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

@@ -19,9 +19,9 @@ step() {  # step <name> <seconds> <cmd...>
 }
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ] && exit "$1"; return 0; }
 step counters 120 rocprofv3 -L; fatal $?
-step mfma_edge 120 tools/mfma_edge_probe || exit $?
-step gather_c5 240 tools/gather_probe 32768 12800 64 144 400 || exit $?
-step gather_c3 120 tools/gather_probe 4096 12304 8 32 400 || exit $?
+step mfma_edge 120 experiments/mfma_edge_probe || exit $?
+step gather_c5 240 experiments/gather_probe 32768 12800 64 144 400 || exit $?
+step gather_c3 120 experiments/gather_probe 4096 12304 8 32 400 || exit $?
 step stamps 300 python -u tools/stage_stamps.py config5,config3 || exit $?
 step blocks 300 python -u tools/block_stamps.py config5,config3 || exit $?
 step variant 900 python -u tools/variant_solve.py --json $O/variant.json || exit $?

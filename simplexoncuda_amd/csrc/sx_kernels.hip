@@ -2612,7 +2612,7 @@ __device__ __forceinline__ void msweep_fixup(const double *Tr, double *Tw, size_
 
 // K5': the same sweep on the matrix cores.  v_mfma_f64_16x16x4f64 computes a 16x16 tile's
 // D = A B + C as the slot-ordered chain of fused multiply-adds, bit for bit
-// (tools/mfma_f64_probe.hip: every element equals fma(a3, b3, fma(a2, b2, fma(a1, b1,
+// (experiments/mfma_f64_probe.hip: every element equals fma(a3, b3, fma(a2, b2, fma(a1, b1,
 // fma(a0, b0, c)))) on MI355X), so SX_KMAX / 4 MFMAs per tile are the batch's updates in the
 // reference's order (solver.cu:34-46).  Operands of step k (slots 4k .. 4k+3):
 //   A (16 rows x 4 slots)     lane l = F[r0 + l % 16][4k + l / 16]   (sx_fidx: 64 consecutive doubles)
