@@ -2519,12 +2519,11 @@ __device__ __forceinline__ void msweep_store(const d4_t (&acc)[2][2], __amdgpu_b
     }
 }
 
-// The rows that left the basis in a batch (k_msweep): row r_s (first slot s where
-// it left) by the row slot s % G, one column per lane, the guarded chain from its stored values
-// (the strips left them unwritten).  The row slot's rows are found in one round trip (lane k:
-// slot gy + G k), and each row's operands -- its stored values, the column's pivot-row values (32
-// slots at a time), the row's factors and the pivots (lane s: slot s, read by v_readlane) -- are
-// loaded together: one or two round trips per row instead of one per 16 slots.
+// The rows that left the basis in a batch (k_msweep): row r_s (first slot s where it left) by
+// the row slot s % G, one column per lane (the strips leave them unwritten).  The row slot's rows
+// are found in one round trip (lane k: slot gy + G k); the column's pivot-row values of every slot
+// are loaded once; each group of NR rows costs one round trip (the pivot-row value it restarts
+// from and its factors; the pivots: lane s = slot s, read by v_readlane) and a branch-free chain.
 template <int NKB>
 __device__ __forceinline__ void msweep_fixup(const double *Tr, double *Tw, size_t ldr, int cr, int c0, int Ns, int rows,
                                              int row0, TLay tl, int gy, int G, int cnt,
@@ -2549,11 +2548,16 @@ __device__ __forceinline__ void msweep_fixup(const double *Tr, double *Tw, size_
             }
         }
     }
-    const double pl = l < cnt ? recs[l].p : 1.0;  // lane s: p_s
     unsigned long long todo = __ballot(rk >= 0);
-    // NR rows at a time (independent chains; within each kernel's register budget: the
-    // two-stage kernel's pivot-row registers are free here, the one-stage kernel keeps its 3
-    // waves per SIMD)
+    if (todo == 0ull) return;
+    const double pl = l < cnt ? recs[l].p : 1.0;  // lane s: p_s
+    // the column's pivot-row values of the NKB * 4 slots held (in the registers of the strips'
+    // U fragments, free by now)
+    constexpr int KU = NKB * 4;
+    double uu[KU];
+#pragma unroll
+    for (int k1 = 0; k1 < KU; ++k1) uu[k1] = (k1 < cnt && j < Ns) ? U[(size_t)k1 * ld + j] : 0.0;
+    // NR rows at a time (independent chains)
     constexpr int NR = NKB == SX_KMAX / 4 ? 4 : 2;
     while (todo) {
         int r[NR];
@@ -2568,29 +2572,30 @@ __device__ __forceinline__ void msweep_fixup(const double *Tr, double *Tw, size_
             bits[q1] = ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(bk >> 32), k) << 32) |
                        (unsigned)__builtin_amdgcn_readlane((int)bk, k);
         }
+        // A row that last left at slot sl held, just before sl, exactly the pivot row's value
+        // U[sl][j] (formed by the objective tiles with the same operations in the same order,
+        // DESIGN.md §3.2), so its value after the batch is U[sl][j] / p_sl followed by the fmas of
+        // the slots after sl: one division, no stored value read, no per-slot branch.
         double x[NR], fl[NR];
+        int sl[NR];
+        int slmin = KU;
 #pragma unroll
         for (int q1 = 0; q1 < NR; ++q1) {
-            x[q1] = (live[q1] && j < Ns) ? Tr[tl.blk ? TLay::b4(r[q1], cr + l, ldr) : (size_t)r[q1] * ldr + cr + l] : 0.0;
+            sl[q1] = live[q1] ? 63 - (int)__builtin_clzll(bits[q1]) : KU;
+            slmin = sl[q1] < slmin ? sl[q1] : slmin;
+            x[q1] = (live[q1] && j < Ns) ? U[(size_t)sl[q1] * ld + j] : 0.0;
             fl[q1] = (live[q1] && l < cnt) ? F[sx_fidx(r[q1], l)] : 0.0;  // lane s: F[r][s]
         }
-        // (32 slots of the column's pivot-row values at a time: registers)
-        for (int c1 = 0; c1 < cnt; c1 += SX_HMAX) {
-            double uu[SX_HMAX];
 #pragma unroll
-            for (int k1 = 0; k1 < SX_HMAX; ++k1)
-                uu[k1] = (c1 + k1 < cnt && j < Ns) ? U[(size_t)(c1 + k1) * ld + j] : 0.0;
+        for (int q1 = 0; q1 < NR; ++q1)
+            if (live[q1]) x[q1] = x[q1] / rdlane(pl, sl[q1]);
 #pragma unroll
-            for (int k1 = 0; k1 < SX_HMAX; ++k1) {
-                const int s1 = c1 + k1;
-                if (s1 < cnt) {
+        for (int s1 = 0; s1 < KU; ++s1) {
+            if (s1 < cnt && s1 > slmin) {
 #pragma unroll
-                    for (int q1 = 0; q1 < NR; ++q1) {
-                        if ((bits[q1] >> s1) & 1ull)
-                            x[q1] = x[q1] / rdlane(pl, s1);
-                        else
-                            x[q1] = fma(rdlane(fl[q1], s1), uu[k1], x[q1]);
-                    }
+                for (int q1 = 0; q1 < NR; ++q1) {
+                    const double t = fma(rdlane(fl[q1], s1), uu[s1], x[q1]);
+                    x[q1] = s1 > sl[q1] ? t : x[q1];
                 }
             }
         }
@@ -2667,6 +2672,13 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
     const unsigned mask2 = cnt > SX_HMAX ? slot_mask(cnt - SX_HMAX) : 0u;
     const int nkb = (cnt + 3) >> 2;
     const int OOB = 0x7fffffff;
+    // lane s: the shard row that left at slot s (-1: none here) -- the strips find their leaving
+    // rows in this register instead of loading per-row bits
+    const int rl = [&] {
+        if (l >= cnt) return -1;
+        const int r = recs[l].r - row0;
+        return r >= 0 && r < rows ? r : -1;
+    }();
     {
         // the lane's columns: c0 + 32p + 2jl and the next, p = 0, 1 (an odd last column's neighbour
         // is an untouched column: not written)
@@ -2710,11 +2722,9 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
         };
         for (int g = gy; g < nstrip; g += G) {
             const int r0 = strip_r0(g);
-            const int fr = r0 + jl;  // the A-operand row of this lane
             const __amdgpu_buffer_rsrc_t rss = strip_rsrc(Tw, r0);
-            // issue order: both pairs' tableau tiles, the strip's factors, its leaving-row bits --
-            // one memory round trip per strip (the bits are only needed after the matrix steps,
-            // and the counter waits are in issue order)
+            // issue order: both pairs' tableau tiles, the strip's factors -- one memory round trip
+            // per strip
             double2 cx[2][4];
             load_tiles(cx, r0);
             double ff[NKB];
@@ -2725,8 +2735,6 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
 #pragma unroll
                 for (int kb = 0; kb < NKB; ++kb) ff[kb] = Fs[64 * kb];
             }
-            const int frc = fr < rows ? fr : r0;
-            const unsigned long long pm1 = PM[frc], pm2 = PM2[frc];
 #pragma unroll
             for (int kb = 0; kb < NKB; ++kb)
                 if (4 * kb + rg >= cnt) ff[kb] = -0.0;
@@ -2739,22 +2747,21 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
                 acc[p][1] = d4_t{cx[p][0].y, cx[p][1].y, cx[p][2].y, cx[p][3].y};
             }
             msweep_steps<NKB>(acc, ff, uf, nkb);
-            // row fr's slots as a leaving row (both stages); bit v of skip: row r0 + rg + 4v
-            // leaves (not stored here)
+            // bit v of skip: row r0 + rg + 4v left in this batch (not stored here): the slots whose
+            // row lies in this strip, from the register list (no memory access)
             unsigned skip = 0u;
             {
-                const unsigned lb = fr < rows ? ((((unsigned)(pm1 >> 32) == B) ? ((unsigned)pm1 & mask) : 0u) |
-                                                 (((unsigned)(pm2 >> 32) == B) ? ((unsigned)pm2 & mask2) : 0u))
-                                              : 0u;
-                if (__ballot(lb != 0u) != 0ull)
-#pragma unroll
-                    for (int v = 0; v < 4; ++v)
-                        if (__shfl(lb, rg + 4 * v) != 0u) skip |= 1u << v;  // (lane rg + 4v: that row's bits)
+                unsigned long long sm = __ballot(rl >= r0 && rl < r0 + 16);
+                while (sm) {
+                    const int k = __builtin_ctzll(sm);
+                    sm &= sm - 1ull;
+                    const int rr = __builtin_amdgcn_readlane(rl, k) - r0;
+                    if ((rr & 3) == rg) skip |= 1u << (rr >> 2);
+                }
             }
             msweep_store(acc, rss, c0, jl, Ns, skip, tile_off);
         }
     }
-    if (cnt <= 0) return;
     msweep_fixup<NKB>(Tr, Tw, ldr, cr, c0, Ns, rows, row0, tl, gy, G, cnt, F, U, ld, recs, PM, PM2, B, mask, mask2);
 }
 
