@@ -359,7 +359,8 @@ def main():
                 ub_traffic = json.load(f)
         out["update_bench"] = dict(variants[0], workload=(
             "config3': the 32-pivot sweep kernel on a synthetic 4096x8192 fp64 matrix (uniform [1,100], seed "
-            "823296) with 32 random pending pivots, median of 3 runs of 50 timed sweeps (HIP events)"),
+            "823296) with 32 random pending pivots (distinct pseudo-random leaving rows since round 5), median of 3 "
+            "runs of 50 timed sweeps (HIP events)"),
             note="the matrix (268 MB) is about the size of the 256 MB Infinity Cache, so sweeps partly hit it; "
                  "out_of_cache is the same kernel on a 2.1 GB matrix (HBM rate)",
             traffic=(ub_traffic or {}).get("4096x8192"),

@@ -2306,8 +2306,23 @@ double simplex_bench_sweep(int rows, int cols, unsigned int seed, int lo, int hi
     const unsigned B = 1;
     std::vector<PivRec> rc(SX_KMAX);
     std::vector<unsigned long long> pm((size_t)rows, 0ull), pm2((size_t)rows, 0ull);
+    // the leaving rows: distinct pseudo-random rows (a fixed LCG of the seed), as the pivot loop's
+    // are -- evenly spaced ones (every rows/pivots-th row, rounds 1-4) put every leaving row of a
+    // 4096-row sweep into the strips of 2 of its 16 row slots
+    std::vector<int> lrow;
+    {
+        std::vector<unsigned char> used((size_t)rows, 0);
+        unsigned long long x = 0x9e3779b97f4a7c15ull ^ seed;
+        while ((int)lrow.size() < SX_KMAX) {
+            x = x * 6364136223846793005ull + 1442695040888963407ull;
+            const int r = (int)((x >> 33) % (unsigned long long)rows);
+            if (used[(size_t)r] && (int)lrow.size() < rows) continue;
+            used[(size_t)r] = 1;
+            lrow.push_back(r);
+        }
+    }
     for (int k = 0; k < SX_KMAX; ++k) {
-        rc[k].r = (int)(((long long)k * rows) / pivots % rows);
+        rc[k].r = lrow[(size_t)k];
         rc[k].e = k;
         rc[k].p = 1.0 + (double)(k % 97);
         if (k < pivots && k < SX_HMAX) pm[(size_t)rc[k].r] = ((unsigned long long)B << 32) | (1ull << k);
