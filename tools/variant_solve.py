@@ -6,7 +6,10 @@ FEASIBLE answer checks a primal/dual certificate on the host from the final obje
   A x <= b, x >= 0, y >= 0, A^T y >= c (each within 1e-9 of the row's scale), |c.x - b.y| <= 1e-6 |c.x|.
 For INFEASIBLE / DEGENERATE it records d[0] and the basic artificial variables
 (twoPhaseMethod.cu:264-282).  (diagnostic; its output is the fixture tests/golden/variant_solves.json)
-usage: python tools/variant_solve.py [n m seed lo hi] [--json out.json]"""
+usage: python tools/variant_solve.py [n m seed lo hi] [--json out.json] [--limit PIVOTS] [--seconds S]
+  --limit: phase-1 pivots before the instance is declared not to end (default 2,000,000);
+  --seconds: also stop phase 1 after S seconds of pivoting (the record says which bound ended it);
+  the record is rewritten after every chunk, so a run cut short still leaves its trace."""
 import json
 import os
 import sys
@@ -43,10 +46,17 @@ def certificate(A, b, c, x, d, n, m):
 
 
 def main():
-    args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    out_json = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
-    if out_json in args:
-        args.remove(out_json)
+    argv = sys.argv[1:]
+    opts = {}
+    for k in ("--json", "--limit", "--seconds"):
+        if k in argv:
+            i = argv.index(k)
+            opts[k] = argv[i + 1]
+            del argv[i:i + 2]
+    args = [a for a in argv if not a.startswith("--")]
+    out_json = opts.get("--json")
+    p1_limit = int(opts.get("--limit", P1_LIMIT))
+    p1_seconds = float(opts.get("--seconds", 0)) or None
     n, m, seed, lo, hi = (int(a) for a in args) if args else (8192, 32768, 851968, -100, 100)
     import threading
     t_start = time.perf_counter()
@@ -66,7 +76,16 @@ def main():
     sess = sx.Session(generated=(n, m, seed, lo, hi))
     t1 = time.perf_counter()
     p1_status, p1_pivots = sx.NOT_ENDED, 0
-    while p1_pivots < P1_LIMIT:
+    bound = "pivot_limit"
+    neg = None
+
+    def record(status):
+        return {"instance": f"generateRandomProblem({n}, {m}, {seed}, {lo}, {hi})", "n": n, "m": m, "seed": seed,
+                "lo": lo, "hi": hi, "status": status, "pivot_limit": p1_limit, "seconds_limit": p1_seconds,
+                "ended_by": bound, "phase1_seconds": time.perf_counter() - t1, "phase1_trace": trace,
+                "negated_rows": neg}
+
+    while p1_pivots < p1_limit:
         tm = sess.pivots(CHUNK)
         p1_pivots = sess.total_pivots()
         p1_status = tm.status
@@ -75,21 +94,26 @@ def main():
               f"{time.perf_counter() - t1:.1f} s", flush=True)
         if p1_status != sx.NOT_ENDED:
             break
+        if out_json and len(trace) % 10 == 0:
+            with open(out_json, "w") as f:
+                json.dump(record("PHASE1_RUNNING"), f, indent=1)
+        if p1_seconds is not None and time.perf_counter() - t1 > p1_seconds:
+            bound = "seconds_limit"
+            break
     sess.close()
     prob = sx.generateRandomProblemDevice(n, m, seed, lo, hi)
     A, b, c = prob.arrays()
+    neg = int(np.count_nonzero(b < -1e-9))
     if p1_status == sx.NOT_ENDED:
         alive.set()
-        rec = {"instance": f"generateRandomProblem({n}, {m}, {seed}, {lo}, {hi})", "n": n, "m": m, "seed": seed,
-               "lo": lo, "hi": hi, "status": "PHASE1_NOT_ENDED", "pivot_limit": P1_LIMIT, "phase1_trace": trace,
-               "negated_rows": int(np.count_nonzero(b < -1e-9))}
+        rec = record("PHASE1_NOT_ENDED")
         print(json.dumps(rec), flush=True)
         if out_json:
             with open(out_json, "w") as f:
                 json.dump(rec, f, indent=1)
         return
     t0 = time.perf_counter()
-    res = sx.twoPhaseMethodEx(prob, max_pivots=4 * P1_LIMIT)
+    res = sx.twoPhaseMethodEx(prob, max_pivots=4 * max(p1_limit, p1_pivots))
     dt = time.perf_counter() - t0
     ph = sx.load()
     import ctypes
