@@ -110,6 +110,13 @@ void simplex_set_mr_single_launch(int on);
  * -1 auto (when the shards span devices, default), 1 always (test hook: the one-GPU cost and
  * parity of that path), 0 never */
 void simplex_set_fine_pivot_rows(int mode);
+/* multi-rank fused batches with the objective row replicated: every rank runs every objective
+ * tile (decides the entering variable and forms the whole pivot row itself), so a pivot's only
+ * cross-rank hand-offs are the ratio tiles' winners and the leaving row read from its owner
+ * (DESIGN.md §5.2): -1 auto (when the shards span devices, default), 1 always (when the grid of
+ * slots + every objective tile per rank fits; else the split objective), 0 never (each rank runs
+ * its share of the objective tiles and the records go to every rank) */
+void simplex_set_replicated_objective(int mode);
 /* new engines' tableau storage inside each region: -1 default (blocks of 4 rows x 4 columns in
  * 16-row strips, unless the environment sets SIMPLEX_BLOCKED=0), 1 blocked, 0 plain row-major
  * (callers' tableaux, tabular.h, are always row-major) */

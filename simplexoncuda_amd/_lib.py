@@ -112,6 +112,7 @@ SIGNATURES = {
     "simplex_set_hang_inject_slot": (None, [ctypes.c_int]),
     "simplex_set_first_batch_id": (None, [ctypes.c_uint]),
     "simplex_set_fine_pivot_rows": (None, [ctypes.c_int]),
+    "simplex_set_replicated_objective": (None, [ctypes.c_int]),
     "simplex_set_blocked": (None, [ctypes.c_int]),
     "twoPhaseMethodEx": (ctypes.c_int, [P_PROBLEM, c_double_p, c_double_p, c_int_p, c_ll_p, ctypes.c_longlong]),
     "simplex_problem_from_arrays": (P_PROBLEM, [ctypes.c_int, ctypes.c_int, c_double_p, c_double_p, c_double_p]),

@@ -394,6 +394,13 @@ def set_fine_pivot_rows(mode):
     _lib.load().simplex_set_fine_pivot_rows(int(mode))
 
 
+def set_replicated_objective(mode):
+    """Multi-rank fused batches with every rank running every objective tile (one cross-rank hop
+    per pivot): -1 default (when shards sit on different devices), 1 always (when
+    the grid fits), 0 never."""
+    _lib.load().simplex_set_replicated_objective(int(mode))
+
+
 def set_regions(mode):
     """New engines' tableau layout: 0 plain rows, 1 auto two-region layout (default), >= 2 region A
     forced to that many slack positions (test hook)."""

@@ -215,13 +215,14 @@ size_t sx_batch_granules_b();
 bool sx_batch_mr_fits(int slots, int nb_local, int k, int grids);
 void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld, TLay tl, Cols c, double *d, double *d_save,
                         int *base, DevState *st, const Pending &pd, int k, int slots, int W, int rank, int tb0, int tb1,
-                        BatchChan *chan, const unsigned long long *ga, const unsigned long long *gb,
+                        int repl, BatchChan *chan, const unsigned long long *ga, const unsigned long long *gb,
                         const unsigned long long *gdone, const PeerView &pv, unsigned long long timeout,
                         hipStream_t s);
 // one rank of a multi-rank launch
 struct MrLaunchRank {
     const double *T;
     int rows, row0, rank, tb0, tb1;
+    int repl;  // replicated objective: every rank runs every objective tile (tb0 = 0, tb1 = all)
     const int *perm;
     double *d, *d_save;
     int *base;

@@ -81,6 +81,7 @@ struct Config {
     int mr_two_stage = -1;         // peer-memory multi-rank batches of two stages (-1: unless SIMPLEX_MR_STAGES=1)
     unsigned first_batch_id = 1;   // test hook: batch id of a new engine's first batch
     int fine_u = -1;               // U in fine-grained memory: -1 across devices, 1 always, 0 never
+    int repl_obj = -1;             // replicated objective in multi-rank batches: -1 across devices, 1 always, 0 never
     int blocked = -1;              // the engine's tableaux in 4x4 blocks (TLay::blk): -1 default (off unless
                                    // SIMPLEX_BLOCKED=1), 0 row-major, 1 blocked
     int ipc_rank = -1, ipc_world = 0;  // test hook: one shard per process, peers through IPC handles, no RCCL
@@ -696,7 +697,9 @@ class Engine {
             const char *e = getenv("SIMPLEX_FINE_PIVOT_ROWS");
             if (e) fu = atoi(e) != 0 ? 1 : 0;
         }
-        x.fineU = fu > 0 || (fu < 0 && ((rccl && !ipc) || multidev));
+        // (with the replicated objective every rank forms the whole pivot row itself and no peer
+        // writes U, once every batch of the solve fits that way)
+        x.fineU = fu > 0 || (fu < 0 && ((rccl && !ipc) || multidev) && !repl_always());
         if (x.fineU)
             SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&x.U), (size_t)SX_KMAX * ld * sizeof(double),
                                          hipDeviceMallocFinegrained));
@@ -1161,13 +1164,37 @@ class Engine {
         }
         if (!p2p) return false;
         const int NBg = (N - 1 + SX_TILE - 1) / SX_TILE;
-        const int nbl = (NBg + W - 1) / W;
-        int grids = 1;  // ranks resident together on one device
-        if (!rccl) {
-            std::map<int, int> per_dev;
-            for (auto &x : sh) grids = std::max(grids, ++per_dev[x.dev]);
-        }
-        return sx_batch_mr_fits(slots, nbl, k, grids);
+        if (repl_now(k)) return true;
+        return sx_batch_mr_fits(slots, (NBg + W - 1) / W, k, mr_grids());
+    }
+
+    // ranks resident together on one device (virtual shards: all of them)
+    int mr_grids() const {
+        if (rccl) return 1;
+        if (!gpus_mode) return std::max(1, W);  // (virtual shards: all on this device)
+        int grids = 1;
+        std::map<int, int> per_dev;
+        for (int d : shard_dev) grids = std::max(grids, ++per_dev[d]);
+        return grids;
+    }
+    // The replicated objective: every rank runs every objective tile, so each
+    // rank decides the entering variable from its own records and forms the whole pivot row in
+    // its own U -- the only cross-rank hand-offs of a pivot are the ratio tiles' winners and the
+    // leaving row read from its owner.  Default across devices (RCCL ranks, a device list on
+    // several GPUs), where the objective hop is an xGMI hop; forced on or off by
+    // simplex_set_replicated_objective.  Used for a batch when its grid (slots + every objective
+    // tile per rank) fits, else the split objective.
+    bool repl_mode() const {
+        if (W < 2 || g_cfg.repl_obj == 0) return false;
+        return g_cfg.repl_obj > 0 || (rccl && !ipc) || multidev;
+    }
+    bool repl_now(int k) const {
+        return repl_mode() && sx_batch_mr_fits(slots, (N - 1 + SX_TILE - 1) / SX_TILE, k, mr_grids());
+    }
+    // ... for every batch of this engine (phase 1 is the widest)
+    bool repl_always() const {
+        return repl_mode() && g_cfg.fused != 0 &&
+               sx_batch_mr_fits(slots, (N1 - 1 + SX_TILE - 1) / SX_TILE, SX_KMAX, mr_grids());
     }
 
     void enqueue_batch(int k) {
@@ -1190,13 +1217,19 @@ class Engine {
             q_host = k;
             return;
         }
-        d_split = true;  // (multi-rank batches keep only each rank's own slice of d current)
+        const bool rp = repl_now(k);
+        if (rp) gather_d();  // (a replicated batch starts from the whole row on every rank)
+        d_split = !rp;       // (split multi-rank batches keep only each rank's own slice of d current)
+        const int NBgk = (N - 1 + SX_TILE - 1) / SX_TILE;
+        auto tb_of = [&](int rank, int &tb0, int &tb1) {
+            tb0 = rp ? 0 : (int)((long long)rank * NBgk / W);
+            tb1 = rp ? NBgk : (int)((long long)(rank + 1) * NBgk / W);
+        };
         if (!rccl && (g_cfg.mr_single_launch || multidev)) {
             // shards of this process: the ranks on one GPU as ONE launch (all of them for virtual
             // shards; one launch per GPU when each shard has its own), so a device's ranks are
             // resident together whenever the grid fits; they hand off through each other's
             // buffers exactly as RCCL ranks do through peer memory
-            const int NBg = (N - 1 + SX_TILE - 1) / SX_TILE;
             std::map<int, std::vector<MrLaunchRank>> by_dev;
             for (size_t i = 0; i < sh.size(); ++i) {
                 Shard &x = sh[i];
@@ -1205,8 +1238,8 @@ class Engine {
                 q.rows = x.rows;
                 q.row0 = x.row0;
                 q.rank = x.rank;
-                q.tb0 = (int)((long long)x.rank * NBg / W);
-                q.tb1 = (int)((long long)(x.rank + 1) * NBg / W);
+                tb_of(x.rank, q.tb0, q.tb1);
+                q.repl = rp ? 1 : 0;
                 q.perm = compact ? x.perm : nullptr;
                 q.d = x.d;
                 q.d_save = x.d_save;
@@ -1228,7 +1261,6 @@ class Engine {
         } else {
             // every rank's batch runs at once (virtual shards: one stream each, forked from and
             // joined back into the engine stream); the ranks hand off through peer memory
-            const int NBg = (N - 1 + SX_TILE - 1) / SX_TILE;
             const unsigned long long timeout = rccl ? 200000000ull : 100000000ull;  // 2 s / 1 s at 100 MHz
             if (!rccl) SX_HIP(hipEventRecord(ev_fork, s));
             for (size_t i = 0; i < sh.size(); ++i) {
@@ -1238,10 +1270,10 @@ class Engine {
                     xs = x.ss;
                     SX_HIP(hipStreamWaitEvent(xs, ev_fork, 0));
                 }
-                const int tb0 = (int)((long long)x.rank * NBg / W), tb1 = (int)((long long)(x.rank + 1) * NBg / W);
+                int tb0, tb1;
+                tb_of(x.rank, tb0, tb1);
                 sx_launch_batch_mr(x.T, x.rows, x.row0, rpr, ld, tl, cols(N, x), x.d, x.d_save, x.base, x.st, pending(x), k,
-                                   slots, W,
-                                   x.rank, tb0, tb1, x.chan, x.ga, x.gb, x.gdone, pv, timeout, xs);
+                                   slots, W, x.rank, tb0, tb1, rp ? 1 : 0, x.chan, x.ga, x.gb, x.gdone, pv, timeout, xs);
                 if (!rccl) SX_HIP(hipEventRecord(ev_join[i], xs));
             }
             if (!rccl)
@@ -1872,6 +1904,7 @@ void simplex_set_hang_inject_slot(int slot) { g_cfg.inject_slot = slot >= 0 ? sl
 long long simplex_hang_recoveries(void) { return g_cfg.hang_recoveries; }
 long long simplex_fused_batches(void) { return g_cfg.fused_batches; }
 void simplex_set_fine_pivot_rows(int mode) { g_cfg.fine_u = mode < 0 ? -1 : (mode ? 1 : 0); }
+void simplex_set_replicated_objective(int mode) { g_cfg.repl_obj = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_blocked(int mode) { g_cfg.blocked = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_first_batch_id(unsigned int id) { g_cfg.first_batch_id = (id >= 1 && id < SX_BATCH_IDS) ? id : 1; }
 

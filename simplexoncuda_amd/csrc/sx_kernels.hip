@@ -1780,7 +1780,11 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
 //                     every rank's gb;
 //   ratio tiles       read all objective records from their own gb and run pass 2 (the next
 //                     entering variable), and apply the pivot to their rows.
-// Between batches every rank keeps only its own slice of d current (Engine::gather_d).  At the
+// Between batches every rank keeps only its own slice of d current (Engine::gather_d).
+// Replicated objective (repl): every rank runs ALL the objective tiles
+// (tb0 = 0, tb1 = NBg) on its own copy of d, writes their records into its own gb and the pivot
+// row into its own U only -- the ratio records and the leaving row's remote reads stay the only
+// cross-rank traffic of a pivot, and every rank's d stays whole.  At the
 // end of the batch a done granule per rank: a rank's last block leaves only when every rank's
 // data has landed, so the sweep that follows reads complete U.  Cross-rank stores and loads are
 // system-scope (sc0 sc1); the records polled across GPUs are uncached allocations.  The same
@@ -1801,8 +1805,8 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                                               double *__restrict__ d_save, int *base, DevState *st, double *U, double *F,
                                               PivRec *recs, unsigned long long *PM, unsigned long long *PM2, unsigned B,
                                               int K, int slots, int W,
-                                              int rank, int tb0, int tb1, int NBg, BatchChan *ch, const u64 *ga,
-                                              const u64 *gb, const u64 *gdone, PeerView pv,
+                                              int rank, int tb0, int tb1, int NBg, int repl, BatchChan *ch,
+                                              const u64 *ga, const u64 *gb, const u64 *gdone, PeerView pv,
                                               unsigned long long timeout) {
     extern __shared__ double s_hist[];  // [K][512]: F history (ratio tiles) / U history (objective tiles)
     __shared__ double s_v[16];
@@ -2173,9 +2177,11 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                     const int win = wi >= 0 ? wi - tb * SX_TILE : 0;
                     const unsigned pl = wi >= 0 ? (unsigned)win : SX_NOIDX;
                     // granule-major over the ranks: the value granules reach every rank first
-                    const int nG = kOU + 2 * (qq + 1);
-                    for (int idx = t; idx < W * nG; idx += 64) {
-                        const int k = idx / W, rk = idx - k * W;
+                    // (replicated objective, repl: every rank runs every objective tile, so the
+                    // record goes to this rank's copy alone)
+                    const int nG = kOU + 2 * (qq + 1), WR = repl ? 1 : W;
+                    for (int idx = t; idx < WR * nG; idx += 64) {
+                        const int k = idx / WR, rk = repl ? rank : idx - k * WR;
                         unsigned data;
                         if (k == kOR) {
                             data = (unsigned)r;
@@ -2193,10 +2199,14 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                     }
                 }
                 // the pivot row into every rank's U[q] (the sweep's input, read after the batch):
-                // issued behind the record, so the W-fold stores do not delay it
+                // issued behind the record, so the W-fold stores do not delay it (repl: this
+                // rank's U alone -- every rank forms the whole row)
                 if (ost == SX_NOT_ENDED && liveB && 1 + ia < c.Ns) {
                     const double uq = s_hist[qq * SX_TILE + t];
-                    for (int k = 0; k < W; ++k) st_sys(pv.U[k] + (size_t)q * ld + mj, uq);
+                    if (repl)
+                        st_sys(pv.U[rank] + (size_t)q * ld + mj, uq);
+                    else
+                        for (int k = 0; k < W; ++k) st_sys(pv.U[k] + (size_t)q * ld + mj, uq);
                 }
                 if (ost != SX_NOT_ENDED) {
                     status = ost;
@@ -2288,11 +2298,11 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
                                                   Cols c, double *__restrict__ d, double *__restrict__ d_save, int *base,
                                                   DevState *st, double *U, double *F, PivRec *recs,
                                                   unsigned long long *PM, unsigned long long *PM2, unsigned B, int K,
-                                                  int slots, int W, int rank, int tb0, int tb1, int NBg,
+                                                  int slots, int W, int rank, int tb0, int tb1, int NBg, int repl,
                                                   BatchChan *ch, const u64 *ga, const u64 *gb, const u64 *gdone,
                                                   PeerView pv, unsigned long long timeout) {
     batch_mr_body((int)blockIdx.x, gridDim.x, T, rows, row0, rpr, ld, tl, c, d, d_save, base, st, U, F, recs, PM, PM2, B, K,
-                  slots, W, rank, tb0, tb1, NBg, ch, ga, gb, gdone, pv, timeout);
+                  slots, W, rank, tb0, tb1, NBg, repl, ch, ga, gb, gdone, pv, timeout);
 }
 
 // The batches of the nloc ranks (of W) that live on one GPU in ONE launch: block b belongs to
@@ -2303,7 +2313,7 @@ __global__ __launch_bounds__(512) void k_batch_mr(const double *__restrict__ T, 
 // GPUs: one launch per GPU.)
 struct MrRank {
     const double *T;
-    int rows, row0, rank, tb0, tb1;
+    int rows, row0, rank, tb0, tb1, repl;
     const int *perm;
     double *d, *d_save;
     int *base;
@@ -2328,7 +2338,7 @@ __global__ __launch_bounds__(512) void k_batch_mr_multi(MrRanks R, int nloc, int
     cx.perm = x.perm;
     batch_mr_body((int)blockIdx.x - R.first[k], (unsigned)(R.first[k + 1] - R.first[k]), x.T, x.rows, x.row0, rpr, ld,
                   tl, cx, x.d, x.d_save, x.base, x.st, x.U, x.F, x.recs, x.PM, x.PM2, B, K, slots, W, x.rank, x.tb0, x.tb1,
-                  NBg, x.ch, x.ga, x.gb, x.gdone, pv, timeout);
+                  NBg, x.repl, x.ch, x.ga, x.gb, x.gdone, pv, timeout);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -3247,15 +3257,16 @@ bool sx_batch_mr_fits(int slots, int nb_local, int k, int grids) {
 
 void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld, TLay tl, Cols c, double *d, double *d_save,
                         int *base, DevState *st, const Pending &pd, int k, int slots, int W, int rank, int tb0, int tb1,
-                        BatchChan *chan, const unsigned long long *ga, const unsigned long long *gb,
+                        int repl, BatchChan *chan, const unsigned long long *ga, const unsigned long long *gb,
                         const unsigned long long *gdone, const PeerView &pv, unsigned long long timeout,
                         hipStream_t s) {
     const int NBg = (c.N - 1 + SX_TILE - 1) / SX_TILE;
-    if (W < 1 || W > SX_MAXW || W * slots > SX_TILE || NBg > SX_TILE || NBg < 1 || tb0 < 0 || tb1 > NBg || tb0 > tb1)
+    if (W < 1 || W > SX_MAXW || W * slots > SX_TILE || NBg > SX_TILE || NBg < 1 || tb0 < 0 || tb1 > NBg || tb0 > tb1 ||
+        (repl && (tb0 != 0 || tb1 != NBg)))
         SX_FATAL("multi-rank fused batch: bad shape");
     k_batch_mr<<<slots + (tb1 - tb0), SX_TILE, batch_lds(k), s>>>(T, rows, row0, rpr, ld, tl, c, d, d_save, base, st, pd.U, pd.F,
                                                                   pd.recs, pd.PM, pd.PM2, pd.batch, k, slots, W, rank, tb0,
-                                                                  tb1, NBg, chan, ga, gb, gdone, pv, timeout);
+                                                                  tb1, NBg, repl, chan, ga, gb, gdone, pv, timeout);
 }
 
 void sx_launch_batch_mr_multi(const MrLaunchRank *ranks, int nloc, int W, int rpr, size_t ld, TLay tl, Cols c, unsigned B,
@@ -3267,7 +3278,9 @@ void sx_launch_batch_mr_multi(const MrLaunchRank *ranks, int nloc, int W, int rp
     R.first[0] = 0;
     for (int i = 0; i < nloc; ++i) {
         const MrLaunchRank &q = ranks[i];
-        if (q.tb0 < 0 || q.tb1 > NBg || q.tb0 > q.tb1) SX_FATAL("multi-rank fused batch: bad objective tiles");
+        if (q.tb0 < 0 || q.tb1 > NBg || q.tb0 > q.tb1 || (q.repl && (q.tb0 != 0 || q.tb1 != NBg)) ||
+            q.repl != ranks[0].repl)
+            SX_FATAL("multi-rank fused batch: bad objective tiles");
         MrRank &x = R.r[i];
         x.T = q.T;
         x.rows = q.rows;
@@ -3275,6 +3288,7 @@ void sx_launch_batch_mr_multi(const MrLaunchRank *ranks, int nloc, int W, int rp
         x.rank = q.rank;
         x.tb0 = q.tb0;
         x.tb1 = q.tb1;
+        x.repl = q.repl;
         x.perm = q.perm;
         x.d = q.d;
         x.d_save = q.d_save;

@@ -791,3 +791,66 @@ def test_subnormal_tableau_bit_exact(gpu, batch, mfma):
     assert done == done_o
     assert np.count_nonzero((T != 0) & (np.abs(T) < 2.2250738585072014e-308)) > 1000  # (subnormal results too)
     assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+
+
+# ------------------------------------------------------------------ round 5
+@pytest.mark.parametrize("batch", [32, 64])
+@pytest.mark.parametrize("W", [2, 3, 4, 8])
+def test_replicated_objective_pivots(gpu, batch, W):
+    """multi-rank fused batches with the objective row replicated (every rank runs every objective
+    tile, decides the entering variable from its own records and forms the whole pivot row in its
+    own U; simplex_set_replicated_objective) on W virtual shards: bit-exact with the
+    oracle, every batch fused, no hang recovery"""
+    lib = sx.load()
+    T, d, base = _phase1_state(300, 1100, 11)
+    f0, h0 = lib.simplex_fused_batches(), lib.simplex_hang_recoveries()
+    try:
+        sx.set_replicated_objective(1)
+        Tg, dg, bg, st, done = _pivots_with({"batch": batch, "W": W, "p2p": 1}, T, d, base, 150)
+    finally:
+        sx.set_replicated_objective(-1)
+    st_o, done_o = oracle.solve(T, d, base, max_pivots=150)
+    assert done == done_o
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+    assert lib.simplex_fused_batches() - f0 >= 150 // batch
+    assert lib.simplex_hang_recoveries() == h0
+
+
+@pytest.mark.parametrize("W", [2, 4])
+@pytest.mark.parametrize("n,m,seed,lo,hi", [(300, 1100, 5, 1, 100), (200, 1500, 77, -100, 100)])
+def test_replicated_objective_two_phase(gpu, W, n, m, seed, lo, hi):
+    """whole two-phase solves (phase 2's narrower row included; the second instance negates rows:
+    no slack compaction) on virtual shards with the replicated objective"""
+    p = sx.generateRandomProblem(n, m, seed, lo, hi)
+    try:
+        sx.set_replicated_objective(1)
+        sx.set_virtual_ranks(W)
+        sx.set_p2p(1)
+        _check_two_phase(p)
+    finally:
+        sx.set_p2p(-1)
+        sx.set_virtual_ranks(1)
+        sx.set_replicated_objective(-1)
+
+
+@pytest.mark.parametrize("slot", [3, 40])
+def test_replicated_objective_hang_recovery(gpu, slot):
+    """a replicated multi-rank batch aborted from inside after `slot` pivots (the objective row
+    already updated by them on every rank): each rank restores its whole row and the batch is
+    re-run on the per-pivot path -- still bit-exact"""
+    lib = sx.load()
+    T, d, base = _phase1_state(300, 1100, 11)
+    h0 = lib.simplex_hang_recoveries()
+    try:
+        sx.set_replicated_objective(1)
+        lib.simplex_set_hang_inject(1)
+        lib.simplex_set_hang_inject_slot(slot)
+        Tg, dg, bg, st, done = _pivots_with({"batch": 64, "W": 2, "p2p": 1}, T, d, base, 150)
+    finally:
+        lib.simplex_set_hang_inject(-1)
+        lib.simplex_set_hang_inject_slot(-1)
+        sx.set_replicated_objective(-1)
+    st_o, done_o = oracle.solve(T, d, base, max_pivots=150)
+    assert done == done_o
+    assert same(Tg, T) and same(dg, d) and np.array_equal(bg, base)
+    assert lib.simplex_hang_recoveries() == h0 + 1
