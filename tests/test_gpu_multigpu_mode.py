@@ -25,6 +25,7 @@ sys.path.insert(0, {root!r})
 import numpy as np
 import simplexoncuda_amd as sx
 lib = sx.load()
+sx.set_replicated_objective({repl})
 p = sx.generateRandomProblem({n}, {m}, {seed}, {lo}, {hi})
 r = sx.twoPhaseMethodEx(p)
 print(json.dumps({{"gpus": sx.gpus(), "status": r.status, "pivots": list(r.pivots), "opt": float(r.optimal_value).hex(),
@@ -34,17 +35,19 @@ print(json.dumps({{"gpus": sx.gpus(), "status": r.status, "pivots": list(r.pivot
 """
 
 
-def run_child(env_gpus, n, m, seed, lo, hi):
+def run_child(env_gpus, n, m, seed, lo, hi, repl=-1):
     env = dict(os.environ, SIMPLEX_GPUS=env_gpus)
-    code = CHILD.format(root=ROOT, n=n, m=m, seed=seed, lo=lo, hi=hi)
+    code = CHILD.format(root=ROOT, n=n, m=m, seed=seed, lo=lo, hi=hi, repl=repl)
     return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=240)
 
 
-@pytest.mark.parametrize("gpus", ["0,0", "0,0,0", "0,0,0,0,0,0,0,0"])
+@pytest.mark.parametrize("gpus,repl", [("0,0", -1), ("0,0,0", -1), ("0,0,0,0,0,0,0,0", -1), ("0,0", 1), ("0,0,0,0", 1)])
 @pytest.mark.parametrize("n,m,seed,lo,hi", [(300, 1100, 41100, 1, 100), (129, 1513, 77, -100, 100)])
-def test_unchanged_caller_gets_shards_from_env(gpu, gpus, n, m, seed, lo, hi):
+def test_unchanged_caller_gets_shards_from_env(gpu, gpus, repl, n, m, seed, lo, hi):
+    """(repl 1: the replicated objective -- the default across GPUs -- forced on the one device,
+    self-check included)"""
     import json
-    r = run_child(gpus, n, m, seed, lo, hi)
+    r = run_child(gpus, n, m, seed, lo, hi, repl)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     got = json.loads(r.stdout.strip().splitlines()[-1])
     assert got["gpus"] == [int(x) for x in gpus.split(",")]
