@@ -99,12 +99,10 @@ std::mutex g_mu;
 
 // The granule records of the RCCL ranks' peer-memory batch are polled inside a launch while
 // other GPUs write them, so they are uncached.  In round 2, single-GPU batches that ran after
-// virtual-shard runs had allocated and freed uncached records diverged from the oracle; the
-// round-4 reuse probe (profiles/r04_uncached_bisect_and_reuse.txt) found no stale word on a
-// freed-and-reused page either way, so that divergence is unexplained.  As a
-// precaution the uncached records are still allocated once per process, after an L2
-// write-back, and never freed; everything else, virtual shards included, uses plain device
-// memory.
+// virtual-shard runs had allocated and freed uncached records diverged from the oracle; round 5
+// tied that class of divergence to freeing uncached allocations (below, g_special; DESIGN.md
+// §5.2), so the uncached records are allocated once per process, after an L2 write-back, and
+// never freed; everything else, virtual shards included, uses plain device memory.
 // A pool of such sets, one per (device, concurrent engine): a second engine alive at the same
 // time (or a second shard on the device) takes another set instead of falling back to cached
 // memory.
@@ -114,6 +112,22 @@ struct UncachedRecords {
     bool busy = false;
 };
 std::vector<UncachedRecords> g_urec;
+
+// The same rule for the pending pivot rows U when they are not plain device memory (fine-grained
+// across devices; uncached under the diagnostic switch): allocated once, kept for the process's
+// lifetime and handed to later engines (best fit on the same device and flags), never freed.
+// Round 5 found what the round-2/4 divergences share (profiles/r05_uncached_u_bisect.txt): W = 8
+// virtual-shard solves with uncached U diverge from one shard only after earlier engines have
+// freed such allocations -- the same code with every uncached U kept allocated was bit-exact in
+// 12 of 12 solves, with them freed it diverged in 4 of 12 -- so no engine frees one.
+struct SpecialBuf {
+    int dev = -1;
+    unsigned flags = 0;
+    size_t bytes = 0;
+    void *p = nullptr;
+    bool busy = false;
+};
+std::vector<SpecialBuf> g_special;
 
 void say(const char *s) {
     if (g_cfg.verbose) {
@@ -129,6 +143,16 @@ T *dalloc(size_t count) {
     T *p = nullptr;
     if (count == 0) count = 1;
     SX_HIP(hipMalloc(reinterpret_cast<void **>(&p), count * sizeof(T)));
+    // (SIMPLEX_DIAG_POISON=1, diagnostic only: every engine allocation starts as all-ones bytes --
+    // NaN doubles, -1 integers -- so a read before the first write shows in the result)
+    static const int poison = [] {
+        const char *e = getenv("SIMPLEX_DIAG_POISON");
+        return e ? atoi(e) : 0;
+    }();
+    if (poison == 1) {
+        SX_HIP(hipMemset(p, 0xFF, count * sizeof(T)));
+        SX_HIP(hipDeviceSynchronize());
+    }
     return p;
 }
 
@@ -292,6 +316,7 @@ struct Shard {
     hipStream_t s = nullptr;          // the engine's stream on that device (every per-shard operation)
     int urec = -1;                    // ga / gb / gdone: index of the uncached record set (g_urec), or -1
     bool fineU = false;               // U in fine-grained memory (peers on other devices write it)
+    bool Upool = false;               // U is one of the process's kept allocations (g_special)
     DevState *st = nullptr;
 };
 
@@ -682,6 +707,36 @@ class Engine {
         return (int)g_urec.size() - 1;
     }
 
+    // a free special allocation (g_special) of >= bytes on `dev` with `flags`, allocated after an L2
+    // write-back when none is free
+    static void *acquire_special(int dev, unsigned flags, size_t bytes, hipStream_t st) {
+        int best = -1;
+        for (size_t i = 0; i < g_special.size(); ++i) {
+            const SpecialBuf &b = g_special[i];
+            if (b.dev == dev && b.flags == flags && !b.busy && b.bytes >= bytes &&
+                (best < 0 || b.bytes < g_special[(size_t)best].bytes))
+                best = (int)i;
+        }
+        if (best >= 0) {
+            g_special[(size_t)best].busy = true;
+            return g_special[(size_t)best].p;
+        }
+        SpecialBuf b;
+        b.dev = dev;
+        b.flags = flags;
+        b.bytes = bytes;
+        sx_launch_l2_writeback(st);
+        SX_HIP(hipStreamSynchronize(st));
+        SX_HIP(hipExtMallocWithFlags(&b.p, bytes, flags));
+        b.busy = true;
+        g_special.push_back(b);
+        return b.p;
+    }
+    static void release_special(void *p) {
+        for (auto &b : g_special)
+            if (b.p == p) b.busy = false;
+    }
+
     // (on the shard's device)
     void alloc_shard(Shard &x) {
         const size_t rows_alloc = x.rows > 0 ? (size_t)x.rows : 1;
@@ -700,9 +755,13 @@ class Engine {
         // (with the replicated objective every rank forms the whole pivot row itself and no peer
         // writes U, once every batch of the solve fits that way)
         x.fineU = fu > 0 || (fu < 0 && ((rccl && !ipc) || multidev) && !repl_always());
-        if (x.fineU)
-            SX_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&x.U), (size_t)SX_KMAX * ld * sizeof(double),
-                                         hipDeviceMallocFinegrained));
+        // (SIMPLEX_DIAG_UNCACHED_U=1, diagnostic only: U of exchanging shards in uncached memory -- the
+        // allocation mode removed in round 4, kept reachable for the bisect of DESIGN.md §5.2)
+        const char *du = xchg ? getenv("SIMPLEX_DIAG_UNCACHED_U") : nullptr;
+        const unsigned uflags = du && atoi(du) == 1 ? hipDeviceMallocUncached : x.fineU ? hipDeviceMallocFinegrained : 0u;
+        x.Upool = uflags != 0u;
+        if (x.Upool)  // (kept for the process, g_special)
+            x.U = static_cast<double *>(acquire_special(x.dev, uflags, (size_t)SX_KMAX * ld * sizeof(double), x.s));
         else
             x.U = dalloc<double>((size_t)SX_KMAX * ld);
         x.d_save = dalloc<double>(round_up((size_t)N1, 16));
@@ -775,6 +834,11 @@ class Engine {
             x.ga = x.gb = x.gdone = nullptr;
             g_urec[(size_t)x.urec].busy = false;
             x.urec = -1;
+        }
+        if (x.Upool) {  // (U stays allocated for later engines, g_special)
+            release_special(x.U);
+            x.U = nullptr;
+            x.Upool = false;
         }
         for (void *p : {(void *)x.T, (void *)x.d, (void *)x.d_save, (void *)x.dx, (void *)x.colE, (void *)x.prow, (void *)x.prow_send,
                         (void *)x.slot_send, (void *)x.slot_all, (void *)x.U, (void *)x.F, (void *)x.recs, (void *)x.PM, (void *)x.PM2,
