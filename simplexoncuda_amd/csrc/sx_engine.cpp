@@ -119,7 +119,9 @@ std::vector<UncachedRecords> g_urec;
 // Round 5 found what the round-2/4 divergences share (profiles/r05_uncached_u_bisect.txt): W = 8
 // virtual-shard solves with uncached U diverge from one shard only after earlier engines have
 // freed such allocations -- the same code with every uncached U kept allocated was bit-exact in
-// 12 of 12 solves, with them freed it diverged in 4 of 12 -- so no engine frees one.
+// 12 of 12 solves, with them freed it diverged in 4 of 12 -- so no engine frees one.  The pool
+// holds at most the largest set of such buffers alive at once, plus one buffer each time a solve
+// needs a larger one than any free (a process solving one shape repeatedly reuses one set).
 struct SpecialBuf {
     int dev = -1;
     unsigned flags = 0;
