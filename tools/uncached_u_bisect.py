@@ -24,6 +24,8 @@ CASES = {
     "unc_rowmajor": (1, {"p2p": 0, "blocked": 0}, (300, 1100)),
     "unc_vsweep": (1, {"p2p": 0, "sweep_mfma": 0}, (300, 1100)),
     "unc_p2p": (1, {"p2p": 1}, (300, 1100)),
+    "fine": (0, {"p2p": 0, "fine": 1}, (300, 1100)),
+    "fine_p2p": (0, {"p2p": 1, "fine": 1}, (300, 1100)),
     "unc_full": (1, {"p2p": 0}, (300, 4000)),
     "ctl_full": (0, {"p2p": 0}, (300, 4000)),
     # (run with SIMPLEX_DIAG_POISON=1: every allocation starts as NaN / -1 -- reads before writes)
@@ -36,7 +38,8 @@ CASES = {
 def knobs(k):
     # (tolerant of older trees without some of the setters: the bisect also runs earlier commits)
     for name, val in (("set_p2p", k.get("p2p", -1)), ("set_compact", k.get("compact", 1)),
-                      ("set_blocked", k.get("blocked", -1)), ("set_sweep_mfma", k.get("sweep_mfma", -1))):
+                      ("set_blocked", k.get("blocked", -1)), ("set_sweep_mfma", k.get("sweep_mfma", -1)),
+                      ("set_fine_pivot_rows", k.get("fine", -1))):
         if hasattr(sx, name):
             getattr(sx, name)(val)
 
