@@ -59,6 +59,60 @@ REF_PIVOTS_PER_S = {"config3": 1e6 / 7607.5}  # (no published number for configs
 REF_SOLVE = {"config3": {"pivot_loop_s": 68.33 + 0.94, "pivots": [8981, 255]}}
 
 
+def _sha(a):
+    import hashlib
+
+    import numpy as np
+    return hashlib.sha256(memoryview(np.ascontiguousarray(a)).cast("B")).hexdigest()
+
+
+def _golden(name):
+    path = os.path.join(ROOT, "tests", "golden", name)
+    if not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        return json.load(f)
+
+
+def window_parity(config, pivots, d, base):
+    """The timed run's own end state against the CPU oracle's pin at the same pivot count
+    (tests/golden/long_pivots.json, tests/golden/scripts/make_long_pins.py): d[0]'s bits and the
+    SHA-256 of the objective row and the basis (the tableau's digest is checked by
+    tests/test_gpu_large.py); None when no pin sits at this pivot count."""
+    rec = _golden("long_pivots.json").get(config)
+    if not rec:
+        return None
+    pin = [c for c in rec["checkpoints"] if c.get("phase", 1) == 1 and c["pivots"] == pivots]
+    if not pin:
+        return None
+    pin = pin[0]
+    ok = {"d0_bits": float(d[0]).hex() == pin["d0_hex"], "objective_row_sha256": _sha(d) == pin["sha256_d"],
+          "basis_sha256": _sha(base) == pin["sha256_base"]}
+    return {"pivots": pivots, "oracle_pin": f"tests/golden/long_pivots.json[{config}] at pivot {pivots}",
+            "match": all(ok.values()), **ok}
+
+
+def solve_parity(name, res):
+    """A whole twoPhaseMethod against the CPU oracle's whole-solve pin (status, pivot counts, the
+    objective's bits, SHA-256 of basis and solution), where one exists."""
+    pin = _golden("oracle_solves.json").get(name)
+    src = "tests/golden/oracle_solves.json"
+    if pin is None:
+        r = (_golden("long_pivots.json").get(name) or {}).get("result")
+        if r and "opt_hex" in r:
+            pin = {"status": r["status"], "pivots": r["pivots"], "opt_hex": r["opt_hex"],
+                   "base_sha256": r["sha256_base"], "x_sha256": r["sha256_x"]}
+            src = "tests/golden/long_pivots.json"
+    if pin is None:
+        return None
+    import numpy as np
+    ok = {"status": res.status == pin["status"], "pivots": list(res.pivots) == list(pin["pivots"]),
+          "objective_bits": float(res.optimal_value).hex() == pin["opt_hex"],
+          "basis_sha256": _sha(np.asarray(res.base, dtype=np.int32)) == pin["base_sha256"],
+          "solution_sha256": _sha(np.asarray(res.solution, dtype=np.float64)) == pin["x_sha256"]}
+    return {"oracle_pin": f"{src}[{name}]", "match": all(ok.values()), **ok}
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -196,6 +250,10 @@ def main():
             tt = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             elapsed = float(tt.item())
+        parity = None
+        if world == 1:  # (outside the timed region: the run's own end state vs the oracle's pin)
+            d_end, base_end = sess.objective_row_and_basis(m, 1 + n + 2 * m)
+            parity = window_parity(config, (warmup + steps) * K, d_end, base_end)
         # per-rank split of the pivot time: this rank's timed sweeps vs the rest (the chain: the
         # fused batches, slack exchanges and launch gaps), from its own HIP events
         mine = {"rank": rank, "rows": tim.local_rows, "pivots": tim.pivots,
@@ -213,7 +271,7 @@ def main():
         achieved = tim.swept_bytes / (tim.update_ms / 1e3) / 1e9 if tim.update_launches else None
         return {"n": n, "m": m, "seed": seed, "tim": tim, "elapsed": elapsed, "pivots": tim.pivots,
                 "avg_update_s": avg_update_s, "achieved": achieved, "setup_s": t_setup,
-                "steps": steps, "warmup": warmup, "per_rank": per_rank, "K": K}
+                "steps": steps, "warmup": warmup, "per_rank": per_rank, "K": K, "parity": parity}
 
     def roofline(cfg, r):
         tim, achieved = r["tim"], r["achieved"]
@@ -311,6 +369,7 @@ def main():
             "pivots_timed": pivots, "first_timed_pivot": args.warmup * K, "status_after": tim.status,
             "setup_s": r["setup_s"],
         },
+        "parity": r["parity"],
         "roofline": roofline(args.config, r),
         "cpu_baseline": None,
     }
@@ -391,7 +450,8 @@ def main():
                     "objective": res.optimal_value,
                     "note": "twoPhaseMethod wall time incl. tableau build from host arrays, both phases and the solution",
                     "pivot_loop_s": [ph[0], ph[1]],
-                    "pivots_per_s": [res.pivots[k] / ph[k] if ph[k] > 0 else None for k in (0, 1)]}
+                    "pivots_per_s": [res.pivots[k] / ph[k] if ph[k] > 0 else None for k in (0, 1)],
+                    "parity": solve_parity(name, res)}
             if name in REF_SOLVE:
                 full["reference_pivots_per_s"] = [8981 / 68.33, 255 / 0.94]  # RTX 2070S, BASELINE.md §1
                 full["reference_pivot_loop_s"] = REF_SOLVE[name]["pivot_loop_s"]

@@ -127,6 +127,12 @@ void simplex_set_blocked(int mode);
  * undone and re-run on the per-pivot path; this counts such recoveries in the process */
 long long simplex_hang_recoveries(void);
 long long simplex_fused_batches(void);           /* fused batch launches in the process */
+/* diagnostic: before every sweep of a multi-shard engine of this process (virtual shards, a
+ * SIMPLEX_GPUS list), compare every shard's pending pivot rows U with shard 0's bit for bit and
+ * count (and print the first) mismatches -- 1 on, 0 off (default; SIMPLEX_CHECK_PIVOT_ROWS=1 also
+ * turns it on).  Synchronous per batch: for tests and diagnosis, not for timing */
+void simplex_set_check_pivot_rows(int on);
+long long simplex_pivot_row_mismatches(void);    /* mismatches counted in the process */
 /* test hook: make the n-th fused batch from now abort as if a wait had timed out (-1 off) */
 void simplex_set_hang_inject(long long batches);
 /* ... at which slot of that batch: -1 (default) before it starts; s >= 0: the batch runs s
@@ -183,9 +189,9 @@ simplex_session *simplex_session_open_generated(int n, int m, unsigned int seed,
  * time_updates = s > 0 brackets every s-th sweep with HIP events */
 int simplex_session_pivots(simplex_session *s, long long k, int time_updates, simplex_timing_t *out);
 double simplex_session_objective(simplex_session *s);   /* d[0] */
-/* the resident tableau in logical column order (m rows of the phase's width at stride ld),
- * the objective row d and the basis; returns the width, or -1 when rows live on other ranks
- * or the buffer is too narrow */
+/* the resident tableau in logical column order (m rows of the phase's width at stride ld; T
+ * null: not copied), the objective row d and the basis; returns the width, or -1 when rows live
+ * on other ranks or the buffer is too narrow */
 long long simplex_session_tableau(simplex_session *s, double *T, long long ld, double *d, int *base);
 /* slack columns the sweeps currently move (m without slack compaction) */
 long long simplex_session_active_slacks(simplex_session *s);

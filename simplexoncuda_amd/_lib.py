@@ -108,6 +108,8 @@ SIGNATURES = {
     "simplex_set_mr_single_launch": (None, [ctypes.c_int]),
     "simplex_hang_recoveries": (ctypes.c_longlong, []),
     "simplex_fused_batches": (ctypes.c_longlong, []),
+    "simplex_set_check_pivot_rows": (None, [ctypes.c_int]),
+    "simplex_pivot_row_mismatches": (ctypes.c_longlong, []),
     "simplex_set_hang_inject": (None, [ctypes.c_longlong]),
     "simplex_set_hang_inject_slot": (None, [ctypes.c_int]),
     "simplex_set_first_batch_id": (None, [ctypes.c_uint]),

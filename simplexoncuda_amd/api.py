@@ -243,6 +243,15 @@ class Session:
             raise RuntimeError(f"simplex_session_tableau: width {w}, expected {width}")
         return T, d, base
 
+    def objective_row_and_basis(self, m, width):
+        """(d, base) without the tableau (simplex_session_tableau with T null)."""
+        d = np.zeros(width, dtype=np.float64)
+        base = np.zeros(m, dtype=np.int32)
+        w = self._lib.simplex_session_tableau(self._h, None, width, _dp(d), _ip(base))
+        if w != width:
+            raise RuntimeError(f"simplex_session_tableau: width {w}, expected {width}")
+        return d, base
+
     def active_slacks(self):
         """Slack columns the sweeps move (m without slack compaction)."""
         return self._lib.simplex_session_active_slacks(self._h)

@@ -78,7 +78,15 @@ struct __attribute__((aligned(16))) PivRec {
 // Device buffers of the pending pivots of a shard, plus the batch id and slot of the pivot
 // being enqueued (kernel arguments).
 struct Pending {
-    double *U;               // [SX_KMAX][ld] pivot rows (current leaving-row values, before /p)
+    // [SX_KMAX][ld] pivot rows (current leaving-row values, before /p).  INVARIANT every writer keeps
+    // (k_pivot_row, k_batch / k_batch_mr objective tiles, k_select_row / the row gathers' remote
+    // rows, k_activate / activate_block's column exchanges): U[s][j] is the EXACT current value of
+    // row r_s at stored column j < Ns just before slot s -- the reference's bits -- for every stored
+    // column the sweep touches.  The sweep's leaving-row fix-up (msweep_fixup) and the ratio tiles'
+    // leaving-row shortcut restart a row that left at slot sl from U[sl][j] / p_sl instead of its
+    // stored value, so they are correct only under this invariant
+    // (tests/test_gpu_parity.py::test_row_leaves_twice_per_stage_compacted).
+    double *U;
     double *F;               // row factors -(a_ie / p), F[sx_fidx(i, s)]
     PivRec *recs;            // [SX_KMAX]
     unsigned long long *PM;  // [rows] (batch id << 32) | slots < SX_HMAX where the row left the basis
@@ -238,6 +246,9 @@ void sx_set_update_waves(float w);  // resident-grid multiple of the sweep (defa
 void sx_set_sweep_record(int *rec);  // next sweeps write (batch tag, count, nact) to rec[0..2] (null: off)
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s);
 void sx_launch_l2_writeback(hipStream_t s);  // every XCD's L2 writes back its dirty lines
+// diagnostic: every shard's pending pivot rows of batch B against shard 0's (counts mismatches in *bad)
+void sx_launch_check_u(const PeerView &pv, int W, size_t ld, int Ns, const DevState *st, unsigned B,
+                       unsigned long long *bad, hipStream_t s);
 // a rank's contribution to the objective-row gather: d on [j0, j1) (and d[0] if with0), -0.0 elsewhere
 void sx_launch_d_contrib(const double *d, double *out, int N, int j0, int j1, int with0, hipStream_t s);
 

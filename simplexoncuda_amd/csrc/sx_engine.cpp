@@ -71,6 +71,13 @@ struct Config {
     int p2p = -1;            // several shards: fused batches exchanging over peer memory: -1 auto, 0 off, 1 force
     bool p2p_ready = false;  // RCCL ranks: the peer-memory path passed the start-up self-check
     std::map<std::vector<int>, int> gpus_checked;  // one process, several GPUs: self-check result per device list
+    // ... of a check run with peer memory off (simplex_set_p2p(0): only the per-pivot exchange checked, so
+    // its result says nothing about the peer-memory batches and is not reused once they are enabled)
+    std::map<std::vector<int>, int> gpus_checked_xchg;
+    // diagnostic (simplex_set_check_pivot_rows / SIMPLEX_CHECK_PIVOT_ROWS=1): before every sweep of
+    // a multi-shard engine of this process, every shard's pending pivot rows against shard 0's
+    int check_u = -1;
+    long long u_mismatches = 0;
     bool single_shard = false;  // every engine one shard on its own device (self-check reference; the
                                 // fallback when the shards' exchange failed the self-check)
     int debug = -1;          // -1: from SIMPLEX_DEBUG; 1: print the tableau after every step
@@ -361,6 +368,9 @@ class Engine {
     unsigned long long *stamps = nullptr;  // diagnostic: in-kernel timestamps of the fused batch
     long long sweeps = 0;
     std::function<void(int)> on_pivot;  // DEBUG trace: called after every pivot (solver.cu:112-116)
+    // split (not replicated) multi-rank batches may run fused: every shard's U is fine-grained, or no
+    // shard's U can be written from another device (decided once, when the shards are allocated)
+    bool split_ok = true;
 
     Engine(int n_, int m_, bool alias_ = true) : n(n_), m(m_) {
         N1 = 1 + n + 2 * m;
@@ -451,6 +461,8 @@ class Engine {
             alloc_shard(x);
             sh.push_back(x);
         }
+        if ((rccl && !ipc) || multidev)
+            for (const auto &x : sh) split_ok = split_ok && x.fineU;
         if (!rccl && xchg) {
             // the shards' pivot-row contributions (pinned host memory: read by every device's kernel)
             SX_HIP(hipHostMalloc(reinterpret_cast<void **>(&sum_srcs), sizeof(double *) * W, hipHostMallocDefault));
@@ -671,6 +683,7 @@ class Engine {
         }
         if (sum_srcs) (void)hipHostFree(sum_srcs);
         if (c_dev) (void)hipFree(c_dev);
+        if (u_bad) (void)hipFree(u_bad);
         if (st_host) (void)hipHostFree(st_host);
         for (auto &e : poll_ev)
             if (e) (void)hipEventDestroy(e);
@@ -993,8 +1006,11 @@ class Engine {
 
     void gather_d() {
         if (!d_split) return;
+        // IPC ranks (a test mode) cannot gather here: the row is whole only after every process has
+        // called simplex_session_sync_d.  A kernel that needs it before then would read a stale
+        // split row -- refuse loudly instead (and keep d_split, so reads stay refused too).
+        if (ipc) SX_FATAL("IPC session: the objective row is split between ranks (simplex_session_sync_d first)");
         d_split = false;
-        if (ipc) return;
         if (rccl) {
             Shard &x = sh[0];
             if (!x.dx) x.dx = dalloc<double>(round_up((size_t)N1, 16));
@@ -1231,6 +1247,7 @@ class Engine {
         if (!p2p) return false;
         const int NBg = (N - 1 + SX_TILE - 1) / SX_TILE;
         if (repl_now(k)) return true;
+        if (!split_ok) return false;  // (peers would write a plain U across devices: the per-pivot path)
         return sx_batch_mr_fits(slots, (NBg + W - 1) / W, k, mr_grids());
     }
 
@@ -1250,9 +1267,16 @@ class Engine {
     // several GPUs), where the objective hop is an xGMI hop; forced on or off by
     // simplex_set_replicated_objective.  Used for a batch when its grid (slots + every objective
     // tile per rank) fits, else the split objective.
+    // In IPC mode (one process per rank, peers connected by the caller) d is gathered only by
+    // simplex_session_sync_d, so a replicated batch could start from a stale split row: never there.
+    // When some shard's U is plain memory while its peers sit on other devices (split_ok false: the
+    // allocation-time decision, alloc_shard), only replicated batches -- no peer writes U -- may run
+    // fused, whatever simplex_set_replicated_objective says now.
     bool repl_mode() const {
-        if (W < 2 || g_cfg.repl_obj == 0) return false;
-        return g_cfg.repl_obj > 0 || (rccl && !ipc) || multidev;
+        if (W < 2 || ipc) return false;
+        if (!split_ok) return true;
+        if (g_cfg.repl_obj == 0) return false;
+        return g_cfg.repl_obj > 0 || rccl || multidev;
     }
     bool repl_now(int k) const {
         return repl_mode() && sx_batch_mr_fits(slots, (N - 1 + SX_TILE - 1) / SX_TILE, k, mr_grids());
@@ -1363,6 +1387,7 @@ class Engine {
                 sx_launch_activate(x.perm, x.iperm, x.act, x.nact, m, x.T, x.rows, x.row0, ld, tl, 1 + n, pending(x), x.st,
                                    q_host, x.s);
             }
+        if (check_u_on()) check_pivot_rows();
         if (ev0) SX_HIP(hipEventRecord(ev0, s));
         for (auto &x : sh) {
             DevGuard g(x.dev);
@@ -1376,6 +1401,35 @@ class Engine {
         q_host = 0;
         batch_activated = false;
         if (++batch_id >= SX_BATCH_IDS) wrap_batch_ids();
+    }
+
+    // the pivot-row check (diagnostic): shards of this process only -- RCCL ranks' peers start their
+    // next batch, which writes into this rank's U, while a check here would still read
+    unsigned long long *u_bad = nullptr;
+    bool check_u_on() const {
+        if (g_cfg.check_u < 0) {
+            const char *e = getenv("SIMPLEX_CHECK_PIVOT_ROWS");
+            g_cfg.check_u = e && atoi(e) == 1 ? 1 : 0;
+        }
+        return g_cfg.check_u == 1 && W > 1 && !rccl && q_host > 0;
+    }
+    void check_pivot_rows() {
+        DevGuard g(device);
+        PeerView v;
+        std::memset(&v, 0, sizeof(v));
+        for (auto &x : sh) v.U[x.rank] = x.U;
+        if (!u_bad) {
+            u_bad = dalloc<unsigned long long>(1);
+            SX_HIP(hipMemsetAsync(u_bad, 0, sizeof(unsigned long long), s));
+        }
+        join();
+        sx_launch_check_u(v, W, ld, cols(N).Ns, sh[0].st, batch_id, u_bad, s);
+        unsigned long long bad = 0;
+        SX_HIP(hipMemcpyAsync(&bad, u_bad, sizeof(bad), hipMemcpyDeviceToHost, s));
+        SX_HIP(hipMemsetAsync(u_bad, 0, sizeof(unsigned long long), s));
+        SX_HIP(hipStreamSynchronize(s));
+        join();
+        g_cfg.u_mismatches += (long long)bad;
     }
 
     // The granule tags keep 15 bits of the batch id ([id | slot (6) | payload (11)],
@@ -1485,7 +1539,7 @@ class Engine {
                 if (st != SX_NOT_ENDED) break;
             }
         }
-        gather_d();
+        if (!ipc) gather_d();  // (IPC ranks: the caller's simplex_session_sync_d)
         sync_all();  // (one synchronous call: every device's work is done)
         DevState f = read_state();
         if (timed) {
@@ -1584,7 +1638,7 @@ class Engine {
         }
         const int s0 = 1 + n;
         for (auto &x : sh) {
-            if (x.rows <= 0) continue;
+            if (x.rows <= 0 || T_host == nullptr) continue;  // (null: the objective row alone)
             tmp.assign((size_t)x.rows * c.Ns, 0.0);
             const int wa = std::min(c.Ns, tl.jB);  // region A's columns, then region B's
             DevGuard g(x.dev);
@@ -1890,12 +1944,14 @@ int selftest_solves(int W, int ref_dev) {
 // decides how the list is used: 2 peer-memory fused batches, 1 the per-pivot
 // exchange, 0 not at all (every solve on the list's first device).  -1 while the check runs.
 int gpus_check(const std::vector<int> &devs) {
-    auto it = g_cfg.gpus_checked.find(devs);
-    if (it != g_cfg.gpus_checked.end()) return it->second;
-    g_cfg.gpus_checked[devs] = -1;  // (the check's own engines run the list)
+    const bool with_p2p = g_cfg.p2p != 0;
+    auto &done = with_p2p ? g_cfg.gpus_checked : g_cfg.gpus_checked_xchg;
+    auto it = done.find(devs);
+    if (it != done.end()) return it->second;
+    done[devs] = -1;  // (the check's own engines run the list)
     const int code = selftest_solves((int)devs.size(), devs[0]);
-    g_cfg.gpus_checked[devs] = code;
-    if (code == 1)
+    done[devs] = code;
+    if (code == 1 && with_p2p)  // (with peer memory off, 1 is the best a check can return)
         fprintf(stderr, "simplex: peer-memory fused batches disagree with the one-shard answer on these GPUs; "
                         "using the per-pivot exchange\n");
     if (code == 0)
@@ -1946,8 +2002,9 @@ int simplex_p2p_ready(void) {
 int simplex_multi_gpu_mode(void) {
     const std::vector<int> v = g_cfg.dist ? std::vector<int>() : shard_devices();
     if (v.size() > 1) {
-        auto it = g_cfg.gpus_checked.find(v);
-        return it == g_cfg.gpus_checked.end() ? -1 : it->second;
+        const auto &done = g_cfg.p2p != 0 ? g_cfg.gpus_checked : g_cfg.gpus_checked_xchg;
+        auto it = done.find(v);
+        return it == done.end() ? -1 : it->second;
     }
     if (!g_cfg.dist) return -1;
     return g_cfg.single_shard ? 0 : g_cfg.p2p_ready ? 2 : 1;
@@ -1971,6 +2028,8 @@ long long simplex_hang_recoveries(void) { return g_cfg.hang_recoveries; }
 long long simplex_fused_batches(void) { return g_cfg.fused_batches; }
 void simplex_set_fine_pivot_rows(int mode) { g_cfg.fine_u = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_replicated_objective(int mode) { g_cfg.repl_obj = mode < 0 ? -1 : (mode ? 1 : 0); }
+void simplex_set_check_pivot_rows(int on) { g_cfg.check_u = on ? 1 : 0; }
+long long simplex_pivot_row_mismatches(void) { return g_cfg.u_mismatches; }
 void simplex_set_blocked(int mode) { g_cfg.blocked = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_first_batch_id(unsigned int id) { g_cfg.first_batch_id = (id >= 1 && id < SX_BATCH_IDS) ? id : 1; }
 
@@ -2001,7 +2060,7 @@ static void p2p_selftest() {
     (void)hipFree(dv);
     g_cfg.p2p_ready = code == 2 && g_cfg.p2p != 0 && g_cfg.world <= SX_MAXW;
     g_cfg.single_shard = code == 0;
-    if (code == 1 && g_cfg.rank == 0)
+    if (code == 1 && g_cfg.p2p != 0 && g_cfg.rank == 0)  // (peer memory off: only the exchange was checked)
         fprintf(stderr, "simplex: peer-memory fused batches disagree with the one-shard answer; using RCCL\n");
     if (code == 0 && g_cfg.rank == 0)
         fprintf(stderr, "simplex: the RCCL exchange disagrees with the one-shard answer; every rank solves alone\n");
@@ -2237,7 +2296,7 @@ int simplex_session_pivots(simplex_session *S, long long k, int time_updates, si
     (void)hipEventDestroy(w0);
     (void)hipEventDestroy(w1);
     S->total = f.pivots;
-    E.gather_d();  // (outside the timed region: the whole objective row on every shard)
+    if (!E.ipc) E.gather_d();  // (outside the timed region: the whole objective row on every shard)
     E.sync_all();
     if (out) *out = t;
     return f.status;
@@ -2278,7 +2337,7 @@ int simplex_session_block_stamps(simplex_session *S, int k, unsigned long long *
     E.enqueue_batch(k);
     E.stamps = nullptr;
     E.enqueue_sweep();
-    E.gather_d();
+    if (!E.ipc) E.gather_d();
     E.sync_all();
     SX_HIP(hipMemcpyAsync(out, dev, sizeof(unsigned long long) * k * 8, hipMemcpyDeviceToHost, E.s));
     if (blk && cap >= (long long)((size_t)k * nb * 4))

@@ -3317,6 +3317,34 @@ __global__ void k_l2_writeback() {
 }
 void sx_launch_l2_writeback(hipStream_t s) { k_l2_writeback<<<4096, 64, 0, s>>>(); }
 
+// Diagnostic (simplex_set_check_pivot_rows): before the sweep reads them, every
+// shard's copy of the batch's pending pivot rows U[q][0..Ns) must equal shard 0's bit for bit -- in
+// every exchange form each rank holds the same rows (split objective: written into every rank by
+// the tile owners; replicated: formed by every rank; per-pivot exchange: copied from one summed
+// row).  Loads are system-scope (peer copies on other GPUs are read over xGMI).  A mismatch is
+// counted in *bad and the first one printed (batch, slot, shard, column, both values' bits).
+__global__ void k_check_u(PeerView pv, int W, size_t ld, int Ns, const DevState *__restrict__ st, unsigned B,
+                          unsigned long long *bad) {
+    const int cnt = st->batch_tag == B ? st->batch_count : 0;
+    const long long total = (long long)cnt * Ns;
+    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < total;
+         k += (long long)gridDim.x * blockDim.x) {
+        const int q = (int)(k / Ns), j = (int)(k - (long long)q * Ns);
+        const u64 a = ld_sys(reinterpret_cast<const u64 *>(pv.U[0] + (size_t)q * ld + j));
+        for (int r = 1; r < W; ++r) {
+            const u64 b = ld_sys(reinterpret_cast<const u64 *>(pv.U[r] + (size_t)q * ld + j));
+            if (a != b && atomicAdd(bad, 1ull) == 0ull)
+                printf("simplex: pivot-row copies differ: batch %u slot %d shard %d column %d: %016llx vs shard 0 %016llx\n",
+                       B, q, r, j, (unsigned long long)b, (unsigned long long)a);
+        }
+    }
+}
+
+void sx_launch_check_u(const PeerView &pv, int W, size_t ld, int Ns, const DevState *st, unsigned B,
+                       unsigned long long *bad, hipStream_t s) {
+    k_check_u<<<1024, 256, 0, s>>>(pv, W, ld, Ns, st, B, bad);
+}
+
 void sx_launch_sum_rows(double *out, const double *const *srcs, int nsrc, int N, hipStream_t s) {
     int g = (N + 255) / 256;
     if (g > 1024) g = 1024;

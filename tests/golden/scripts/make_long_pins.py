@@ -143,7 +143,7 @@ def main():
             save_rec(name, rec)
             if whole and (ended or cp >= 5000):
                 save_state(name, T, d, base, k, 1, rec)
-            if ended or not whole or cp == cps[-1]:
+            if ended or cp == cps[-1]:
                 break
         if not whole:
             return

@@ -1,13 +1,16 @@
 """Shards that own no rows, solved again and again in one process (needs an MI355X).
 
 Round 4's bisect saw W = 8 virtual-shard solves of a 1,100-row instance diverge from one shard
-when the pending pivot rows U were allocated uncached.  Round 5 re-ran it: on
-the current code it never diverges (uncached, fine-grained or plain U; per-pivot exchange or
-peer-memory batches), while be1d656^/be1d656 rebuilt on the same box still did in 2 of 3
-repetitions -- only from the process's second W = 8 solve on, and only on instances where
-512-row blocks leave shards empty (1,100 rows at W = 8: shards 3..7 own no rows;
-profiles/r05_uncached_u_bisect.txt).  This file keeps exactly those conditions -- empty shards,
-repeated solves in one process, each U allocation mode -- in the default GPU suite.
+when the pending pivot rows U were allocated uncached.  Round 5 re-ran it
+(profiles/r05_uncached_u_bisect.txt): be1d656^/be1d656 rebuilt on one box still diverged, from the
+process's second multi-shard solve on, at W = 8 (1,100 rows: shards 3..7 own no rows) and also at
+W = 2 (shards of 1,024 and 76 rows: no empty shard; status -3 after 417 and 529 pivots), and
+HEAD itself failed this file's uncached case before every non-plain U was pooled for the process
+(pivots (1321, 63) instead of (1318, 79)).  With the pool (sx_engine.cpp g_special: no engine
+frees a fine-grained or uncached allocation) these tests pass.  This file keeps the conditions --
+repeated solves in one process, empty and non-empty shards, each U allocation mode -- in the
+default GPU suite, with the pivot-row check on (simplex_set_check_pivot_rows: every shard's U
+against shard 0's before every sweep, no mismatch allowed).
 Bar: bit-exact against the oracle's whole two-phase solve (solver.cu:78-149,
 twoPhaseMethod.cu:385-435).
 """
@@ -35,6 +38,8 @@ def test_empty_shards_repeated_solves(gpu, monkeypatch, umode, p2p):
     if umode == "uncached":  # (diagnostic allocation, sx_engine.cpp alloc_shard)
         monkeypatch.setenv("SIMPLEX_DIAG_UNCACHED_U", "1")
     lib.simplex_set_fine_pivot_rows(1 if umode == "fine" else 0)
+    lib.simplex_set_check_pivot_rows(1)
+    bad0 = lib.simplex_pivot_row_mismatches()
     sx.set_p2p(p2p)
     try:
         for rep in range(3):
@@ -52,6 +57,8 @@ def test_empty_shards_repeated_solves(gpu, monkeypatch, umode, p2p):
                 assert np.array_equal(got.base, ref["base"]), where
                 assert np.array_equal(bits(got.optimal_value), bits(ref["opt"])), where
                 assert np.array_equal(bits(got.solution), bits(ref["x"])), where
+                assert lib.simplex_pivot_row_mismatches() == bad0, where
     finally:
+        lib.simplex_set_check_pivot_rows(0)
         lib.simplex_set_fine_pivot_rows(-1)
         sx.set_p2p(-1)

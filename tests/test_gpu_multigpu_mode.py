@@ -62,6 +62,41 @@ def test_unchanged_caller_gets_shards_from_env(gpu, gpus, repl, n, m, seed, lo, 
     assert got["p2p_ready"] == 1 and got["fused"] > 0 and got["hangs"] == 0
 
 
+CHILD_P2P_OFF_ON = r"""
+import sys, json
+sys.path.insert(0, {root!r})
+import simplexoncuda_amd as sx
+lib = sx.load()
+out = {{}}
+for mode in (0, -1):
+    sx.set_p2p(mode)
+    f0 = lib.simplex_fused_batches()
+    r = sx.twoPhaseMethodEx(sx.generateRandomProblem(300, 1100, 41100, 1, 100))
+    out[str(mode)] = {{"status": r.status, "pivots": list(r.pivots), "mode": lib.simplex_multi_gpu_mode(),
+                      "p2p_ready": lib.simplex_p2p_ready(), "fused": lib.simplex_fused_batches() - f0}}
+print(json.dumps(out))
+"""
+
+
+def test_self_check_with_peer_memory_off_then_on(gpu):
+    """simplex_set_p2p(0) checks only the per-pivot exchange: that result (1) must not be reused once
+    peer memory is enabled again -- the next solve runs the full check and the peer-memory batches
+    """
+    import json
+    env = dict(os.environ, SIMPLEX_GPUS="0,0")
+    r = subprocess.run([sys.executable, "-c", CHILD_P2P_OFF_ON.format(root=ROOT)], capture_output=True, text=True,
+                       env=env, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "disagree" not in r.stderr
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    A, b, c = oracle.generate(300, 1100, 41100, 1, 100)
+    ref = two_phase_ref(A, b, c)
+    for mode in ("0", "-1"):
+        assert got[mode]["status"] == ref["status"] and tuple(got[mode]["pivots"]) == ref["pivots"]
+    assert got["0"]["mode"] == 1 and got["0"]["p2p_ready"] == 0
+    assert got["-1"]["mode"] == 2 and got["-1"]["p2p_ready"] == 1 and got["-1"]["fused"] > 0
+
+
 def test_missing_device_is_fatal(gpu):
     import torch
     n_vis = torch.cuda.device_count()

@@ -502,6 +502,44 @@ def test_fused_history_chains(gpu, W, case):
     assert same(Tg, ref[0]) and same(dg, ref[1]) and np.array_equal(bg, ref[2])
 
 
+@pytest.mark.parametrize("W,repl", [(1, -1), (2, 0), (2, 1)])
+def test_row_leaves_twice_per_stage_compacted(gpu, W, repl):
+    """the U invariant the leaving-row restarts rely on (sx_common.hpp Pending::U): a generated
+    instance (slack compaction active) whose row 1334 leaves at pivots 394, 420, 427 and 476, 496,
+    506 -- twice or more inside both stages of 64-pivot batches (slots 10 / 36 / 43, 28 / 48 / 58) --
+    and which lies on shard 1 at W = 2 (rows 1024..1535), while the split objective tiles that form
+    its pivot rows sit on both ranks (repl 0) or on every rank (repl 1); 512 pivots against the oracle
+    bit for bit, every batch fused"""
+    n, m, seed, k = 16, 1536, 142542, 512
+    T, d, base = _phase1_state(n, m, seed)
+    st_o, done_o = oracle.solve(T, d, base, max_pivots=k)
+    lib = sx.load()
+    h0, f0 = lib.simplex_hang_recoveries(), lib.simplex_fused_batches()
+    bad0 = lib.simplex_pivot_row_mismatches()
+    sx.set_virtual_ranks(W)
+    sx.set_p2p(1 if W > 1 else -1)
+    sx.set_batch(64)
+    sx.set_replicated_objective(repl)
+    lib.simplex_set_check_pivot_rows(1)
+    try:
+        sess = sx.Session(generated=(n, m, seed, 1, 100))
+        tim = sess.pivots(k)
+        act = sess.active_slacks()
+        Tg, dg, bg = sess.tableau(m, T.shape[1])
+        sess.close()
+    finally:
+        lib.simplex_set_check_pivot_rows(0)
+        sx.set_replicated_objective(-1)
+        sx.set_batch(0)
+        sx.set_p2p(-1)
+        sx.set_virtual_ranks(1)
+    assert lib.simplex_pivot_row_mismatches() == bad0  # (every rank's U equal before every sweep)
+    assert done_o == k and tim.pivots == k
+    assert act < m  # (compaction active: only the slacks of rows that left are swept)
+    assert lib.simplex_fused_batches() >= f0 + k // 64 and lib.simplex_hang_recoveries() == h0
+    assert np.array_equal(bg, base) and same(dg, d) and same(Tg, T)
+
+
 @pytest.mark.parametrize("batch", [4, 16])
 @pytest.mark.parametrize("W", [2, 3])
 def test_batched_virtual_ranks(gpu, batch, W):
