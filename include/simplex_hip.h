@@ -108,7 +108,8 @@ void simplex_set_mr_single_launch(int on);
 
 /* the pending pivot rows U (written by peer ranks in the multi-rank batch) in fine-grained memory:
  * -1 auto (when the shards span devices, default), 1 always (test hook: the one-GPU cost and
- * parity of that path), 0 never */
+ * parity of that path), 0 never; 2 (test hook): uncached memory for exchanging shards, the
+ * allocation of the round-4/5 divergence */
 void simplex_set_fine_pivot_rows(int mode);
 /* multi-rank fused batches with the objective row replicated: every rank runs every objective
  * tile (decides the entering variable and forms the whole pivot row itself), so a pivot's only

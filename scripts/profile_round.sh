@@ -1,12 +1,12 @@
 #!/bin/bash
-# Round-5 profiles of the final code: rocprofv3 kernel trace + HBM counters (FETCH_SIZE / WRITE_SIZE
+# Profiles of the final code of a round: rocprofv3 kernel trace + HBM counters (FETCH_SIZE / WRITE_SIZE
 # in passes of their own) + SQ counters of the driver's bench command (config 5), the same for
 # config 3 alone, and the HBM counters of the synthetic update bench.  Each step under its own time
 # limit; a failure ends the script.  Summaries: scripts/profile_bench.py, tools/pmc_summary.py.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=${PROF_OUT:-gpurun_out/prof_r05}
+O=${PROF_OUT:-gpurun_out/prof}
 mkdir -p $O
 step() {
     local name=$1 secs=$2; shift 2

@@ -152,16 +152,6 @@ T *dalloc(size_t count) {
     T *p = nullptr;
     if (count == 0) count = 1;
     SX_HIP(hipMalloc(reinterpret_cast<void **>(&p), count * sizeof(T)));
-    // (SIMPLEX_DIAG_POISON=1, diagnostic only: every engine allocation starts as all-ones bytes --
-    // NaN doubles, -1 integers -- so a read before the first write shows in the result)
-    static const int poison = [] {
-        const char *e = getenv("SIMPLEX_DIAG_POISON");
-        return e ? atoi(e) : 0;
-    }();
-    if (poison == 1) {
-        SX_HIP(hipMemset(p, 0xFF, count * sizeof(T)));
-        SX_HIP(hipDeviceSynchronize());
-    }
     return p;
 }
 
@@ -763,17 +753,17 @@ class Engine {
         // L2: DESIGN.md §5); on one device, or when forced off, plain device memory.
         x.d = dalloc<double>(round_up((size_t)N1, 16));
         int fu = g_cfg.fine_u;
-        if (fu < 0) {  // (SIMPLEX_FINE_PIVOT_ROWS=0/1 overrides the default, as simplex_set_fine_pivot_rows)
+        if (fu < 0) {  // (SIMPLEX_FINE_PIVOT_ROWS=0/1/2 overrides the default, as simplex_set_fine_pivot_rows)
             const char *e = getenv("SIMPLEX_FINE_PIVOT_ROWS");
-            if (e) fu = atoi(e) != 0 ? 1 : 0;
+            if (e) fu = atoi(e);
         }
         // (with the replicated objective every rank forms the whole pivot row itself and no peer
         // writes U, once every batch of the solve fits that way)
-        x.fineU = fu > 0 || (fu < 0 && ((rccl && !ipc) || multidev) && !repl_always());
-        // (SIMPLEX_DIAG_UNCACHED_U=1, diagnostic only: U of exchanging shards in uncached memory -- the
-        // allocation mode removed in round 4, kept reachable for the bisect of DESIGN.md §5.2)
-        const char *du = xchg ? getenv("SIMPLEX_DIAG_UNCACHED_U") : nullptr;
-        const unsigned uflags = du && atoi(du) == 1 ? hipDeviceMallocUncached : x.fineU ? hipDeviceMallocFinegrained : 0u;
+        // (test hook, fu == 2: U of exchanging shards in uncached memory -- the allocation of the
+        // round-4/5 divergence, DESIGN.md §5.2, kept reachable for tests/test_gpu_empty_shards.py)
+        const bool uncU = fu == 2 && xchg;
+        x.fineU = fu == 1 || (fu < 0 && ((rccl && !ipc) || multidev) && !repl_always());
+        const unsigned uflags = uncU ? hipDeviceMallocUncached : x.fineU ? hipDeviceMallocFinegrained : 0u;
         x.Upool = uflags != 0u;
         if (x.Upool)  // (kept for the process, g_special)
             x.U = static_cast<double *>(acquire_special(x.dev, uflags, (size_t)SX_KMAX * ld * sizeof(double), x.s));
@@ -2026,7 +2016,7 @@ void simplex_set_hang_inject(long long batches) { g_cfg.inject_hang = batches >=
 void simplex_set_hang_inject_slot(int slot) { g_cfg.inject_slot = slot >= 0 ? slot : -1; }
 long long simplex_hang_recoveries(void) { return g_cfg.hang_recoveries; }
 long long simplex_fused_batches(void) { return g_cfg.fused_batches; }
-void simplex_set_fine_pivot_rows(int mode) { g_cfg.fine_u = mode < 0 ? -1 : (mode ? 1 : 0); }
+void simplex_set_fine_pivot_rows(int mode) { g_cfg.fine_u = mode < 0 ? -1 : mode > 2 ? 1 : mode; }
 void simplex_set_replicated_objective(int mode) { g_cfg.repl_obj = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_check_pivot_rows(int on) { g_cfg.check_u = on ? 1 : 0; }
 long long simplex_pivot_row_mismatches(void) { return g_cfg.u_mismatches; }

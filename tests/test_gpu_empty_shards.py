@@ -30,14 +30,12 @@ def bits(a):
 
 @pytest.mark.parametrize("p2p", [0, 1])
 @pytest.mark.parametrize("umode", ["plain", "fine", "uncached"])
-def test_empty_shards_repeated_solves(gpu, monkeypatch, umode, p2p):
+def test_empty_shards_repeated_solves(gpu, umode, p2p):
     n, m = 300, 1100  # 512-row blocks: W = 8 leaves shards 3..7 without rows
     A, b, c = oracle.generate(n, m, n * 100 + m, 1, 100)
     ref = two_phase_ref(A, b, c)
     lib = sx.load()
-    if umode == "uncached":  # (diagnostic allocation, sx_engine.cpp alloc_shard)
-        monkeypatch.setenv("SIMPLEX_DIAG_UNCACHED_U", "1")
-    lib.simplex_set_fine_pivot_rows(1 if umode == "fine" else 0)
+    lib.simplex_set_fine_pivot_rows({"plain": 0, "fine": 1, "uncached": 2}[umode])
     lib.simplex_set_check_pivot_rows(1)
     bad0 = lib.simplex_pivot_row_mismatches()
     sx.set_p2p(p2p)
