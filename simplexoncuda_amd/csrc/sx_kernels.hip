@@ -684,11 +684,10 @@ __device__ __forceinline__ unsigned ld_sc1(const unsigned *p) {
 
 // k_batch's objective-tile records as its ratio blocks poll them: 4 granules per tile (the tile
 // winner's d value and its pivot-row value of the pivot), at most SX_OBJ_TILES
-// tiles, SX_OBJ_PER_LANE granules per lane of the polling wave
+// tiles (every wave of a ratio block polls an eighth of them: at most 2 granules per lane)
 #define SX_GB4 4
 #define SX_GBS 16  // their stride in memory, granules: one 128-byte line per record (no two producers share a line)
 #define SX_OBJ_TILES 160
-#define SX_OBJ_PER_LANE 10
 
 // 8-byte write-through (sc1) store / L1-bypassing load of a double
 __device__ __forceinline__ void st_sc1(double *p, double v) {
@@ -704,6 +703,11 @@ struct IdOff {
 // the value granules (2 per tile) of k_batch's 4-granule objective records
 struct Rec4Val {
     __device__ __forceinline__ int operator()(int k) const { return (k >> 1) * SX_GBS + (k & 1); }
+};
+// all 4 granules of each record, from granule k0 on
+struct Rec4AllFrom {
+    int k0;
+    __device__ __forceinline__ int operator()(int k) const { return ((k0 + k) >> 2) * SX_GBS + ((k0 + k) & 3); }
 };
 // all 4 granules of each record
 struct Rec4All {
@@ -729,7 +733,7 @@ __device__ __forceinline__ void poll_pause() { __builtin_amdgcn_s_sleep(1); }
 template <typename OFF, bool SYS, int PL, typename PAYF>
 __device__ __forceinline__ int poll_wave_f(const u64 *base, int n, OFF off, unsigned tag, unsigned *out, unsigned *abort_w,
                            unsigned long long timeout, PAYF payf) {
-    const int t = threadIdx.x;
+    const int t = threadIdx.x & 63;
     const u64 t0 = __builtin_amdgcn_s_memrealtime();
     if (n <= 64) {
         bool have = t >= n;
@@ -794,6 +798,35 @@ __device__ int poll_wave(const u64 *base, int n, OFF off, unsigned tag, unsigned
                                                      [pay](int k, unsigned pl) {
                                                          if (pay && !(k & 1)) pay[k >> 1] = pl;
                                                      });
+}
+
+// The same poll spread over every wave of the block: wave w polls its share of the n granules (whole
+// records of `rec` granules, in order; granule k at base[off(k)] into out[k], payf(k, payload) as
+// it arrives), then one block barrier; block-uniform result (false: the batch was aborted or a wait
+// timed out).  Every thread of the block must call it.  Eight waves with at most two granules per
+// lane each hand a batch's records over faster than one wave with up to ten per lane (round 6,
+// profiles/r06_poll_waves_ab.txt: the objective->ratio hop 3.18 -> 2.46 us at config 5).
+template <typename OFF>
+struct OffFrom {
+    OFF off;
+    int k0;
+    __device__ __forceinline__ int operator()(int k) const { return off(k0 + k); }
+};
+template <bool SYS = false, typename OFF, typename PAYF>
+__device__ __forceinline__ int poll_block(const u64 *base, int n, int rec, OFF off, unsigned tag, unsigned *out,
+                                          unsigned *abort_w, unsigned long long timeout, PAYF payf, int *s_okw) {
+    const int w = (int)threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
+    const int per = ((n + nw - 1) / nw + rec - 1) / rec * rec;
+    const int k0 = w * per, nk = n - k0 < per ? (n - k0 > 0 ? n - k0 : 0) : per;
+    int ok = 1;
+    if (nk > 0)
+        ok = poll_wave_f<OffFrom<OFF>, SYS, 2>(base, nk, OffFrom<OFF>{off, k0}, tag, out + k0, abort_w, timeout,
+                                                 [&](int kl, unsigned pl) { payf(k0 + kl, pl); });
+    if ((threadIdx.x & 63) == 0) s_okw[w] = ok;
+    __syncthreads();
+    int all = 1;
+    for (int w1 = 0; w1 < nw; ++w1) all &= s_okw[w1];
+    return all;
 }
 
 // Pass 2 of the reference's argmin (deviceReduceKernel<false><<<1,1024>>>, reduction.cu:239-241)
@@ -1272,6 +1305,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
     __shared__ int s_sel_ok, s_sel_r, s_sel_any, s_det_ok, s_det_e, s_det_st, s_ent_ok, s_ent_e, s_ent_m;
     __shared__ double s_det_dmin, s_ent_v, s_br, s_ent_p;
     __shared__ int s_welig[SX_TILE / 64];
+    __shared__ int s_okw[SX_TILE / 64];
     const int t = threadIdx.x;
     const bool isA = (int)blockIdx.x < NA;
     // stamps (diagnostic, normally null): s_memrealtime (100 MHz) at hand-off points of ratio
@@ -1498,24 +1532,27 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 }
                 // ---- the objective side's answer: pass 2 over the objective tiles (the entering variable
                 // of pivot q + 1), its stored column and its pivot-row entry of this pivot from the
-                // winner's record (wave 0 polls; one block barrier)
+                // winner's record.  Every wave polls an eighth of the records (poll_block: 3.18 -> 2.46 us
+                // for this hop at config 5 against wave 0 alone, profiles/r06_poll_waves_ab.txt), then
+                // wave 0 runs pass 2; two block barriers.  (The ratio records -- 2 granules per tile,
+                // at most 2 per lane of one wave -- stay polled by wave 0: the second barrier cost more
+                // than the split saved, config 3 ratio->objective hop 1.12 -> 1.40 us.)
+                unsigned short *po = s_payo;
+                const int okb = poll_block(gb, SX_GB4 * NB, SX_GB4, Rec4All(), tag, s_g, &ch->abort_w, 20000000ull,
+                                           [po](int k, unsigned pl) {
+                                               if ((k & 3) < 3) po[(k & 3) * SX_OBJ_TILES + (k >> 2)] = (unsigned short)pl;
+                                           }, s_okw);
                 if (t < 64) {
-                    unsigned short *po = s_payo;
-                    const int ok = poll_wave_f<Rec4All, false, SX_OBJ_PER_LANE>(
-                        gb, SX_GB4 * NB, Rec4All(), tag, s_g, &ch->abort_w, 20000000ull,
-                        [po](int k, unsigned pl) {
-                            if ((k & 3) < 3) po[(k & 3) * SX_OBJ_TILES + (k >> 2)] = (unsigned short)pl;
-                        });
                     double ev = DBL_MAX;
                     int ei = -1, any = 0;
-                    if (ok) wave_pass2<SX_GB4, unsigned short>(s_g, s_payo, NB, s_v, s_i, ev, ei, any);
+                    if (okb) wave_pass2<SX_GB4, unsigned short>(s_g, s_payo, NB, s_v, s_i, ev, ei, any);
                     if (t == 0) {
-                        s_ent_ok = ok;
+                        s_ent_ok = okb;
                         s_ent_e = ei;
                         s_ent_v = ev;
                         s_ent_m = 0;
                         s_uq = 0.0;
-                        if (ok && ei >= 0) {
+                        if (okb && ei >= 0) {
                             const int wt = ei / SX_TILE;
                             s_ent_m = (int)s_payo[SX_OBJ_TILES + wt] | ((int)s_payo[2 * SX_OBJ_TILES + wt] << SX_PAYBITS);
                             s_uq = gd(s_g[SX_GB4 * wt + 2], s_g[SX_GB4 * wt + 3]);
@@ -1808,6 +1845,8 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                                               int rank, int tb0, int tb1, int NBg, int repl, BatchChan *ch,
                                               const u64 *ga, const u64 *gb, const u64 *gdone, PeerView pv,
                                               unsigned long long timeout) {
+    const bool pollb = (timeout >> 62) & 1ull;  // (A/B switch, round 6)
+    timeout &= (1ull << 62) - 1ull;
     extern __shared__ double s_hist[];  // [K][512]: F history (ratio tiles) / U history (objective tiles)
     __shared__ double s_v[16];
     __shared__ int s_i[16];
@@ -1819,6 +1858,7 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
     __shared__ unsigned s_g[4 * SX_TILE];
     __shared__ unsigned s_pay[SX_TILE];
     __shared__ int s_ok, s_flag;
+    __shared__ int s_okw[SX_TILE / 64];
     // per-step results written by wave 0 before the step's one barrier (as in k_batch)
     __shared__ int s_sel_ok, s_sel_r, s_sel_any, s_det_ok, s_det_e, s_det_st, s_ent_ok, s_ent_e, s_ent_r, s_ent_st, s_ent_m;
     __shared__ double s_det_dmin, s_ent_v, s_br, s_ent_p;
@@ -1961,9 +2001,16 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 }
                 // ---- the objective side's answer (every rank's objective tiles, from this rank's gb):
                 // the next entering variable, then r, p, the RHS, the status and U[s <= q][e]
+                int okb = 1;
+                if (pollb) {
+                    unsigned *pay = s_pay;
+                    okb = poll_block<true>(
+                        gb, 2 * NBg, 2, gather_b, tag, s_g, &ch->abort_w, timeout,
+                        [pay](int k, unsigned pl) { if (!(k & 1)) pay[k >> 1] = pl; }, s_okw);
+                }
                 if (t < 64) {
-                    int ok = poll_wave<decltype(gather_b), true>(gb, 2 * NBg, gather_b, tag, s_g, &ch->abort_w, timeout,
-                                                                 s_pay);
+                    int ok = pollb ? okb : poll_wave<decltype(gather_b), true>(gb, 2 * NBg, gather_b, tag, s_g, &ch->abort_w,
+                                                                               timeout, s_pay);
                     double ev = DBL_MAX;
                     int ei = -1, any = 0;
                     if (ok) wave_pass2(s_g, s_pay, NBg, s_v, s_i, ev, ei, any);
@@ -3264,6 +3311,7 @@ void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld,
     if (W < 1 || W > SX_MAXW || W * slots > SX_TILE || NBg > SX_TILE || NBg < 1 || tb0 < 0 || tb1 > NBg || tb0 > tb1 ||
         (repl && (tb0 != 0 || tb1 != NBg)))
         SX_FATAL("multi-rank fused batch: bad shape");
+    if (getenv("SIMPLEX_MR_POLLB") && atoi(getenv("SIMPLEX_MR_POLLB")) == 1) timeout |= 1ull << 62;
     k_batch_mr<<<slots + (tb1 - tb0), SX_TILE, batch_lds(k), s>>>(T, rows, row0, rpr, ld, tl, c, d, d_save, base, st, pd.U, pd.F,
                                                                   pd.recs, pd.PM, pd.PM2, pd.batch, k, slots, W, rank, tb0,
                                                                   tb1, NBg, repl, chan, ga, gb, gdone, pv, timeout);
@@ -3306,6 +3354,7 @@ void sx_launch_batch_mr_multi(const MrLaunchRank *ranks, int nloc, int W, int rp
         R.first[i + 1] = R.first[i] + slots + (q.tb1 - q.tb0);
     }
     for (int i = nloc + 1; i <= SX_MAXW; ++i) R.first[i] = R.first[nloc];
+    if (getenv("SIMPLEX_MR_POLLB") && atoi(getenv("SIMPLEX_MR_POLLB")) == 1) timeout |= 1ull << 62;
     k_batch_mr_multi<<<R.first[nloc], SX_TILE, batch_lds(k), s>>>(R, nloc, rpr, ld, tl, c, B, k, slots, W, NBg, pv,
                                                                   timeout);
 }
