@@ -812,7 +812,7 @@ struct OffFrom {
     int k0;
     __device__ __forceinline__ int operator()(int k) const { return off(k0 + k); }
 };
-template <bool SYS = false, typename OFF, typename PAYF>
+template <typename OFF, typename PAYF>
 __device__ __forceinline__ int poll_block(const u64 *base, int n, int rec, OFF off, unsigned tag, unsigned *out,
                                           unsigned *abort_w, unsigned long long timeout, PAYF payf, int *s_okw) {
     const int w = (int)threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
@@ -820,7 +820,7 @@ __device__ __forceinline__ int poll_block(const u64 *base, int n, int rec, OFF o
     const int k0 = w * per, nk = n - k0 < per ? (n - k0 > 0 ? n - k0 : 0) : per;
     int ok = 1;
     if (nk > 0)
-        ok = poll_wave_f<OffFrom<OFF>, SYS, 2>(base, nk, OffFrom<OFF>{off, k0}, tag, out + k0, abort_w, timeout,
+        ok = poll_wave_f<OffFrom<OFF>, false, 2>(base, nk, OffFrom<OFF>{off, k0}, tag, out + k0, abort_w, timeout,
                                                  [&](int kl, unsigned pl) { payf(k0 + kl, pl); });
     if ((threadIdx.x & 63) == 0) s_okw[w] = ok;
     __syncthreads();
@@ -1845,8 +1845,6 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                                               int rank, int tb0, int tb1, int NBg, int repl, BatchChan *ch,
                                               const u64 *ga, const u64 *gb, const u64 *gdone, PeerView pv,
                                               unsigned long long timeout) {
-    const bool pollb = (timeout >> 62) & 1ull;  // (A/B switch, round 6)
-    timeout &= (1ull << 62) - 1ull;
     extern __shared__ double s_hist[];  // [K][512]: F history (ratio tiles) / U history (objective tiles)
     __shared__ double s_v[16];
     __shared__ int s_i[16];
@@ -1858,7 +1856,6 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
     __shared__ unsigned s_g[4 * SX_TILE];
     __shared__ unsigned s_pay[SX_TILE];
     __shared__ int s_ok, s_flag;
-    __shared__ int s_okw[SX_TILE / 64];
     // per-step results written by wave 0 before the step's one barrier (as in k_batch)
     __shared__ int s_sel_ok, s_sel_r, s_sel_any, s_det_ok, s_det_e, s_det_st, s_ent_ok, s_ent_e, s_ent_r, s_ent_st, s_ent_m;
     __shared__ double s_det_dmin, s_ent_v, s_br, s_ent_p;
@@ -2001,16 +1998,9 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 }
                 // ---- the objective side's answer (every rank's objective tiles, from this rank's gb):
                 // the next entering variable, then r, p, the RHS, the status and U[s <= q][e]
-                int okb = 1;
-                if (pollb) {
-                    unsigned *pay = s_pay;
-                    okb = poll_block<true>(
-                        gb, 2 * NBg, 2, gather_b, tag, s_g, &ch->abort_w, timeout,
-                        [pay](int k, unsigned pl) { if (!(k & 1)) pay[k >> 1] = pl; }, s_okw);
-                }
                 if (t < 64) {
-                    int ok = pollb ? okb : poll_wave<decltype(gather_b), true>(gb, 2 * NBg, gather_b, tag, s_g, &ch->abort_w,
-                                                                               timeout, s_pay);
+                    int ok = poll_wave<decltype(gather_b), true>(gb, 2 * NBg, gather_b, tag, s_g, &ch->abort_w, timeout,
+                                                                 s_pay);
                     double ev = DBL_MAX;
                     int ei = -1, any = 0;
                     if (ok) wave_pass2(s_g, s_pay, NBg, s_v, s_i, ev, ei, any);
@@ -3311,7 +3301,6 @@ void sx_launch_batch_mr(const double *T, int rows, int row0, int rpr, size_t ld,
     if (W < 1 || W > SX_MAXW || W * slots > SX_TILE || NBg > SX_TILE || NBg < 1 || tb0 < 0 || tb1 > NBg || tb0 > tb1 ||
         (repl && (tb0 != 0 || tb1 != NBg)))
         SX_FATAL("multi-rank fused batch: bad shape");
-    if (getenv("SIMPLEX_MR_POLLB") && atoi(getenv("SIMPLEX_MR_POLLB")) == 1) timeout |= 1ull << 62;
     k_batch_mr<<<slots + (tb1 - tb0), SX_TILE, batch_lds(k), s>>>(T, rows, row0, rpr, ld, tl, c, d, d_save, base, st, pd.U, pd.F,
                                                                   pd.recs, pd.PM, pd.PM2, pd.batch, k, slots, W, rank, tb0,
                                                                   tb1, NBg, repl, chan, ga, gb, gdone, pv, timeout);
@@ -3354,7 +3343,6 @@ void sx_launch_batch_mr_multi(const MrLaunchRank *ranks, int nloc, int W, int rp
         R.first[i + 1] = R.first[i] + slots + (q.tb1 - q.tb0);
     }
     for (int i = nloc + 1; i <= SX_MAXW; ++i) R.first[i] = R.first[nloc];
-    if (getenv("SIMPLEX_MR_POLLB") && atoi(getenv("SIMPLEX_MR_POLLB")) == 1) timeout |= 1ull << 62;
     k_batch_mr_multi<<<R.first[nloc], SX_TILE, batch_lds(k), s>>>(R, nloc, rpr, ld, tl, c, B, k, slots, W, NBg, pv,
                                                                   timeout);
 }

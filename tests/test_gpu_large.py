@@ -164,3 +164,70 @@ def test_config5_degenerate_variant_long_pins(gpu, W, p2p, stops):
     finally:
         sx.set_virtual_ranks(1)
         sx.set_p2p(-1)
+
+
+with open(os.path.join(GOLDEN, "long_pivots.json")) as _f:
+    LONGP = json.load(_f)
+
+
+def _phase1_pins(name):
+    return {c["pivots"]: c for c in LONGP[name]["checkpoints"] if c.get("phase", 1) == 1}
+
+
+@pytest.mark.parametrize("name,W,p2p,stops", [("config5", 1, -1, (320, 1600, 2080)), ("config5", 8, 1, (2080,)),
+                                              ("config4", 1, -1, (320, 1600, 2080)), ("config4", 4, 1, (2080,))])
+def test_bench_window_long_pins(gpu, name, W, p2p, stops):
+    """the benchmark's own window against the CPU oracle: the driver's
+    `bench.py --steps 20 --warmup 5` times config 5's phase-1 pivots 320..1600 (the default run
+    0..2080); after 320, 1600 and 2080 pivots the logical tableau, the objective row and the basis are
+    the oracle's bit for bit (tests/golden/long_pivots.json, tests/golden/scripts/make_long_pins.py:
+    the serial restatement with its row update on host threads) -- on one shard and on the
+    peer-memory virtual shards of the multi-GPU split (W = 8 for config 5, W = 4 for config 4)"""
+    pins = _phase1_pins(name)
+    rec = LONGP[name]
+    n, m, width = rec["n"], rec["m"], rec["width"]
+    lib = sx.load()
+    h0 = lib.simplex_hang_recoveries()
+    sx.set_virtual_ranks(W)
+    sx.set_p2p(p2p)
+    try:
+        sess = sx.Session(generated=(n, m, rec["seed"], rec["lo"], rec["hi"]))
+        for k in stops:
+            pin = pins[k]
+            tim = sess.pivots(k - sess.total_pivots())
+            assert tim.status == sx.NOT_ENDED and sess.total_pivots() == k
+            T, d, base = sess.tableau(m, width)
+            assert float(d[0]).hex() == pin["d0_hex"], k
+            assert sha(base) == pin["sha256_base"], k
+            assert sha(d) == pin["sha256_d"], k
+            assert sha(T) == pin["sha256_T"], k
+            del T
+        sess.close()
+    finally:
+        sx.set_virtual_ranks(1)
+        sx.set_p2p(-1)
+    assert lib.simplex_hang_recoveries() == h0
+
+
+@pytest.mark.parametrize("W,p2p", [(1, -1), (4, 1)])
+def test_config4_whole_solve_matches_oracle(gpu, W, p2p):
+    """config 4's whole twoPhaseMethod against the CPU oracle's whole solve (twoPhaseMethod.cu:225-435,
+    the solution :370-383; tests/golden/long_pivots.json["config4"]["result"]): status, both phases'
+    pivot counts, the objective's bits and the SHA-256 of the final basis and solution -- on one
+    shard and on 4 peer-memory virtual shards"""
+    rec = LONGP["config4"]
+    res = rec["result"]
+    p = sx.generateRandomProblemDevice(rec["n"], rec["m"], rec["seed"], rec["lo"], rec["hi"])
+    sx.set_virtual_ranks(W)
+    sx.set_p2p(p2p)
+    try:
+        got = sx.twoPhaseMethodEx(p)
+    finally:
+        sx.set_virtual_ranks(1)
+        sx.set_p2p(-1)
+        p.close()
+    assert got.status == res["status"]
+    assert list(got.pivots) == res["pivots"]
+    assert float(got.optimal_value).hex() == res["opt_hex"]
+    assert hashlib.sha256(np.ascontiguousarray(got.base, dtype=np.int32).tobytes()).hexdigest() == res["sha256_base"]
+    assert hashlib.sha256(np.ascontiguousarray(got.solution, dtype=np.float64).tobytes()).hexdigest() == res["sha256_x"]
