@@ -13,6 +13,11 @@ W = 8 split of config 5), and through the peer-memory fused batch (W = 2, 3, and
 splits W = 4 / 8: the virtual ranks' batches run as one launch on one GPU), and through the
 one-process multi-GPU mode (SIMPLEX_GPUS / simplex_set_gpus) with every shard mapped onto this
 GPU: device list [0] * W, the peer-memory batch enabled by the mode's own start-up self-check.
+
+tests/golden/long_pivots.json (tests/golden/scripts/make_long_pins.py, the same restatement with
+its row update on host threads) carries the pins further: config 5 at pivots 320, 1600 and 2080 --
+the edges of bench.py's timed windows -- config 4 from 48 pivots to the end of its phase 1 and its
+whole two-phase solve, and config 5's [-100, 100] variant to 3000 pivots.
 """
 import hashlib
 import json
