@@ -4,7 +4,8 @@ two-phase solve -- made in the build container (the GPU box only reads the JSON)
 
   config5_degenerate  generateRandomProblem(8192, 32768, 851968, -100, 100)  pivots 48..3000
   config5             generateRandomProblem(8192, 32768, 851968, 1, 100)     pivots 48, 320, 1600, 2080
-                      (bench.py's timed window: the driver's --warmup 5 --steps 20 is pivots 320..1600)
+                      (bench.py's timed window: the driver's --warmup 5 --steps 20 is pivots 320..1600),
+                      every 5000 after, toward the whole solve (as far as the build container's time allows)
   config4             generateRandomProblem(4096, 16384, 425984, 1, 100)     pivots 48..2080, every
                       5000 after, then the whole two-phase solve (status, pivot counts, objective
                       bits, basis and solution digests: twoPhaseMethod.cu:225-435, :370-383)
@@ -37,10 +38,13 @@ import oracle  # noqa: E402
 
 CASES = {
     "config5_degenerate": ((8192, 32768, 851968, -100, 100), [48, 100, 250, 500, 1000, 2000, 3000], False),
-    "config5": ((8192, 32768, 851968, 1, 100), [48, 320, 1600, 2080], False),
+    "config5": ((8192, 32768, 851968, 1, 100), [48, 320, 1600, 2080] + list(range(5000, 200001, 5000)), True),
     "config4": ((4096, 16384, 425984, 1, 100), [48, 320, 1600, 2080] + list(range(5000, 200001, 5000)), True),
 }
 OUT = os.path.join(ROOT, "tests", "golden", "long_pivots.json")
+# (a long run may write its progress elsewhere -- PIN_OUT -- and be merged into OUT when it is done,
+# so a working tree sent to the GPU meanwhile keeps the committed pins)
+OUT = os.environ.get("PIN_OUT", OUT)
 STATE = os.environ.get("PIN_STATE_DIR", "/tmp")
 
 
