@@ -7,9 +7,10 @@ in HBM (10.7 GB stored: artificial columns aliased to their slack columns, DESIG
 A "step" is one pass of the hot path over the tableau: one batch of simplex pivots (64: two
 stages of 32, DESIGN.md §3, on one GPU and on several) -- entering argmin, ratio test,
 pivot row and objective row of each -- followed by one sweep that applies their rank-1 updates
-to every stored tableau element.  W untimed steps, then K timed steps: by default about the
-first 2000 phase-1 pivots after the warmup (the scaling curve is the first 2000
-phase-1 pivots).  Every timed step is a full batch, so the timed window runs exactly the kernels
+to every stored tableau element.  W untimed steps, then K timed steps: by default the driver's
+window, W = 5 and K = 20 (phase-1 pivots 320..1600 of the first 2000), whose end
+state is checked against the CPU oracle's pin at pivot 1600 (the line's `parity`); --steps 0 times
+up to about pivot 2080.  Every timed step is a full batch, so the timed window runs exactly the kernels
 the warmup ran.
 
 N GPUs: the constraint rows are split into N contiguous 512-aligned blocks, each GPU sweeps only
@@ -168,9 +169,9 @@ def cpu_baseline(n, m, seed, pivots, sx):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=0,
-                    help="timed steps; a step = one batch of pivots + one tableau sweep (0 = about 2016 pivots)")
-    ap.add_argument("--warmup", type=int, default=2, help="untimed steps before timing")
+    ap.add_argument("--steps", type=int, default=20,
+                    help="timed steps; a step = one batch of pivots + one tableau sweep (0 = up to about pivot 2080)")
+    ap.add_argument("--warmup", type=int, default=5, help="untimed steps before timing")
     ap.add_argument("--config", default="config5", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0,
                     help="pivots per tableau sweep (0 = library default: 64 from 4096 rows, else 32)")
