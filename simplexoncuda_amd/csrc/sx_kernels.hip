@@ -2568,31 +2568,28 @@ __device__ __forceinline__ void msweep_store(const d4_t (&acc)[2][2], __amdgpu_b
 
 // The rows that left the basis in a batch (k_msweep): row r_s (first slot s where it left) by
 // the row slot s % G, one column per lane (the strips leave them unwritten).  The row slot's rows
-// are found in one round trip (lane k: slot gy + G k); the column's pivot-row values of every slot
-// are loaded once; each group of NR rows costs one round trip (the pivot-row value it restarts
-// from and its factors; the pivots: lane s = slot s, read by v_readlane) and a branch-free chain.
+// and their leaving slots come from the sweep's register list rl (lane s: the shard row that left
+// at slot s) -- a shuffle and a ballot per slot, no memory access (round 6: the PM / PM2 loads were
+// two dependent round trips in the sweep's tail); the column's pivot-row values of every slot are
+// loaded once; each group of NR rows costs one round trip (the pivot-row value it restarts from and
+// its factors; the pivots: lane s = slot s, read by v_readlane) and a branch-free chain.
 template <int NKB>
 __device__ __forceinline__ void msweep_fixup(const double *Tr, double *Tw, size_t ldr, int cr, int c0, int Ns, int rows,
                                              int row0, TLay tl, int gy, int G, int cnt,
                                              const double *__restrict__ F, const double *__restrict__ U, size_t ld,
-                                             const PivRec *__restrict__ recs,
-                                             const unsigned long long *__restrict__ PM,
-                                             const unsigned long long *__restrict__ PM2, unsigned B, unsigned mask,
-                                             unsigned mask2) {
+                                             const PivRec *__restrict__ recs, int rl) {
     const int OOB = 0x7fffffff;
     const int l = (int)threadIdx.x & 63;
     const int j = c0 + l;
     int rk = -1;                // lane k: the row of slot gy + G k, if this is its first slot
     unsigned long long bk = 0;  // ... and its leaving slots
-    {
-        const int sk = gy + G * l;
-        if (sk < cnt) {
-            const int r = recs[sk].r - row0;
-            if (r >= 0 && r < rows) {
-                bk = (unsigned long long)pend_bits(PM, r, B, mask) |
-                     ((unsigned long long)(mask2 ? pend_bits(PM2, r, B, mask2) : 0u) << SX_HMAX);
-                if (bk != 0ull && (int)__builtin_ctzll(bk) == sk) rk = r;
-            }
+    for (int k = 0; gy + G * k < cnt; ++k) {  // (wave-uniform)
+        const int sk = gy + G * k;
+        const int r = __shfl(rl, sk);
+        const unsigned long long b = __ballot(r >= 0 && rl == r);
+        if (l == k && r >= 0 && (int)__builtin_ctzll(b) == sk) {
+            rk = r;
+            bk = b;
         }
     }
     unsigned long long todo = __ballot(rk >= 0);
@@ -2715,8 +2712,6 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
     double *const Tw = inB ? Tdst + tl.offB : Tdst;
     const size_t ldr = inB ? tl.ldB : tl.ldA;
     const int cr = inB ? c0 - tl.jB : c0;
-    const unsigned mask = cnt > 0 ? slot_mask(cnt) : 0u;
-    const unsigned mask2 = cnt > SX_HMAX ? slot_mask(cnt - SX_HMAX) : 0u;
     const int nkb = (cnt + 3) >> 2;
     const int OOB = 0x7fffffff;
     // lane s: the shard row that left at slot s (-1: none here) -- the strips find their leaving
@@ -2809,7 +2804,7 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
             msweep_store(acc, rss, c0, jl, Ns, skip, tile_off);
         }
     }
-    msweep_fixup<NKB>(Tr, Tw, ldr, cr, c0, Ns, rows, row0, tl, gy, G, cnt, F, U, ld, recs, PM, PM2, B, mask, mask2);
+    msweep_fixup<NKB>(Tr, Tw, ldr, cr, c0, Ns, rows, row0, tl, gy, G, cnt, F, U, ld, recs, rl);
 }
 
 // Slack compaction (sx_common.hpp Cols), between a batch's selections and its
