@@ -950,46 +950,18 @@ __device__ __forceinline__ double rdlane(double v, int l) {
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
-// The batch's pending pivots s < q of one stage applied, in slot order, to a ratio row's
-// entering-column entry `a` (solver.cu:34-46 on that element): a / p_s at the slots in `bits`
-// (the row itself left the basis there), fma(F[row][s], U[s][e], a) at the others.  A row that
-// left at slots in `bits` has, just before its last such slot sl, exactly the value the pivot
-// row of slot sl held in this column -- U[sl][e], formed by the objective tiles with the same
-// operations in the same order -- so its chain is U[sl][e] / p_sl followed by the fmas of the
-// slots after sl: one division and a select per slot instead of a branch per slot (~25
-// instructions each).  A wave none of whose rows left -- nearly always -- runs the plain chain.
-__device__ __forceinline__ double hist_col(double a, int q, unsigned bits, const double *s_hist, const double *s_ue,
-                                           const double *s_p) {
-    const int t = threadIdx.x, lane = t & 63;
-    const double wu = s_ue[lane & (SX_HMAX - 1)];  // lane s: U[s][e]
-    if (__ballot(bits != 0u) == 0ull) {
-        int s = 0;
-        for (; s + 8 <= q; s += 8) {
-            double h[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) h[k] = s_hist[(s + k) * SX_TILE + t];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) a = fma(h[k], rdlane(wu, s + k), a);
-        }
-        for (; s < q; ++s) a = fma(s_hist[s * SX_TILE + t], rdlane(wu, s), a);
-        return a;
-    }
-    const int sl = bits ? 31 - __builtin_clz(bits) : -1;  // the row's last leaving slot
-    if (bits) a = s_ue[sl] / s_p[sl];
-    for (int s0 = 0; s0 < q; s0 += 8) {  // (slots past q read slot s0 and are not used)
-        double h[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) h[k] = s_hist[(s0 + k < q ? s0 + k : s0) * SX_TILE + t];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            if (s0 + k < q) {
-                const double y = fma(h[k], rdlane(wu, s0 + k), a);
-                a = s0 + k > sl ? y : a;
-            }
-        }
-    }
-    return a;
-}
+// The batch's pending pivots s < q of one stage are applied, in slot order, to a ratio row's
+// entering-column entry (solver.cu:34-46 on that element): a / p_s at the slots where the row itself
+// left the basis, fma(F[row][s], U[s][e], a) at the others -- and to the pivot row's entry on an
+// objective tile's column: u / p_s where the leaving row r left before, fma(F[r][s], U[s][j], u)
+// elsewhere.  A row that left at slots in `bits` has, just before its last such slot sl, exactly the
+// value the pivot row of slot sl held in this column -- U[sl][e], formed by the objective tiles with the
+// same operations in the same order -- so its chain is U[sl][e] / p_sl followed by the fmas of the
+// slots after sl: one division and a select per slot instead of a branch per slot.  Two stages
+// (pivots SX_HMAX .. SX_KMAX - 1): the first stage's history, moved from LDS to registers at the
+// switch (h1), is applied before the second stage's.  The block-uniform operands of a slot (the
+// entering column's U[s][e], the leaving row's F[r][s]) come from one wave register or LDS array per
+// stage, fed to each step by a DPP broadcast (below).
 
 // 64-bit value of lane src (per-lane src; ds_bpermute)
 __device__ __forceinline__ double shfl_d(double v, int src) {
@@ -998,132 +970,171 @@ __device__ __forceinline__ double shfl_d(double v, int src) {
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
-// hist_col with the entering column's pending pivot-row values in a register of the wave (lane s:
-// U[s][e] of the stage's slot s) instead of LDS: k_batch's ratio blocks load them from U themselves
-// (every wave its own copy), in the same round trip as the column's stored values.
-__device__ __forceinline__ double hist_col_w(double a, int q, unsigned bits, const double *s_hist, double wu,
-                                             const double *s_p) {
-    const int t = threadIdx.x;
-    if (__ballot(bits != 0u) == 0ull) {
-        int s = 0;
-        for (; s + 8 <= q; s += 8) {
-            double h[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) h[k] = s_hist[(s + k) * SX_TILE + t];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) a = fma(h[k], rdlane(wu, s + k), a);
-        }
-        for (; s < q; ++s) a = fma(s_hist[s * SX_TILE + t], rdlane(wu, s), a);
-        return a;
+// ---- history chains with the slot values as DPP broadcasts (round 6).  A chain step
+// x = fma(w_s, h_s, x) took two v_readlane (lane s of the wave register holding the slot values, into
+// scalar registers), an s_nop for the scalar hazard and the fma -- three VALU issues per step, the two
+// waves of a SIMD sharing them.  Here the 32 slot values sit in two registers as broadcast sources --
+// lane l of W.w[j] holds slot 16 j + (l & 15) -- and each step is ONE v_fmac_f64_dpp with
+// row_newbcast:(s & 15), which feeds every lane of a 16-lane row from that row's lane s & 15, i.e.
+// slot s.  The same fma per element in the same slot order (w_s * h_s is one exactly rounded product
+// either way): the same bits.
+template <int K>
+__device__ __forceinline__ double fma_bc(double w, double h, double x) {
+    asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(x) : "v"(w), "v"(h), "n"(K));
+    return x;
+}
+struct Bc2 {
+    double w[2];
+};
+// (a VALU write of a register a DPP instruction reads needs 2 wait states: the s_nop, ordered after the
+// writes by its operands, provides them once per chain)
+__device__ __forceinline__ void bc2_fence(Bc2 &b) { asm volatile("s_nop 1" : "+v"(b.w[0]), "+v"(b.w[1])); }
+// from a wave register holding slot s in lane s (s < 32)
+__device__ __forceinline__ Bc2 bc2_from_lanes(double wv) {
+    const int l = (int)threadIdx.x & 15;
+    Bc2 b{{shfl_d(wv, l), shfl_d(wv, 16 + l)}};
+    bc2_fence(b);
+    return b;
+}
+// from an LDS array holding slot s at s_v[s] (s < 32)
+__device__ __forceinline__ Bc2 bc2_from_lds(const double *s_v) {
+    const int l = (int)threadIdx.x & 15;
+    Bc2 b{{s_v[l], s_v[16 + l]}};
+    bc2_fence(b);
+    return b;
+}
+// steps S0 .. S0 + 7 of a chain on the history values h[0..8), those at slots in [from, q) applied
+// (all: plain steps; SEL: y = the step, kept only where keep(slot) -- a lane-dependent select)
+template <int S0>
+__device__ __forceinline__ double bc_steps8(double x, const Bc2 &W, const double (&h)[8], int from, int q) {
+#define SX_BCS(K)                                                                       \
+    if (S0 + K >= from && S0 + K < q) x = fma_bc<(S0 + K) & 15>(W.w[(S0 + K) >> 4], h[K], x);
+    SX_BCS(0) SX_BCS(1) SX_BCS(2) SX_BCS(3) SX_BCS(4) SX_BCS(5) SX_BCS(6) SX_BCS(7)
+#undef SX_BCS
+    return x;
+}
+template <int S0>
+__device__ __forceinline__ double bc_steps8_after(double x, const Bc2 &W, const double (&h)[8], int q, int sl,
+                                                  bool all) {
+#define SX_BCS(K)                                                                          \
+    if (S0 + K < q) {                                                                      \
+        const double y = fma_bc<(S0 + K) & 15>(W.w[(S0 + K) >> 4], h[K], x);               \
+        x = (all || S0 + K > sl) ? y : x;                                                  \
     }
+    SX_BCS(0) SX_BCS(1) SX_BCS(2) SX_BCS(3) SX_BCS(4) SX_BCS(5) SX_BCS(6) SX_BCS(7)
+#undef SX_BCS
+    return x;
+}
+// the history of slots [from, q) of this thread's column / row from LDS (s_hist[s][t]), 8 slots per
+// group of loads
+__device__ __forceinline__ double bc_chain_lds(double x, const Bc2 &W, const double *s_hist, int from, int q) {
+    const int t = threadIdx.x;
+    double h[8];
+#define SX_BCG(S0)                                                                     \
+    if (S0 < q && S0 + 8 > from) {                                                     \
+        _Pragma("unroll") for (int k = 0; k < 8; ++k) h[k] = s_hist[(S0 + k) * SX_TILE + t]; \
+        x = bc_steps8<S0>(x, W, h, from, q);                                           \
+    }
+    SX_BCG(0) SX_BCG(8) SX_BCG(16) SX_BCG(24)
+#undef SX_BCG
+    return x;
+}
+__device__ __forceinline__ double bc_chain_lds_after(double x, const Bc2 &W, const double *s_hist, int q, int sl,
+                                                     bool all) {
+    const int t = threadIdx.x;
+    double h[8];
+#define SX_BCG(S0)                                                                     \
+    if (S0 < q) {                                                                      \
+        _Pragma("unroll") for (int k = 0; k < 8; ++k) h[k] = s_hist[(S0 + k) * SX_TILE + t]; \
+        x = bc_steps8_after<S0>(x, W, h, q, sl, all);                                  \
+    }
+    SX_BCG(0) SX_BCG(8) SX_BCG(16) SX_BCG(24)
+#undef SX_BCG
+    return x;
+}
+// ... of all 32 slots of a register-held history (the first stage, h1)
+__device__ __forceinline__ double bc_chain_regs(double x, const Bc2 &W, const double (&h1)[SX_HMAX], int from) {
+    double h[8];
+#define SX_BCG(S0)                                                                     \
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) h[k] = h1[S0 + k];                   \
+    x = bc_steps8<S0>(x, W, h, from, SX_HMAX);
+    SX_BCG(0) SX_BCG(8) SX_BCG(16) SX_BCG(24)
+#undef SX_BCG
+    return x;
+}
+__device__ __forceinline__ double bc_chain_regs_after(double x, const Bc2 &W, const double (&h1)[SX_HMAX], int sl,
+                                                      bool all) {
+    double h[8];
+#define SX_BCG(S0)                                                                     \
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) h[k] = h1[S0 + k];                   \
+    x = bc_steps8_after<S0>(x, W, h, SX_HMAX, sl, all);
+    SX_BCG(0) SX_BCG(8) SX_BCG(16) SX_BCG(24)
+#undef SX_BCG
+    return x;
+}
+
+// hist_col_w / stage1_col_w / hist_row / stage1_row with the broadcast steps: the same decisions
+// (the leaving-row restart from U[sl] / p_sl, then the slots after sl), the same operations
+__device__ __forceinline__ double hist_col_bc(double a, int q, unsigned bits, const double *s_hist, double wu,
+                                              const double *s_p) {
+    const Bc2 W = bc2_from_lanes(wu);
+    if (__ballot(bits != 0u) == 0ull) return bc_chain_lds(a, W, s_hist, 0, q);
     const int sl = bits ? 31 - __builtin_clz(bits) : 0;  // the row's last leaving slot
     const double usl = shfl_d(wu, sl);
     if (bits) a = usl / s_p[sl];
-    for (int s0 = 0; s0 < q; s0 += 8) {  // (slots past q read slot s0 and are not used)
-        double h[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) h[k] = s_hist[(s0 + k < q ? s0 + k : s0) * SX_TILE + t];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            if (s0 + k < q) {
-                const double y = fma(h[k], rdlane(wu, s0 + k), a);
-                a = (bits && s0 + k > sl) || !bits ? y : a;
-            }
-        }
-    }
-    return a;
+    return bc_chain_lds_after(a, W, s_hist, q, bits ? sl : -1, !bits);
 }
-
-// The same for the pivot row's entry `u` on an objective tile's column: u / p_s at the slots
-// where the leaving row r itself left before (s_r[s] == r), else fma(F[r][s], U[s][j], u).
-// The slots where r left are block-uniform: with none the chain is branch-free; else it starts
-// from U[sl][j] / p_sl (this thread's own history of slot sl, the last) and runs the fmas of
-// the slots after sl.
-__device__ __forceinline__ double hist_row(double u, int q, int r, const double *s_hist, const double *s_fr,
-                                           const double *s_p, const int *s_r) {
-    const int t = threadIdx.x, lane = t & 63;
-    const double wf = s_fr[lane & (SX_HMAX - 1)];  // lane s: F[r][s]
-    const unsigned long long left = __ballot(lane < q && s_r[lane < q ? lane : 0] == r);
-    int s = 0;
-    if (left) {
-        const int sl = 63 - __builtin_clzll(left);
-        u = s_hist[sl * SX_TILE + t] / s_p[sl];
-        s = sl + 1;
-    }
-    for (; s + 8 <= q; s += 8) {
-        double h[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) h[k] = s_hist[(s + k) * SX_TILE + t];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) u = fma(rdlane(wf, s + k), h[k], u);
-    }
-    for (; s < q; ++s) u = fma(rdlane(wf, s), s_hist[s * SX_TILE + t], u);
-    return u;
-}
-
-// A two-stage batch (k_batch, pivots SX_HMAX .. SX_KMAX - 1): the first stage's SX_HMAX pending
-// pivots, whose history each thread moved from LDS to registers (h[s]: a ratio row's factor F[.][s],
-// an objective column's pivot-row value U[s][.]), applied before the second stage's
-// (hist_col / hist_row on the LDS history): the same operations in slot order, the same
-// leaving-row shortcut.  s_u / s_f: the first stage's U[s][e] (entering column) / F[r][s]
-// (leaving row), block-uniform in LDS.
-__device__ __forceinline__ double stage1_col(double a, const double (&h)[SX_HMAX], unsigned bits, const double *s_u,
-                                             const double *s_p) {
-    const int lane = threadIdx.x & 63;
-    const double wu = s_u[lane & (SX_HMAX - 1)];
-    if (__ballot(bits != 0u) == 0ull) {
-#pragma unroll
-        for (int s = 0; s < SX_HMAX; ++s) a = fma(h[s], rdlane(wu, s), a);
-        return a;
-    }
-    const int sl = bits ? 31 - __builtin_clz(bits) : -1;
-    if (bits) a = s_u[sl] / s_p[sl];
-#pragma unroll
-    for (int s = 0; s < SX_HMAX; ++s) {
-        const double y = fma(h[s], rdlane(wu, s), a);
-        a = s > sl ? y : a;
-    }
-    return a;
-}
-// stage1_col with the first stage's U[s][e] in a register of the wave (lane s), as hist_col_w
-__device__ __forceinline__ double stage1_col_w(double a, const double (&h)[SX_HMAX], unsigned bits, double wu,
-                                               const double *s_p) {
-    if (__ballot(bits != 0u) == 0ull) {
-#pragma unroll
-        for (int s = 0; s < SX_HMAX; ++s) a = fma(h[s], rdlane(wu, s), a);
-        return a;
-    }
+__device__ __forceinline__ double stage1_col_bc(double a, const double (&h)[SX_HMAX], unsigned bits, double wu,
+                                                const double *s_p) {
+    const Bc2 W = bc2_from_lanes(wu);
+    if (__ballot(bits != 0u) == 0ull) return bc_chain_regs(a, W, h, 0);
     const int sl = bits ? 31 - __builtin_clz(bits) : 0;
     const double usl = shfl_d(wu, sl);
     if (bits) a = usl / s_p[sl];
-#pragma unroll
-    for (int s = 0; s < SX_HMAX; ++s) {
-        const double y = fma(h[s], rdlane(wu, s), a);
-        a = (bits && s > sl) || !bits ? y : a;
-    }
-    return a;
+    return bc_chain_regs_after(a, W, h, bits ? sl : -1, !bits);
 }
-__device__ __forceinline__ double stage1_row(double u, const double (&h)[SX_HMAX], int r, const double *s_f,
-                                             const double *s_p, const int *s_r) {
-    const int lane = threadIdx.x & 63;
-    const double wf = s_f[lane & (SX_HMAX - 1)];
-    const unsigned long long left = __ballot(lane < SX_HMAX && s_r[lane < SX_HMAX ? lane : 0] == r);
-    if (left == 0ull) {
-#pragma unroll
-        for (int s = 0; s < SX_HMAX; ++s) u = fma(rdlane(wf, s), h[s], u);
-        return u;
+// (the multi-rank batch's ratio tiles: the entering column's pending values U[s][e] in LDS, s_ue)
+__device__ __forceinline__ double hist_col_bcl(double a, int q, unsigned bits, const double *s_hist, const double *s_ue,
+                                               const double *s_p) {
+    const Bc2 W = bc2_from_lds(s_ue);
+    if (__ballot(bits != 0u) == 0ull) return bc_chain_lds(a, W, s_hist, 0, q);
+    const int sl = bits ? 31 - __builtin_clz(bits) : -1;
+    if (bits) a = s_ue[sl] / s_p[sl];
+    return bc_chain_lds_after(a, W, s_hist, q, sl, !bits);
+}
+__device__ __forceinline__ double stage1_col_bcl(double a, const double (&h)[SX_HMAX], unsigned bits, const double *s_u,
+                                                 const double *s_p) {
+    const Bc2 W = bc2_from_lds(s_u);
+    if (__ballot(bits != 0u) == 0ull) return bc_chain_regs(a, W, h, 0);
+    const int sl = bits ? 31 - __builtin_clz(bits) : -1;
+    if (bits) a = s_u[sl] / s_p[sl];
+    return bc_chain_regs_after(a, W, h, sl, !bits);
+}
+__device__ __forceinline__ double hist_row_bc(double u, int q, int r, const double *s_hist, const double *s_fr,
+                                              const double *s_p, const int *s_r) {
+    const int t = threadIdx.x, lane = t & 63;
+    const Bc2 W = bc2_from_lds(s_fr);
+    const unsigned long long left = __ballot(lane < q && s_r[lane < q ? lane : 0] == r);
+    int from = 0;
+    if (left) {
+        const int sl = 63 - __builtin_clzll(left);
+        u = s_hist[sl * SX_TILE + t] / s_p[sl];
+        from = sl + 1;
     }
+    return bc_chain_lds(u, W, s_hist, from, q);
+}
+__device__ __forceinline__ double stage1_row_bc(double u, const double (&h)[SX_HMAX], int r, const double *s_f,
+                                                const double *s_p, const int *s_r) {
+    const int lane = threadIdx.x & 63;
+    const Bc2 W = bc2_from_lds(s_f);
+    const unsigned long long left = __ballot(lane < SX_HMAX && s_r[lane < SX_HMAX ? lane : 0] == r);
+    if (left == 0ull) return bc_chain_regs(u, W, h, 0);
     const int sl = 63 - __builtin_clzll(left);  // (block-uniform)
     double hs = 0.0;
 #pragma unroll
-    for (int s = 0; s < SX_HMAX; ++s) hs = s == sl ? h[s] : hs;
+    for (int s1 = 0; s1 < SX_HMAX; ++s1) hs = s1 == sl ? h[s1] : hs;
     u = hs / s_p[sl];
-#pragma unroll
-    for (int s = 0; s < SX_HMAX; ++s) {
-        const double y = fma(rdlane(wf, s), h[s], u);
-        u = s > sl ? y : u;
-    }
-    return u;
+    return bc_chain_regs(u, W, h, sl + 1);
 }
 
 // Slack compaction's bookkeeping for one batch (what k_activate does as its own launch; here
@@ -1399,8 +1410,8 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                 if (blockIdx.x == 0) SX_STAMP(0);
                 SX_BSTAMP(0);
                 double a1 = a_pre;
-                if (hb && !done) a1 = stage1_col_w(a1, h1, bits1, wu1, s_p);
-                const double a = done ? 0.0 : hist_col_w(a1, qq, bits, s_hist, wu, s_p + hb);
+                if (hb && !done) a1 = stage1_col_bc(a1, h1, bits1, wu1, s_p);
+                const double a = done ? 0.0 : hist_col_bc(a1, qq, bits, s_hist, wu, s_p + hb);
                 double rv = DBL_MAX;
                 int ri = -1, elig = 0;
                 if (liveA && !done) {
@@ -1664,8 +1675,8 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                     cnt = q + 1;
                     // ---- objective tile: current pivot row on this column, d, tile winner
                     if (tb == 0) SX_STAMP(6);
-                    if (hb) u = stage1_row(u, h1, r, s_fr1, s_p, s_r);
-                    u = hist_row(u, qq, r, s_hist, s_fr, s_p + hb, s_r + hb);
+                    if (hb) u = stage1_row_bc(u, h1, r, s_fr1, s_p, s_r);
+                    u = hist_row_bc(u, qq, r, s_hist, s_fr, s_p + hb, s_r + hb);
                     s_hist[qq * SX_TILE + t] = u;
                     if (tb == 0) SX_STAMP(7);
                     const double fd = -dmin / p;  // updateCostsVector, solver.cu:48-56
@@ -1937,8 +1948,8 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 const int qq = q - hb;  // slot within the stage
                 const bool done = !(cmp_eps(dmin, 0.0) < 0);  // solver.cu:88: optimal
                 double a1 = a_pre;
-                if (hb && !done) a1 = stage1_col(a1, h1, bits1, s_ue1, s_p);
-                const double a = done ? 0.0 : hist_col(a1, qq, bits, s_hist, s_ue, s_p + hb);
+                if (hb && !done) a1 = stage1_col_bcl(a1, h1, bits1, s_ue1, s_p);
+                const double a = done ? 0.0 : hist_col_bcl(a1, qq, bits, s_hist, s_ue, s_p + hb);
                 double rv = DBL_MAX;
                 int ri = -1, elig = 0;
                 if (liveA && !done) {
@@ -2184,8 +2195,8 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 int i = -1;
                 if (ost == SX_NOT_ENDED) {
                     cnt = q + 1;
-                    if (hb) u = stage1_row(u, h1, r, s_fr1, s_p, s_r);
-                    u = hist_row(u, qq, r, s_hist, s_fr, s_p + hb, s_r + hb);
+                    if (hb) u = stage1_row_bc(u, h1, r, s_fr1, s_p, s_r);
+                    u = hist_row_bc(u, qq, r, s_hist, s_fr, s_p + hb, s_r + hb);
                     s_hist[qq * SX_TILE + t] = u;
                     const double fd = -dmin / p;  // updateCostsVector, solver.cu:48-56
                     if (tb == 0 && t == 0) d0 = fma(fd, br, d0);
