@@ -1093,22 +1093,102 @@ __device__ __forceinline__ double stage1_col_bc(double a, const double (&h)[SX_H
     if (bits) a = usl / s_p[sl];
     return bc_chain_regs_after(a, W, h, bits ? sl : -1, !bits);
 }
-// (the multi-rank batch's ratio tiles: the entering column's pending values U[s][e] in LDS, s_ue)
-__device__ __forceinline__ double hist_col_bcl(double a, int q, unsigned bits, const double *s_hist, const double *s_ue,
-                                               const double *s_p) {
-    const Bc2 W = bc2_from_lds(s_ue);
-    if (__ballot(bits != 0u) == 0ull) return bc_chain_lds(a, W, s_hist, 0, q);
-    const int sl = bits ? 31 - __builtin_clz(bits) : -1;
+// The multi-rank batch keeps the round-5 form of its chains: the slot value of each step read by
+// v_readlane into scalar registers (lane s of a wave register holds slot s).  Its register file is
+// full: with the broadcast form (two more register pairs per chain) its chain measured 0.1-0.25 us per
+// pivot slower on 2..8 virtual ranks (profiles/r06_dpp_chains_ab.txt).
+__device__ __forceinline__ double hist_col_rl(double a, int q, unsigned bits, const double *s_hist, const double *s_ue,
+                                              const double *s_p) {
+    const int t = threadIdx.x, lane = t & 63;
+    const double wu = s_ue[lane & (SX_HMAX - 1)];  // lane s: U[s][e]
+    if (__ballot(bits != 0u) == 0ull) {
+        int s = 0;
+        for (; s + 8 <= q; s += 8) {
+            double h[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) h[k] = s_hist[(s + k) * SX_TILE + t];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a = fma(h[k], rdlane(wu, s + k), a);
+        }
+        for (; s < q; ++s) a = fma(s_hist[s * SX_TILE + t], rdlane(wu, s), a);
+        return a;
+    }
+    const int sl = bits ? 31 - __builtin_clz(bits) : -1;  // the row's last leaving slot
     if (bits) a = s_ue[sl] / s_p[sl];
-    return bc_chain_lds_after(a, W, s_hist, q, sl, !bits);
+    for (int s0 = 0; s0 < q; s0 += 8) {  // (slots past q read slot s0 and are not used)
+        double h[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) h[k] = s_hist[(s0 + k < q ? s0 + k : s0) * SX_TILE + t];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (s0 + k < q) {
+                const double y = fma(h[k], rdlane(wu, s0 + k), a);
+                a = s0 + k > sl ? y : a;
+            }
+        }
+    }
+    return a;
 }
-__device__ __forceinline__ double stage1_col_bcl(double a, const double (&h)[SX_HMAX], unsigned bits, const double *s_u,
-                                                 const double *s_p) {
-    const Bc2 W = bc2_from_lds(s_u);
-    if (__ballot(bits != 0u) == 0ull) return bc_chain_regs(a, W, h, 0);
+__device__ __forceinline__ double stage1_col_rl(double a, const double (&h)[SX_HMAX], unsigned bits, const double *s_u,
+                                                const double *s_p) {
+    const int lane = threadIdx.x & 63;
+    const double wu = s_u[lane & (SX_HMAX - 1)];
+    if (__ballot(bits != 0u) == 0ull) {
+#pragma unroll
+        for (int s = 0; s < SX_HMAX; ++s) a = fma(h[s], rdlane(wu, s), a);
+        return a;
+    }
     const int sl = bits ? 31 - __builtin_clz(bits) : -1;
     if (bits) a = s_u[sl] / s_p[sl];
-    return bc_chain_regs_after(a, W, h, sl, !bits);
+#pragma unroll
+    for (int s = 0; s < SX_HMAX; ++s) {
+        const double y = fma(h[s], rdlane(wu, s), a);
+        a = s > sl ? y : a;
+    }
+    return a;
+}
+__device__ __forceinline__ double hist_row_rl(double u, int q, int r, const double *s_hist, const double *s_fr,
+                                              const double *s_p, const int *s_r) {
+    const int t = threadIdx.x, lane = t & 63;
+    const double wf = s_fr[lane & (SX_HMAX - 1)];  // lane s: F[r][s]
+    const unsigned long long left = __ballot(lane < q && s_r[lane < q ? lane : 0] == r);
+    int s = 0;
+    if (left) {
+        const int sl = 63 - __builtin_clzll(left);
+        u = s_hist[sl * SX_TILE + t] / s_p[sl];
+        s = sl + 1;
+    }
+    for (; s + 8 <= q; s += 8) {
+        double h[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) h[k] = s_hist[(s + k) * SX_TILE + t];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) u = fma(rdlane(wf, s + k), h[k], u);
+    }
+    for (; s < q; ++s) u = fma(rdlane(wf, s), s_hist[s * SX_TILE + t], u);
+    return u;
+}
+__device__ __forceinline__ double stage1_row_rl(double u, const double (&h)[SX_HMAX], int r, const double *s_f,
+                                                const double *s_p, const int *s_r) {
+    const int lane = threadIdx.x & 63;
+    const double wf = s_f[lane & (SX_HMAX - 1)];
+    const unsigned long long left = __ballot(lane < SX_HMAX && s_r[lane < SX_HMAX ? lane : 0] == r);
+    if (left == 0ull) {
+#pragma unroll
+        for (int s = 0; s < SX_HMAX; ++s) u = fma(rdlane(wf, s), h[s], u);
+        return u;
+    }
+    const int sl = 63 - __builtin_clzll(left);  // (block-uniform)
+    double hs = 0.0;
+#pragma unroll
+    for (int s = 0; s < SX_HMAX; ++s) hs = s == sl ? h[s] : hs;
+    u = hs / s_p[sl];
+#pragma unroll
+    for (int s = 0; s < SX_HMAX; ++s) {
+        const double y = fma(rdlane(wf, s), h[s], u);
+        u = s > sl ? y : u;
+    }
+    return u;
 }
 __device__ __forceinline__ double hist_row_bc(double u, int q, int r, const double *s_hist, const double *s_fr,
                                               const double *s_p, const int *s_r) {
@@ -1948,8 +2028,8 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 const int qq = q - hb;  // slot within the stage
                 const bool done = !(cmp_eps(dmin, 0.0) < 0);  // solver.cu:88: optimal
                 double a1 = a_pre;
-                if (hb && !done) a1 = stage1_col_bcl(a1, h1, bits1, s_ue1, s_p);
-                const double a = done ? 0.0 : hist_col_bcl(a1, qq, bits, s_hist, s_ue, s_p + hb);
+                if (hb && !done) a1 = stage1_col_rl(a1, h1, bits1, s_ue1, s_p);
+                const double a = done ? 0.0 : hist_col_rl(a1, qq, bits, s_hist, s_ue, s_p + hb);
                 double rv = DBL_MAX;
                 int ri = -1, elig = 0;
                 if (liveA && !done) {
@@ -2195,8 +2275,8 @@ __device__ __forceinline__ void batch_mr_body(int bid, unsigned nbl, const doubl
                 int i = -1;
                 if (ost == SX_NOT_ENDED) {
                     cnt = q + 1;
-                    if (hb) u = stage1_row_bc(u, h1, r, s_fr1, s_p, s_r);
-                    u = hist_row_bc(u, qq, r, s_hist, s_fr, s_p + hb, s_r + hb);
+                    if (hb) u = stage1_row_rl(u, h1, r, s_fr1, s_p, s_r);
+                    u = hist_row_rl(u, qq, r, s_hist, s_fr, s_p + hb, s_r + hb);
                     s_hist[qq * SX_TILE + t] = u;
                     const double fd = -dmin / p;  // updateCostsVector, solver.cu:48-56
                     if (tb == 0 && t == 0) d0 = fma(fd, br, d0);
