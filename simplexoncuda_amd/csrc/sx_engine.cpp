@@ -128,7 +128,8 @@ std::vector<UncachedRecords> g_urec;
 // freed such allocations -- the same code with every uncached U kept allocated was bit-exact in
 // 12 of 12 solves, with them freed it diverged in 4 of 12 -- so no engine frees one.  The pool
 // holds at most the largest set of such buffers alive at once, plus one buffer each time a solve
-// needs a larger one than any free (a process solving one shape repeatedly reuses one set).
+// needs a larger one than any free (a process solving one shape repeatedly reuses one set).  Pinned
+// host buffers (acquire_pinned) live in the same pool.
 struct SpecialBuf {
     int dev = -1;
     unsigned flags = 0;
@@ -455,10 +456,10 @@ class Engine {
             for (const auto &x : sh) split_ok = split_ok && x.fineU;
         if (!rccl && xchg) {
             // the shards' pivot-row contributions (pinned host memory: read by every device's kernel)
-            SX_HIP(hipHostMalloc(reinterpret_cast<void **>(&sum_srcs), sizeof(double *) * W, hipHostMallocDefault));
+            sum_srcs = acquire_pinned<const double *>((size_t)W);
             for (int k = 0; k < W; ++k) sum_srcs[k] = sh[(size_t)k].prow_send;
         }
-        SX_HIP(hipHostMalloc(reinterpret_cast<void **>(&st_host), 2 * sizeof(DevState), hipHostMallocDefault));
+        st_host = acquire_pinned<DevState>(2);
         for (auto &e : poll_ev) SX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         setup_peers();
     }
@@ -671,10 +672,10 @@ class Engine {
             DevGuard g(x.dev);
             free_shard(x);
         }
-        if (sum_srcs) (void)hipHostFree(sum_srcs);
+        if (sum_srcs) release_special(sum_srcs);
         if (c_dev) (void)hipFree(c_dev);
         if (u_bad) (void)hipFree(u_bad);
-        if (st_host) (void)hipHostFree(st_host);
+        if (st_host) release_special(st_host);
         for (auto &e : poll_ev)
             if (e) (void)hipEventDestroy(e);
         for (auto &kv : djoin) {
@@ -736,6 +737,32 @@ class Engine {
         b.busy = true;
         g_special.push_back(b);
         return b.p;
+    }
+    // pinned host memory (the engine's state mirror, the per-pivot exchange's source list) under the
+    // same rule: allocated once, reused by later engines, never freed (every
+    // non-plain allocation, not only U)
+    static constexpr unsigned kPinnedHost = 0xffffffffu;
+    template <typename T>
+    static T *acquire_pinned(size_t count) {
+        const size_t bytes = count * sizeof(T);
+        int best = -1;
+        for (size_t i = 0; i < g_special.size(); ++i) {
+            const SpecialBuf &b = g_special[i];
+            if (b.flags == kPinnedHost && !b.busy && b.bytes >= bytes &&
+                (best < 0 || b.bytes < g_special[(size_t)best].bytes))
+                best = (int)i;
+        }
+        if (best >= 0) {
+            g_special[(size_t)best].busy = true;
+            return static_cast<T *>(g_special[(size_t)best].p);
+        }
+        SpecialBuf b;
+        b.flags = kPinnedHost;
+        b.bytes = bytes;
+        SX_HIP(hipHostMalloc(&b.p, bytes, hipHostMallocDefault));
+        b.busy = true;
+        g_special.push_back(b);
+        return static_cast<T *>(b.p);
     }
     static void release_special(void *p) {
         for (auto &b : g_special)
