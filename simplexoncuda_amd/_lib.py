@@ -97,6 +97,7 @@ SIGNATURES = {
     "simplex_set_exchange_mode": (None, [ctypes.c_int]),
     "simplex_set_alias": (None, [ctypes.c_int]),
     "simplex_set_compact": (None, [ctypes.c_int]),
+    "simplex_set_deactivate": (None, [ctypes.c_int]),
     "simplex_set_fused": (None, [ctypes.c_int]),
     "simplex_last_phase_seconds": (None, [ctypes.POINTER(ctypes.c_double)]),
     "simplex_last_objective_row": (ctypes.c_longlong, [ctypes.POINTER(ctypes.c_double), ctypes.c_longlong]),

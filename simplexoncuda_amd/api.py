@@ -371,6 +371,12 @@ def set_compact(on):
     _lib.load().simplex_set_compact(1 if on else 0)
 
 
+def set_deactivate(on):
+    """With slack compaction on one shard (default on): sweeps also skip the slack columns that
+    entered the basis and are still basic (exact unit vectors)."""
+    _lib.load().simplex_set_deactivate(1 if on else 0)
+
+
 def set_fused(mode):
     """-1 auto (one launch per batch of pivots on a single shard), 0 two launches per pivot."""
     _lib.load().simplex_set_fused(int(mode))

@@ -202,21 +202,33 @@ void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, 
                      const Pending &pd, const DevState *st, int rev, SweepCfg cfg, hipStream_t s);
 // slack compaction, after a batch's selections and before its sweep: move the slack column
 // of every row that left the basis for the first time into the swept block
-void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, int m, double *T, int rows, int row0,
-                        size_t ld, TLay tl, int s0, const Pending &pd, const DevState *st, int slots,
+// (ucol[r]: the unswept slack column that is the unit vector e_r, or -1; urow[k]: the row of unswept
+// slack k's unit vector -- k itself until row k first leaves)
+void sx_launch_activate(int *perm, int *iperm, int *ucol, const int *urow, int *nact, int m, double *T, int rows,
+                        int row0, size_t ld, TLay tl, int s0, const Pending &pd, const DevState *st, int slots,
                         hipStream_t s);  // slots: the batch size (two passes above SX_HMAX)
+// one shard, after a batch's sweep: the slacks that entered in the batch and are still basic (their
+// columns exact unit vectors, checked) moved behind the swept block (k_deact_*)
+struct DeactPlan {
+    unsigned long long bad;  // candidates whose column is not e_r bit for bit (k_deact_check)
+    int nsw;                 // column exchanges of the batch
+    int dst[SX_KMAX], src[SX_KMAX], row[SX_KMAX];
+};
+void sx_launch_deactivate(int *perm, int *iperm, int *ucol, int *urow, int *nact, int n, int m, bool alias, double *T,
+                          int rows, TLay tl, int s0, const Pending &pd, const DevState *st, DeactPlan *plan,
+                          hipStream_t s);
 // fused batch of up to k pivots on one shard (ratio tiles + objective tiles in one resident
 // grid); returns false (nothing launched) when the grid cannot be resident at once
 bool sx_batch_fits(int rows, Cols c, int k);
 int sx_batch_obj_tile_limit();  // objective tiles a one-shard fused batch holds (logical width <= 512 x this + 1)
 // d_save: the objective row as the batch found it (restored by the host after SX_HANG); the
 // basis is written only by a batch that completed
-// perm / iperm / act / nact (slack compaction, or null): the batch's last block also activates
+// perm / iperm / ucol / urow / nact (slack compaction, or null): the batch's last block also activates
 // the slack columns of the rows that left the basis for the first time (k_activate's work)
 void sx_launch_batch(const double *T, int rows, size_t ld, TLay tl, Cols c, double *d, double *d_save, int *base,
                      DevState *st, const Pending &pd, int k, BatchChan *chan, unsigned long long *ga,
-                     unsigned long long *gb, unsigned long long *stamps, int *perm, int *iperm, unsigned char *act,
-                     int *nact, int m, hipStream_t s);
+                     unsigned long long *gb, unsigned long long *stamps, int *perm, int *iperm, int *ucol,
+                     const int *urow, int *nact, int m, hipStream_t s);
 size_t sx_batch_granules_a();
 size_t sx_batch_granules_b();
 // the multi-rank fused batch: `grids` co-resident launches of this shape must fit the device

@@ -1218,35 +1218,37 @@ __device__ __forceinline__ double stage1_row_bc(double u, const double (&h)[SX_H
 }
 
 // Slack compaction's bookkeeping for one batch (what k_activate does as its own launch; here
-// run by the fused batch's last block, after every other block has left): the first time row
-// r leaves the basis, its slack column -- still the unit vector e_r as built, never swept -- is
-// exchanged with the slack column at the first untouched stored position s0 + nact (also a
-// unit vector), so the swept block [0, s0 + nact) grows by one.  The exchanges of the batch are
+// run by the fused batch's last block, after every other block has left): when row r leaves the
+// basis and an unswept slack column is the unit vector e_r -- its own slack, untouched since the
+// build, or a slack that entered at row r and was moved out of the swept block since
+// (k_deact_*) -- that column (ucol[r]) is exchanged with the slack column at the first unswept
+// stored position s0 + nact (also a unit vector, of row urow[.]), so the swept block
+// [0, s0 + nact) grows by one.  The exchanges of the batch are
 // resolved in slot order by wave 0, one list entry per lane (stored offset, slack held before
 // the batch, slack held now); their net effect is then applied at once: to the pending pivot
 // rows U[s] (whose entries at the two columns are the leaving rows' current values there; the
 // objective blocks stored them write-through, and they are read here with sc1 loads), to T
-// (zeros and ones of the unit vectors) and to perm / iperm / act / nact.  All threads of the
+// (zeros and ones of the unit vectors) and to perm / iperm / ucol / nact.  All threads of the
 // block call it; s_rr[0..cnt) are the batch's leaving rows (local = global: one shard).
-__device__ void activate_block(int *__restrict__ perm, int *__restrict__ iperm, unsigned char *__restrict__ act,
+__device__ void activate_block(int *__restrict__ perm, int *__restrict__ iperm, int *__restrict__ ucol,
+                               const int *__restrict__ urow,
                                int *__restrict__ nact_p, int m, double *__restrict__ T, int rows, TLay tl, int s0,
                                double *__restrict__ U, size_t ld, int nU, const int *s_rr, int cnt, int *s_pl,
                                int *s_ol, int *s_cl, int *s_src, int *s_misc, double *s_u) {
     const int t = threadIdx.x;
     if (t < 64) {
         const int na0 = *nact_p;
-        int r = 0, a = 1, pr = 0, win = -1;
+        int kc = -1, pr = 0, win = -1;
         if (t < cnt) {
-            r = s_rr[t];
-            a = act[r];
-            pr = perm[r];
+            kc = ucol[s_rr[t]];  // the unswept slack column that is e_r, if any
+            pr = kc >= 0 ? perm[kc] : 0;
             if (na0 + t < m) win = iperm[na0 + t];
         }
         int pl = -1, ol = -1, cl = -1;  // this lane's list entry
         int nl = 0, added = 0;
         for (int s = 0; s < cnt; ++s) {
-            const int rs = __shfl(r, s);
-            if (__shfl(a, s)) continue;  // its slack was touched in an earlier batch
+            const int rs = __shfl(kc, s);  // (a slack id from here on)
+            if (rs < 0) continue;  // every column of the row's basic variable is swept already
             // already moved into the window in this batch?
             if (__ballot(t < nl && cl == rs && pl >= na0 && pl < na0 + added)) continue;
             const unsigned long long hP = __ballot(t < nl && cl == rs);
@@ -1313,14 +1315,15 @@ __device__ void activate_block(int *__restrict__ perm, int *__restrict__ iperm, 
     }
     if (t < nl) {
         const int x = s_pl[t], o = s_ol[t], cc = s_cl[t];
-        if (o != cc) {
-            if (o < rows) T[tl.idx(o, s0 + x)] = 0.0;
-            if (cc < rows) T[tl.idx(cc, s0 + x)] = 1.0;
+        if (o != cc) {  // (both unswept unit vectors before the batch: of rows urow[o], urow[cc])
+            const int ro = urow[o], rc = urow[cc];
+            if (ro < rows) T[tl.idx(ro, s0 + x)] = 0.0;
+            if (rc < rows) T[tl.idx(rc, s0 + x)] = 1.0;
         }
         iperm[x] = cc;
         perm[cc] = x;
         const int na0 = s_misc[2];
-        if (x >= na0 && x < na0 + s_misc[1]) act[cc] = 1;
+        if (x >= na0 && x < na0 + s_misc[1]) ucol[urow[cc]] = -1;
     }
     if (t == 0) *nact_p = s_misc[2] + s_misc[1];
 }
@@ -1378,7 +1381,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
                                                unsigned long long *PM, unsigned long long *PM2, unsigned B, int K,
                                                int NA, int NB,
                                                BatchChan *ch, u64 *ga, u64 *gb, unsigned long long *stamps,
-                                               int *perm, int *iperm, unsigned char *act, int *nact, int m) {
+                                               int *perm, int *iperm, int *ucol, const int *urow, int *nact, int m) {
     extern __shared__ double s_hist[];  // [stage slots][512]: F history (ratio blocks) / U history (objective blocks)
     __shared__ double s_v[16];
     __shared__ int s_i[16];
@@ -1862,7 +1865,7 @@ __global__ __launch_bounds__(512) void k_batch(const double *T, int rows, size_t
         // each swaps the entries of all the batch's pending rows U[s]
         for (int s1 = 0; s1 < cnt; s1 += SX_HMAX) {
             if (s1) __syncthreads();
-            activate_block(perm, iperm, act, nact, m, const_cast<double *>(T), rows, tl, c.s0, U, ld, cnt, s_r + s1,
+            activate_block(perm, iperm, ucol, urow, nact, m, const_cast<double *>(T), rows, tl, c.s0, U, ld, cnt, s_r + s1,
                            cnt - s1 < SX_HMAX ? cnt - s1 : SX_HMAX, reinterpret_cast<int *>(s_g),
                            reinterpret_cast<int *>(s_g) + 64, reinterpret_cast<int *>(s_g) + 128,
                            reinterpret_cast<int *>(s_g) + 192, reinterpret_cast<int *>(s_pay), s_hist);
@@ -2912,7 +2915,8 @@ __global__ __launch_bounds__(256, 2) void k_msweep(const double *Tsrc, double *T
 // does): a pass lists the exchanges of the slots [sb, sb + SX_HMAX) -- at most 2 entries per slot,
 // one per lane -- and swaps the entries of every pending row U[s], s < cnt.
 __global__ __launch_bounds__(256) void k_activate(int *__restrict__ perm, int *__restrict__ iperm,
-                                                  unsigned char *__restrict__ act, int *__restrict__ nact_p, int m,
+                                                  int *__restrict__ ucol, const int *__restrict__ urow,
+                                                  int *__restrict__ nact_p, int m,
                                                   double *__restrict__ T, int rows, int row0, size_t ld, TLay tl,
                                                   int s0, double *__restrict__ U, const PivRec *__restrict__ recs,
                                                   const DevState *__restrict__ st, unsigned B, int sb) {
@@ -2926,20 +2930,19 @@ __global__ __launch_bounds__(256) void k_activate(int *__restrict__ perm, int *_
     __shared__ int s_nl, s_added;
     __shared__ double s_u[SX_KMAX * 64];
     if (t < 64) {
-        // lane s: slot s's leaving row, whether its slack was ever touched, its stored offset,
-        // and the slack at window offset na0 + s
-        int r = 0, a = 1, pr = 0, win = -1;
+        // lane s: the unswept slack column that is the unit vector of slot s's leaving row (-1:
+        // none), its stored offset, and the slack at window offset na0 + s
+        int kc = -1, pr = 0, win = -1;
         if (t < pc) {
-            r = recs[t].r;
-            a = act[r];
-            pr = perm[r];
+            kc = ucol[recs[t].r];
+            pr = kc >= 0 ? perm[kc] : 0;
             if (na0 + t < m) win = iperm[na0 + t];
         }
         int pl = -1, ol = -1, cl = -1;  // this lane's list entry
         int nl = 0, added = 0;
         for (int s = 0; s < pc; ++s) {
-            const int rs = __shfl(r, s);
-            if (__shfl(a, s)) continue;  // its slack was touched in an earlier batch
+            const int rs = __shfl(kc, s);  // (a slack id from here on)
+            if (rs < 0) continue;  // every column of the row's basic variable is swept already
             // already moved into the window in this batch?
             if (__ballot(t < nl && cl == rs && pl >= na0 && pl < na0 + added)) continue;
             const unsigned long long hP = __ballot(t < nl && cl == rs);
@@ -3004,15 +3007,172 @@ __global__ __launch_bounds__(256) void k_activate(int *__restrict__ perm, int *_
     }
     if (t < nl) {
         const int x = s_pl[t], o = s_ol[t], c = s_cl[t];
-        if (o != c) {
-            if (o >= row0 && o < row0 + rows) T[tl.idx(o - row0, s0 + x)] = 0.0;
-            if (c >= row0 && c < row0 + rows) T[tl.idx(c - row0, s0 + x)] = 1.0;
+        if (o != c) {  // (both unswept unit vectors before the batch: of rows urow[o], urow[c])
+            const int ro = urow[o], rc = urow[c];
+            if (ro >= row0 && ro < row0 + rows) T[tl.idx(ro - row0, s0 + x)] = 0.0;
+            if (rc >= row0 && rc < row0 + rows) T[tl.idx(rc - row0, s0 + x)] = 1.0;
         }
         iperm[x] = c;
         perm[c] = x;
-        if (x >= na0 && x < na0 + s_added) act[c] = 1;
+        if (x >= na0 && x < na0 + s_added) ucol[urow[c]] = -1;
     }
     if (t == 0) *nact_p = na0 + s_added;
+}
+
+// Basic slack columns out of the sweep (one shard; after a batch's sweep).  A variable that enters
+// at pivot s leaves its column exactly the unit vector e_{r_s}: the pivot row becomes p / p = 1 and
+// every other row fma(-p / p, x, x) = x - x = +0 (solver.cu:34-46, finite x); every later pivot row
+// holds +0 there while the variable stays basic, so the reference's updates leave the column
+// bit-identical (fma(f, +0, +0) = +0, fma(f, +0, 1) = 1, finite f) until its row leaves again.  A
+// slack that entered in this batch and whose row did not leave again is therefore moved behind
+// the swept block, like the untouched slacks of slack compaction: the sweep stops before it, and
+// the next batch whose leaving row is r_s moves it back (activate_block / k_activate: ucol[r] is
+// the unswept column that is e_r, urow[k] the row of unswept slack k).  Three launches:
+//   k_deact_check  every row checks each candidate's stored column against e_r bit for bit (a
+//                  column that is not -- a non-finite entry at its entry -- stays swept);
+//   k_deact_plan   one wave: the candidates keep their stored positions if they lie in the last
+//                  d positions of the swept block, else each is exchanged with a non-candidate
+//                  there; perm / iperm / ucol / urow / nact updated;
+//   k_deact_move   the exchanges on T: the non-candidate's column copied to the candidate's old
+//                  position, e_r written at its new one.
+// Each candidate is a distinct slack with a distinct row (a slack that entered twice in the batch
+// left in between, so its row left after the first entry).
+__device__ __forceinline__ int deact_slack(int v, int n, int m, bool alias) {
+    if (v >= n && v < n + m) return v - n;
+    if (alias && v >= n + m && v < n + 2 * m) return v - n - m;  // (an artificial is stored as its slack)
+    return -1;
+}
+
+// lane s (< 64): slot s's slack id if it is a candidate (entered at slot s and its row r_s does not
+// leave at a later slot), else -1; *r = r_s
+__device__ __forceinline__ int deact_candidate(const PivRec *recs, int cnt, int n, int m, bool alias, int *r) {
+    const int l = (int)threadIdx.x & 63;
+    int rr = -1, k = -1;
+    if (l < cnt) {
+        rr = recs[l].r;
+        k = deact_slack(recs[l].e, n, m, alias);
+    }
+    bool later = false;
+    for (int s = 1; s < cnt; ++s) {  // (wave-uniform loop)
+        const int rs = __shfl(rr, s);
+        later = later || (s > l && rs == rr);
+    }
+    *r = rr;
+    return later ? -1 : k;
+}
+
+__global__ __launch_bounds__(256) void k_deact_check(const int *__restrict__ perm, int n, int m, bool alias,
+                                                     const double *__restrict__ T, int rows, TLay tl, int s0,
+                                                     const PivRec *__restrict__ recs, const DevState *__restrict__ st,
+                                                     unsigned B, DeactPlan *plan) {
+    const int cnt = st->batch_tag == B ? st->batch_count : 0;
+    if (cnt <= 0) return;
+    __shared__ int s_pos[SX_KMAX], s_row[SX_KMAX];
+    __shared__ unsigned long long s_bad;
+    const int t = threadIdx.x;
+    if (t < 64) {
+        int r;
+        const int k = deact_candidate(recs, cnt, n, m, alias, &r);
+        s_pos[t] = k >= 0 ? s0 + perm[k] : -1;
+        s_row[t] = r;
+        if (t == 0) s_bad = 0ull;
+    }
+    __syncthreads();
+    const int i = (int)blockIdx.x * 256 + t;
+    unsigned long long bad = 0ull;
+    if (i < rows)
+        for (int s = 0; s < cnt; ++s) {
+            const int x = s_pos[s];
+            if (x < 0) continue;
+            const double want = i == s_row[s] ? 1.0 : 0.0;
+            if (__double_as_longlong(T[tl.idx(i, x)]) != __double_as_longlong(want)) bad |= 1ull << s;
+        }
+    if (bad) atomicOr(&s_bad, bad);
+    __syncthreads();
+    if (t == 0 && s_bad) atomicOr(&plan->bad, s_bad);
+}
+
+__global__ __launch_bounds__(64) void k_deact_plan(int *__restrict__ perm, int *__restrict__ iperm,
+                                                   int *__restrict__ ucol, int *__restrict__ urow,
+                                                   int *__restrict__ nact_p, int n, int m, bool alias,
+                                                   const PivRec *__restrict__ recs, const DevState *__restrict__ st,
+                                                   unsigned B, DeactPlan *plan) {
+    const int l = threadIdx.x;
+    const int cnt = st->batch_tag == B ? st->batch_count : 0;
+    const unsigned long long bad = plan->bad;
+    if (l == 0) plan->bad = 0ull;  // (for the next batch)
+    if (cnt <= 0) {
+        if (l == 0) plan->nsw = 0;
+        return;
+    }
+    int r;
+    int k = deact_candidate(recs, cnt, n, m, alias, &r);
+    const int na = *nact_p;
+    int P = k >= 0 ? perm[k] : -1;
+    if (k >= 0 && (((bad >> l) & 1ull) || P >= na)) k = -1;  // (not e_r bit for bit / not swept)
+    const unsigned long long cand = __ballot(k >= 0);
+    const int d = __popcll(cand);
+    if (d == 0) {
+        if (l == 0) plan->nsw = 0;
+        return;
+    }
+    const int nna = na - d;  // the swept block after
+    const unsigned long long lower = (1ull << l) - 1ull;
+    // candidates outside the last d positions, in lane order
+    const unsigned long long outside = __ballot(k >= 0 && P < nna);
+    // lane l < d: tail position nna + l, its slack, and whether that slack is a candidate
+    const int Q = nna + l;
+    const int o = l < d ? iperm[Q] : -1;
+    bool oc = false;
+    for (int s = 0; s < 64; ++s) {  // (wave-uniform loop)
+        const int ks = __shfl(k, s);
+        oc = oc || (ks >= 0 && ks == o);
+    }
+    const unsigned long long free_tail = __ballot(l < d && !oc);  // tail positions to exchange into
+    // the j-th outside candidate is exchanged with the j-th free tail position
+    const int nsw = __popcll(outside);
+    int j = -1;
+    if ((outside >> l) & 1ull) j = __popcll(outside & lower);
+    int tl_lane = -1;  // lane holding the j-th free tail position
+    {
+        unsigned long long f = free_tail;
+        for (int q = 0; q < 64 && f; ++q) {
+            const int b = __builtin_ctzll(f);
+            f &= f - 1ull;
+            if (q == j) tl_lane = b;
+        }
+    }
+    const int Qj = __shfl(Q, tl_lane < 0 ? 0 : tl_lane), oj = __shfl(o, tl_lane < 0 ? 0 : tl_lane);
+    if (j >= 0) {
+        plan->dst[j] = P;   // the candidate's old position receives the tail slack's column
+        plan->src[j] = Qj;  // ... and the tail position receives e_r
+        plan->row[j] = r;
+        perm[k] = Qj;
+        iperm[Qj] = k;
+        perm[oj] = P;
+        iperm[P] = oj;
+    }
+    if (k >= 0) {
+        urow[k] = r;
+        ucol[r] = k;
+    }
+    if (l == 0) {
+        plan->nsw = nsw;
+        *nact_p = nna;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_deact_move(double *__restrict__ T, int rows, TLay tl, int s0,
+                                                    const DeactPlan *__restrict__ plan) {
+    const int nsw = plan->nsw;
+    if (nsw <= 0) return;
+    const int i = (int)blockIdx.x * 256 + (int)threadIdx.x;
+    if (i >= rows) return;
+    for (int j = 0; j < nsw; ++j) {
+        const int P = s0 + plan->dst[j], Q = s0 + plan->src[j];
+        T[tl.idx(i, P)] = T[tl.idx(i, Q)];
+        T[tl.idx(i, Q)] = i == plan->row[j] ? 1.0 : 0.0;
+    }
 }
 
 // Virtual-rank "allreduce": out = sum of the shards' contributions in rank order.  Exact,
@@ -3283,12 +3443,24 @@ static void launch_msweep(double *T, int rows, int row0, size_t ld, TLay tl, int
     }
 }
 
-void sx_launch_activate(int *perm, int *iperm, unsigned char *act, int *nact, int m, double *T, int rows, int row0,
-                        size_t ld, TLay tl, int s0, const Pending &pd, const DevState *st, int slots, hipStream_t s) {
-    k_activate<<<1, 256, 0, s>>>(perm, iperm, act, nact, m, T, rows, row0, ld, tl, s0, pd.U, pd.recs, st, pd.batch, 0);
+void sx_launch_activate(int *perm, int *iperm, int *ucol, const int *urow, int *nact, int m, double *T, int rows,
+                        int row0, size_t ld, TLay tl, int s0, const Pending &pd, const DevState *st, int slots,
+                        hipStream_t s) {
+    k_activate<<<1, 256, 0, s>>>(perm, iperm, ucol, urow, nact, m, T, rows, row0, ld, tl, s0, pd.U, pd.recs, st, pd.batch,
+                                 0);
     if (slots > SX_HMAX)
-        k_activate<<<1, 256, 0, s>>>(perm, iperm, act, nact, m, T, rows, row0, ld, tl, s0, pd.U, pd.recs, st, pd.batch,
-                                     SX_HMAX);
+        k_activate<<<1, 256, 0, s>>>(perm, iperm, ucol, urow, nact, m, T, rows, row0, ld, tl, s0, pd.U, pd.recs, st,
+                                     pd.batch, SX_HMAX);
+}
+
+void sx_launch_deactivate(int *perm, int *iperm, int *ucol, int *urow, int *nact, int n, int m, bool alias, double *T,
+                          int rows, TLay tl, int s0, const Pending &pd, const DevState *st, DeactPlan *plan,
+                          hipStream_t s) {
+    if (rows <= 0 || m <= 0) return;
+    const int g = (rows + 255) / 256;
+    k_deact_check<<<g, 256, 0, s>>>(perm, n, m, alias, T, rows, tl, s0, pd.recs, st, pd.batch, plan);
+    k_deact_plan<<<1, 64, 0, s>>>(perm, iperm, ucol, urow, nact, n, m, alias, pd.recs, st, pd.batch, plan);
+    k_deact_move<<<g, 256, 0, s>>>(T, rows, tl, s0, plan);
 }
 
 void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, const int *nact, int s0,
@@ -3346,13 +3518,13 @@ bool sx_batch_fits(int rows, Cols c, int k) {
 
 void sx_launch_batch(const double *T, int rows, size_t ld, TLay tl, Cols c, double *d, double *d_save, int *base,
                      DevState *st, const Pending &pd, int k, BatchChan *chan, unsigned long long *ga,
-                     unsigned long long *gb, unsigned long long *stamps, int *perm, int *iperm, unsigned char *act,
-                     int *nact, int m, hipStream_t s) {
+                     unsigned long long *gb, unsigned long long *stamps, int *perm, int *iperm, int *ucol,
+                     const int *urow, int *nact, int m, hipStream_t s) {
     if (!sx_batch_fits(rows, c, k)) SX_FATAL("fused batch grid does not fit the device");
     const int NA = (rows + SX_TILE - 1) / SX_TILE, NB = (c.N - 1 + SX_TILE - 1) / SX_TILE;
     k_batch<<<NA + NB, SX_TILE, batch_lds(k), s>>>(T, rows, ld, tl, c, d, d_save, base, st, pd.U, pd.F, pd.recs, pd.PM,
-                                                   pd.PM2, pd.batch, k, NA, NB, chan, ga, gb, stamps, perm, iperm, act,
-                                                   nact, m);
+                                                   pd.PM2, pd.batch, k, NA, NB, chan, ga, gb, stamps, perm, iperm, ucol,
+                                                   urow, nact, m);
 }
 
 bool sx_batch_mr_fits(int slots, int nb_local, int k, int grids) {
