@@ -71,10 +71,10 @@ void simplex_set_alias(int on);
  * an untouched unit vector, so it is kept past the swept block of the tableau and skipped by
  * every sweep -- bit-identical results; active only when no row is negated (b >= 0) */
 void simplex_set_compact(int on);
-/* with slack compaction on one shard (default on): after each sweep, the slacks that entered the
- * basis in the batch and are still basic -- their columns exact unit vectors, checked bit for bit --
- * are moved past the swept block too, and moved back when their row leaves; bit-identical results */
-void simplex_set_deactivate(int on);
+/* with slack compaction on one shard: every `every` sweeps (default 8; 0 off) the swept slack
+ * columns whose slack is basic -- exact unit vectors, checked bit for bit -- are moved past the swept
+ * block too, and moved back when their row leaves; bit-identical results */
+void simplex_set_deactivate(int every);
 /* one shard: run each batch of pivots as ONE resident launch (ratio tiles + objective-row tiles
  * handing off through write-through records) instead of two launches per pivot;
  * -1 auto (default: when the grid fits the device), 0 off */

@@ -9,7 +9,7 @@ from .api import (  # noqa: F401
     STATUS_NAMES, UNBOUNDED, Problem, Result, Session, bench_sweep, dev_argmin, dev_build_phase1,
     dev_build_phase1_generated, dev_pivots, dev_update_objective, generateRandomProblem, last_objective_row,
     generateRandomProblemDevice, gpus, p2p_ready, printProblemToStream, readProblemFromFile, readRandomProblemFromFile,
-    set_alias, set_batch, set_compact, set_deactivate, set_exchange_mode, set_force_exchange, set_fused, set_mr_single_launch,
+    DEACTIVATE_EVERY, set_alias, set_batch, set_compact, set_deactivate, set_exchange_mode, set_force_exchange, set_fused, set_mr_single_launch,
     set_blocked, set_fine_pivot_rows, set_gpus, set_p2p, set_regions, set_replicated_objective, set_sweep_mfma,
     set_update_waves, set_verbose, set_virtual_ranks,
     twoPhaseMethod, twoPhaseMethodEx)

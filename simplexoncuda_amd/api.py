@@ -371,10 +371,13 @@ def set_compact(on):
     _lib.load().simplex_set_compact(1 if on else 0)
 
 
-def set_deactivate(on):
-    """With slack compaction on one shard (default on): sweeps also skip the slack columns that
-    entered the basis and are still basic (exact unit vectors)."""
-    _lib.load().simplex_set_deactivate(1 if on else 0)
+DEACTIVATE_EVERY = 8  # the engine's default
+
+
+def set_deactivate(every):
+    """With slack compaction on one shard: every `every` sweeps (default 8; 0 off) the swept slack
+    columns whose slack is basic (exact unit vectors) leave the swept block."""
+    _lib.load().simplex_set_deactivate(int(every))
 
 
 def set_fused(mode):

@@ -207,16 +207,17 @@ void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, 
 void sx_launch_activate(int *perm, int *iperm, int *ucol, const int *urow, int *nact, int m, double *T, int rows,
                         int row0, size_t ld, TLay tl, int s0, const Pending &pd, const DevState *st, int slots,
                         hipStream_t s);  // slots: the batch size (two passes above SX_HMAX)
-// one shard, after a batch's sweep: the slacks that entered in the batch and are still basic (their
-// columns exact unit vectors, checked) moved behind the swept block (k_deact_*)
-struct DeactPlan {
-    unsigned long long bad;  // candidates whose column is not e_r bit for bit (k_deact_check)
-    int nsw;                 // column exchanges of the batch
-    int dst[SX_KMAX], src[SX_KMAX], row[SX_KMAX];
+// one shard, after a sweep (every few batches): the swept slack columns whose slack is basic (exact
+// unit vectors, checked) moved behind the swept block (k_deact_*)
+#define SX_DEACT_CAP 4096  // columns per round (a multiple of 1024)
+struct DeactList {
+    int C;    // listed columns (swept slacks that are basic), stored-position order
+    int nsw;  // column exchanges of the round
+    int x[SX_DEACT_CAP], r[SX_DEACT_CAP], bad[SX_DEACT_CAP];  // position, unit row, failed the check
+    int dst[SX_DEACT_CAP], src[SX_DEACT_CAP], row[SX_DEACT_CAP];
 };
-void sx_launch_deactivate(int *perm, int *iperm, int *ucol, int *urow, int *nact, int n, int m, bool alias, double *T,
-                          int rows, TLay tl, int s0, const Pending &pd, const DevState *st, DeactPlan *plan,
-                          hipStream_t s);
+void sx_launch_deactivate(int *perm, int *iperm, int *ucol, int *urow, int *nact, const int *base, int n, int m,
+                          bool alias, double *T, int rows, TLay tl, int s0, int *crow, DeactList *L, hipStream_t s);
 // fused batch of up to k pivots on one shard (ratio tiles + objective tiles in one resident
 // grid); returns false (nothing launched) when the grid cannot be resident at once
 bool sx_batch_fits(int rows, Cols c, int k);

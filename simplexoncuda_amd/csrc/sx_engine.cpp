@@ -64,8 +64,8 @@ struct Config {
     int exchange_mode = 0;   // 0 auto, 1 tile allgather + row allreduce, 2 row-gather
     int alias = 1;           // store phase-1 artificial columns as their slack columns
     int compact = 1;         // sweep only the slack columns pivots have touched (when exact)
-    int deact = -1;          // ... and move slacks that entered and stay basic out of the sweep (one shard;
-                             // -1: SIMPLEX_DEACTIVATE=0/1, else on)
+    int deact = -1;          // ... and move the swept slacks that are basic out of the sweep every `deact`
+                             // sweeps (one shard; 0 off; -1: SIMPLEX_DEACTIVATE=k, else 8)
     int mr_single_launch = 1;  // virtual shards: all ranks' fused batches as one launch (0: one per stream)
     int regions = 1;         // two-region tableau layout (TLay): 0 off, 1 auto (aliasing, m > 4096),
                              // >= 2: region A holds that many slack positions (test hook)
@@ -297,7 +297,8 @@ struct Shard {
     int *ucol = nullptr;              //   row r -> the unswept slack column that is e_r, or -1 [m]
     int *urow = nullptr;              //   unswept slack k -> the row of its unit vector [m]
     int *nact = nullptr;              //   swept slack columns (the swept block's width past 1+n)
-    DeactPlan *dplan = nullptr;       //   basic slacks moved out of the sweep (one shard)
+    DeactList *dlist = nullptr;       //   basic slacks moved out of the sweep (one shard)
+    int *dcrow = nullptr;             //   its scratch: stored slack offset -> basic row [m]
     double *F = nullptr;              // pending row factors [rows][SX_KMAX]
     PivRec *recs = nullptr;           // pending pivot records [SX_KMAX]
     unsigned long long *PM = nullptr; // [rows] pending leaving-row slots (batch-tagged)
@@ -881,7 +882,7 @@ class Engine {
                         (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
                         (void *)x.rhs_all, (void *)x.base, (void *)x.enter_parts, (void *)x.tiles_local, (void *)x.chan,
                         (void *)x.ga, (void *)x.gb, (void *)x.gdone, (void *)x.perm, (void *)x.iperm,
-                        (void *)x.ucol, (void *)x.urow, (void *)x.nact, (void *)x.dplan,
+                        (void *)x.ucol, (void *)x.urow, (void *)x.nact, (void *)x.dlist, (void *)x.dcrow,
                         (void *)x.tiles_all, (void *)x.st})
             if (p) (void)hipFree(p);
     }
@@ -1143,14 +1144,15 @@ class Engine {
                     x.ucol = dalloc<int>(m);
                     x.urow = dalloc<int>(m);
                     x.nact = dalloc<int>(1);
-                    x.dplan = dalloc<DeactPlan>(1);
+                    x.dlist = dalloc<DeactList>(1);
+                    x.dcrow = dalloc<int>(m);
                 }
                 SX_HIP(hipMemcpyAsync(x.perm, id.data(), sizeof(int) * m, hipMemcpyHostToDevice, x.s));
                 SX_HIP(hipMemcpyAsync(x.iperm, id.data(), sizeof(int) * m, hipMemcpyHostToDevice, x.s));
                 SX_HIP(hipMemcpyAsync(x.ucol, id.data(), sizeof(int) * m, hipMemcpyHostToDevice, x.s));
                 SX_HIP(hipMemcpyAsync(x.urow, id.data(), sizeof(int) * m, hipMemcpyHostToDevice, x.s));
                 SX_HIP(hipMemsetAsync(x.nact, 0, sizeof(int), x.s));
-                SX_HIP(hipMemsetAsync(x.dplan, 0, sizeof(DeactPlan), x.s));
+                SX_HIP(hipMemsetAsync(x.dlist, 0, sizeof(DeactList), x.s));
             }
             sync_all();
         }
@@ -1422,15 +1424,15 @@ class Engine {
         }
         if (rec_shard0) sx_set_sweep_record(nullptr);
         if (ev1) SX_HIP(hipEventRecord(ev1, s));
-        // one shard: the slacks that entered in this batch and stay basic leave the swept block
+        // one shard, every g_cfg.deact sweeps: the swept slacks that are basic leave the swept block
         if (g_cfg.deact < 0) {
             const char *e = getenv("SIMPLEX_DEACTIVATE");
-            g_cfg.deact = e && atoi(e) == 0 ? 0 : 1;
+            g_cfg.deact = e ? (atoi(e) > 0 ? atoi(e) : 0) : 8;
         }
-        if (compact && W == 1 && g_cfg.deact != 0) {
+        if (compact && W == 1 && g_cfg.deact > 0 && (sweeps + 1) % g_cfg.deact == 0) {
             Shard &x = sh[0];
-            sx_launch_deactivate(x.perm, x.iperm, x.ucol, x.urow, x.nact, n, m, cols(N).art0 != 0x7fffffff, x.T, x.rows,
-                                 tl, 1 + n, pending(x), x.st, x.dplan, x.s);
+            sx_launch_deactivate(x.perm, x.iperm, x.ucol, x.urow, x.nact, x.base, n, m, cols(N).art0 != 0x7fffffff, x.T,
+                                 x.rows, tl, 1 + n, x.dcrow, x.dlist, x.s);
         }
         ++sweeps;
         q_host = 0;
@@ -2024,7 +2026,7 @@ void simplex_set_alias(int on) { g_cfg.alias = on ? 1 : 0; }
 void simplex_set_regions(int mode) { g_cfg.regions = mode < 0 ? 1 : mode; }
 void simplex_set_mr_single_launch(int on) { g_cfg.mr_single_launch = on ? 1 : 0; }
 void simplex_set_compact(int on) { g_cfg.compact = on ? 1 : 0; }
-void simplex_set_deactivate(int on) { g_cfg.deact = on ? 1 : 0; }
+void simplex_set_deactivate(int every) { g_cfg.deact = every > 0 ? every : 0; }
 void simplex_set_fused(int mode) { g_cfg.fused = mode < 0 ? -1 : (mode ? 1 : 0); }
 void simplex_set_p2p(int mode) { g_cfg.p2p = mode < 0 ? -1 : (mode ? 1 : 0); }
 int simplex_p2p_ready(void) {

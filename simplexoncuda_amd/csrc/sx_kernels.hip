@@ -3019,159 +3019,193 @@ __global__ __launch_bounds__(256) void k_activate(int *__restrict__ perm, int *_
     if (t == 0) *nact_p = na0 + s_added;
 }
 
-// Basic slack columns out of the sweep (one shard; after a batch's sweep).  A variable that enters
-// at pivot s leaves its column exactly the unit vector e_{r_s}: the pivot row becomes p / p = 1 and
-// every other row fma(-p / p, x, x) = x - x = +0 (solver.cu:34-46, finite x); every later pivot row
-// holds +0 there while the variable stays basic, so the reference's updates leave the column
-// bit-identical (fma(f, +0, +0) = +0, fma(f, +0, 1) = 1, finite f) until its row leaves again.  A
-// slack that entered in this batch and whose row did not leave again is therefore moved behind
-// the swept block, like the untouched slacks of slack compaction: the sweep stops before it, and
-// the next batch whose leaving row is r_s moves it back (activate_block / k_activate: ucol[r] is
-// the unswept column that is e_r, urow[k] the row of unswept slack k).  Three launches:
-//   k_deact_check  every row checks each candidate's stored column against e_r bit for bit (a
-//                  column that is not -- a non-finite entry at its entry -- stays swept);
-//   k_deact_plan   one wave: the candidates keep their stored positions if they lie in the last
-//                  d positions of the swept block, else each is exchanged with a non-candidate
-//                  there; perm / iperm / ucol / urow / nact updated;
-//   k_deact_move   the exchanges on T: the non-candidate's column copied to the candidate's old
-//                  position, e_r written at its new one.
-// Each candidate is a distinct slack with a distinct row (a slack that entered twice in the batch
-// left in between, so its row left after the first entry).
+// Basic slack columns out of the sweep (one shard; after a sweep, every few batches).  A variable
+// that enters at row r leaves its column exactly the unit vector e_r: the pivot row becomes p / p = 1
+// and every other row fma(-p / p, x, x) = x - x = +0 (solver.cu:34-46, finite x); every later pivot
+// row holds +0 there while the variable stays basic, so the reference's updates leave the column
+// bit-identical (fma(f, +0, +0) = +0, fma(f, +0, 1) = 1, finite f) until row r leaves.  The swept
+// slack columns whose slack is basic are therefore moved behind the swept block, like the untouched
+// slacks of slack compaction: the sweep stops before them, and the batch whose leaving row is r moves
+// the column back (activate_block / k_activate: ucol[r] is the unswept column that is e_r, urow[k]
+// the row of unswept slack k).  Four launches:
+//   k_deact_list   one block: the rows whose basic variable is a swept slack (the basis), in stored
+//                  position order (at most SX_DEACT_CAP; the rest wait for the next round);
+//   k_deact_check  every row compares each listed column with e_r bit for bit (a column that is not
+//                  -- a non-finite entry when it entered -- stays swept);
+//   k_deact_plan   one block: the d checked columns keep their positions if they lie in the last d
+//                  positions of the swept block, else each is exchanged with a column there that is
+//                  not one of them (the j-th such candidate with the j-th such position); perm / iperm /
+//                  ucol / urow / nact updated;
+//   k_deact_move   the exchanges on T: the other column copied to the candidate's position, e_r
+//                  written at the candidate's new one.
 __device__ __forceinline__ int deact_slack(int v, int n, int m, bool alias) {
     if (v >= n && v < n + m) return v - n;
     if (alias && v >= n + m && v < n + 2 * m) return v - n - m;  // (an artificial is stored as its slack)
     return -1;
 }
 
-// lane s (< 64): slot s's slack id if it is a candidate (entered at slot s and its row r_s does not
-// leave at a later slot), else -1; *r = r_s
-__device__ __forceinline__ int deact_candidate(const PivRec *recs, int cnt, int n, int m, bool alias, int *r) {
-    const int l = (int)threadIdx.x & 63;
-    int rr = -1, k = -1;
-    if (l < cnt) {
-        rr = recs[l].r;
-        k = deact_slack(recs[l].e, n, m, alias);
+// exclusive prefix sum of v over a block of 1024 threads (s_w: 16 ints of LDS); *total = the sum
+__device__ __forceinline__ int block_exscan1024(int v, int *s_w, int *total) {
+    const int t = threadIdx.x, l = t & 63, w = t >> 6;
+    int x = v;  // inclusive scan within the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (l >= o) x += y;
     }
-    bool later = false;
-    for (int s = 1; s < cnt; ++s) {  // (wave-uniform loop)
-        const int rs = __shfl(rr, s);
-        later = later || (s > l && rs == rr);
+    if (l == 63) s_w[w] = x;
+    __syncthreads();
+    int before = 0, all = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int c = s_w[k];
+        before += k < w ? c : 0;
+        all += c;
     }
-    *r = rr;
-    return later ? -1 : k;
+    __syncthreads();  // (s_w reusable)
+    *total = all;
+    return before + x - v;
 }
 
-__global__ __launch_bounds__(256) void k_deact_check(const int *__restrict__ perm, int n, int m, bool alias,
-                                                     const double *__restrict__ T, int rows, TLay tl, int s0,
-                                                     const PivRec *__restrict__ recs, const DevState *__restrict__ st,
-                                                     unsigned B, DeactPlan *plan) {
-    const int cnt = st->batch_tag == B ? st->batch_count : 0;
-    if (cnt <= 0) return;
-    __shared__ int s_pos[SX_KMAX], s_row[SX_KMAX];
-    __shared__ unsigned long long s_bad;
+__global__ __launch_bounds__(1024) void k_deact_list(const int *__restrict__ base, const int *__restrict__ perm,
+                                                     const int *__restrict__ nact_p, int n, int m, bool alias,
+                                                     int *__restrict__ crow, DeactList *L) {
+    __shared__ int s_w[16];
     const int t = threadIdx.x;
-    if (t < 64) {
-        int r;
-        const int k = deact_candidate(recs, cnt, n, m, alias, &r);
-        s_pos[t] = k >= 0 ? s0 + perm[k] : -1;
-        s_row[t] = r;
-        if (t == 0) s_bad = 0ull;
+    const int na = *nact_p;
+    for (int x = t; x < na; x += 1024) crow[x] = -1;
+    __syncthreads();
+    for (int i = t; i < m; i += 1024) {
+        const int k = deact_slack(base[i], n, m, alias);
+        if (k >= 0) {
+            const int x = perm[k];
+            if (x < na) crow[x] = i;  // (a swept slack basic in row i)
+        }
     }
     __syncthreads();
-    const int i = (int)blockIdx.x * 256 + t;
-    unsigned long long bad = 0ull;
-    if (i < rows)
-        for (int s = 0; s < cnt; ++s) {
-            const int x = s_pos[s];
-            if (x < 0) continue;
-            const double want = i == s_row[s] ? 1.0 : 0.0;
-            if (__double_as_longlong(T[tl.idx(i, x)]) != __double_as_longlong(want)) bad |= 1ull << s;
+    const int chunk = (na + 1023) / 1024, x0 = t * chunk, x1 = x0 + chunk < na ? x0 + chunk : na;
+    int c = 0;
+    for (int x = x0; x < x1; ++x) c += crow[x] >= 0;
+    int total;
+    int o = block_exscan1024(c, s_w, &total);
+    for (int x = x0; x < x1 && o < SX_DEACT_CAP; ++x)
+        if (crow[x] >= 0) {
+            L->x[o] = x;
+            L->r[o] = crow[x];
+            L->bad[o] = 0;
+            ++o;
         }
-    if (bad) atomicOr(&s_bad, bad);
-    __syncthreads();
-    if (t == 0 && s_bad) atomicOr(&plan->bad, s_bad);
+    if (t == 0) L->C = total < SX_DEACT_CAP ? total : SX_DEACT_CAP;
 }
 
-__global__ __launch_bounds__(64) void k_deact_plan(int *__restrict__ perm, int *__restrict__ iperm,
-                                                   int *__restrict__ ucol, int *__restrict__ urow,
-                                                   int *__restrict__ nact_p, int n, int m, bool alias,
-                                                   const PivRec *__restrict__ recs, const DevState *__restrict__ st,
-                                                   unsigned B, DeactPlan *plan) {
-    const int l = threadIdx.x;
-    const int cnt = st->batch_tag == B ? st->batch_count : 0;
-    const unsigned long long bad = plan->bad;
-    if (l == 0) plan->bad = 0ull;  // (for the next batch)
-    if (cnt <= 0) {
-        if (l == 0) plan->nsw = 0;
-        return;
+__global__ __launch_bounds__(256) void k_deact_check(const double *__restrict__ T, int rows, TLay tl, int s0,
+                                                     DeactList *L) {
+    const int C = L->C;
+    const int i = (int)blockIdx.x * 256 + (int)threadIdx.x;
+    if (i >= rows) return;
+    for (int j = 0; j < C; ++j) {
+        const double want = i == L->r[j] ? 1.0 : 0.0;
+        if (__double_as_longlong(T[tl.idx(i, s0 + L->x[j])]) != __double_as_longlong(want)) L->bad[j] = 1;
     }
-    int r;
-    int k = deact_candidate(recs, cnt, n, m, alias, &r);
-    const int na = *nact_p;
-    int P = k >= 0 ? perm[k] : -1;
-    if (k >= 0 && (((bad >> l) & 1ull) || P >= na)) k = -1;  // (not e_r bit for bit / not swept)
-    const unsigned long long cand = __ballot(k >= 0);
-    const int d = __popcll(cand);
+}
+
+__global__ __launch_bounds__(1024) void k_deact_plan(int *__restrict__ perm, int *__restrict__ iperm,
+                                                     int *__restrict__ ucol, int *__restrict__ urow,
+                                                     int *__restrict__ nact_p, DeactList *L) {
+    __shared__ int s_w[16];
+    __shared__ int s_free[SX_DEACT_CAP];           // tail positions that receive a candidate
+    __shared__ unsigned s_tail[SX_DEACT_CAP / 32];  // tail positions held by a candidate (bits)
+    const int t = threadIdx.x;
+    const int C = L->C, na = *nact_p;
+    constexpr int PER = SX_DEACT_CAP / 1024;
+    // candidates: list entries j = PER t .. PER t + PER - 1 that passed the check
+    int ok[PER], nok = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int j = PER * t + q;
+        ok[q] = j < C && L->bad[j] == 0;
+        nok += ok[q];
+    }
+    int d;
+    const int before = block_exscan1024(nok, s_w, &d);
+    (void)before;
     if (d == 0) {
-        if (l == 0) plan->nsw = 0;
+        if (t == 0) L->nsw = 0;
         return;
     }
     const int nna = na - d;  // the swept block after
-    const unsigned long long lower = (1ull << l) - 1ull;
-    // candidates outside the last d positions, in lane order
-    const unsigned long long outside = __ballot(k >= 0 && P < nna);
-    // lane l < d: tail position nna + l, its slack, and whether that slack is a candidate
-    const int Q = nna + l;
-    const int o = l < d ? iperm[Q] : -1;
-    bool oc = false;
-    for (int s = 0; s < 64; ++s) {  // (wave-uniform loop)
-        const int ks = __shfl(k, s);
-        oc = oc || (ks >= 0 && ks == o);
+    for (int k = t; k < SX_DEACT_CAP / 32; k += 1024) s_tail[k] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int j = PER * t + q;
+        if (ok[q] && L->x[j] >= nna) atomicOr(&s_tail[(L->x[j] - nna) >> 5], 1u << ((L->x[j] - nna) & 31));
     }
-    const unsigned long long free_tail = __ballot(l < d && !oc);  // tail positions to exchange into
-    // the j-th outside candidate is exchanged with the j-th free tail position
-    const int nsw = __popcll(outside);
-    int j = -1;
-    if ((outside >> l) & 1ull) j = __popcll(outside & lower);
-    int tl_lane = -1;  // lane holding the j-th free tail position
+    __syncthreads();
+    // free tail positions (not a candidate's), in order: the j-th receives the j-th outside candidate
     {
-        unsigned long long f = free_tail;
-        for (int q = 0; q < 64 && f; ++q) {
-            const int b = __builtin_ctzll(f);
-            f &= f - 1ull;
-            if (q == j) tl_lane = b;
+        const int chunk = (d + 1023) / 1024, y0 = t * chunk, y1 = y0 + chunk < d ? y0 + chunk : d;
+        int c = 0;
+        for (int y = y0; y < y1; ++y) c += !((s_tail[y >> 5] >> (y & 31)) & 1u);
+        int tot;
+        int o = block_exscan1024(c, s_w, &tot);
+        for (int y = y0; y < y1; ++y)
+            if (!((s_tail[y >> 5] >> (y & 31)) & 1u)) s_free[o++] = nna + y;
+    }
+    __syncthreads();
+    // outside candidates (position < nna), in list (= position) order
+    int nout = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) nout += ok[q] && L->x[PER * t + q] < nna;
+    int nsw;
+    int o = block_exscan1024(nout, s_w, &nsw);
+    // read every slack involved before any write
+    int kc[PER], ko[PER], Pq[PER], Qq[PER], jo[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int j = PER * t + q;
+        kc[q] = ok[q] ? iperm[L->x[j]] : -1;
+        jo[q] = -1;
+        if (ok[q] && L->x[j] < nna) {
+            jo[q] = o++;
+            Pq[q] = L->x[j];
+            Qq[q] = s_free[jo[q]];
+            ko[q] = iperm[Qq[q]];
         }
     }
-    const int Qj = __shfl(Q, tl_lane < 0 ? 0 : tl_lane), oj = __shfl(o, tl_lane < 0 ? 0 : tl_lane);
-    if (j >= 0) {
-        plan->dst[j] = P;   // the candidate's old position receives the tail slack's column
-        plan->src[j] = Qj;  // ... and the tail position receives e_r
-        plan->row[j] = r;
-        perm[k] = Qj;
-        iperm[Qj] = k;
-        perm[oj] = P;
-        iperm[P] = oj;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int j = PER * t + q;
+        if (kc[q] < 0) continue;
+        const int r = L->r[j];
+        urow[kc[q]] = r;
+        ucol[r] = kc[q];
+        if (jo[q] >= 0) {
+            L->dst[jo[q]] = Pq[q];
+            L->src[jo[q]] = Qq[q];
+            L->row[jo[q]] = r;
+            perm[kc[q]] = Qq[q];
+            iperm[Qq[q]] = kc[q];
+            perm[ko[q]] = Pq[q];
+            iperm[Pq[q]] = ko[q];
+        }
     }
-    if (k >= 0) {
-        urow[k] = r;
-        ucol[r] = k;
-    }
-    if (l == 0) {
-        plan->nsw = nsw;
+    if (t == 0) {
+        L->nsw = nsw;
         *nact_p = nna;
     }
 }
 
 __global__ __launch_bounds__(256) void k_deact_move(double *__restrict__ T, int rows, TLay tl, int s0,
-                                                    const DeactPlan *__restrict__ plan) {
-    const int nsw = plan->nsw;
-    if (nsw <= 0) return;
+                                                    const DeactList *__restrict__ L) {
+    const int nsw = L->nsw;
     const int i = (int)blockIdx.x * 256 + (int)threadIdx.x;
-    if (i >= rows) return;
+    if (nsw <= 0 || i >= rows) return;
     for (int j = 0; j < nsw; ++j) {
-        const int P = s0 + plan->dst[j], Q = s0 + plan->src[j];
+        const int P = s0 + L->dst[j], Q = s0 + L->src[j];
         T[tl.idx(i, P)] = T[tl.idx(i, Q)];
-        T[tl.idx(i, Q)] = i == plan->row[j] ? 1.0 : 0.0;
+        T[tl.idx(i, Q)] = i == L->row[j] ? 1.0 : 0.0;
     }
 }
 
@@ -3453,14 +3487,14 @@ void sx_launch_activate(int *perm, int *iperm, int *ucol, const int *urow, int *
                                      pd.batch, SX_HMAX);
 }
 
-void sx_launch_deactivate(int *perm, int *iperm, int *ucol, int *urow, int *nact, int n, int m, bool alias, double *T,
-                          int rows, TLay tl, int s0, const Pending &pd, const DevState *st, DeactPlan *plan,
-                          hipStream_t s) {
+void sx_launch_deactivate(int *perm, int *iperm, int *ucol, int *urow, int *nact, const int *base, int n, int m,
+                          bool alias, double *T, int rows, TLay tl, int s0, int *crow, DeactList *L, hipStream_t s) {
     if (rows <= 0 || m <= 0) return;
     const int g = (rows + 255) / 256;
-    k_deact_check<<<g, 256, 0, s>>>(perm, n, m, alias, T, rows, tl, s0, pd.recs, st, pd.batch, plan);
-    k_deact_plan<<<1, 64, 0, s>>>(perm, iperm, ucol, urow, nact, n, m, alias, pd.recs, st, pd.batch, plan);
-    k_deact_move<<<g, 256, 0, s>>>(T, rows, tl, s0, plan);
+    k_deact_list<<<1, 1024, 0, s>>>(base, perm, nact, n, m, alias, crow, L);
+    k_deact_check<<<g, 256, 0, s>>>(T, rows, tl, s0, L);
+    k_deact_plan<<<1, 1024, 0, s>>>(perm, iperm, ucol, urow, nact, L);
+    k_deact_move<<<g, 256, 0, s>>>(T, rows, tl, s0, L);
 }
 
 void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, const int *nact, int s0,

@@ -51,10 +51,11 @@ def _session_run(p, stops, deact, fused, batch):
     finally:
         sx.set_batch(0)
         sx.set_fused(-1)
-        sx.set_deactivate(1)
+        sx.set_deactivate(sx.DEACTIVATE_EVERY)
     return out
 
 
+@pytest.mark.parametrize("every", [1, 3])
 @pytest.mark.parametrize("n,m,stops,fused,batch", [
     (64, 700, (150, 400, 700), -1, 0),     # fused batches (32 pivots below 4096 rows)
     (64, 700, (150, 400, 700), 0, 0),      # per-pivot launches + k_activate
@@ -62,9 +63,10 @@ def _session_run(p, stops, deact, fused, batch):
     (300, 1100, (300, 900), -1, 64),
     (16, 1536, (500, 1200), -1, 64),       # few structurals: the slacks re-enter quickly
 ])
-def test_deactivated_slacks_tableau_bit_exact(gpu, n, m, stops, fused, batch):
+def test_deactivated_slacks_tableau_bit_exact(gpu, n, m, stops, fused, batch, every):
+    """(every: sweeps between two rounds of moving basic slacks out)"""
     p = sx.generateRandomProblem(n, m, n * 100 + m + 7, 1, 100)
-    on = _session_run(p, stops, 1, fused, batch)
+    on = _session_run(p, stops, every, fused, batch)
     off = _session_run(p, stops, 0, fused, batch)
     assert len(on) == len(off)
     moved_out = False
@@ -78,7 +80,7 @@ def test_deactivated_slacks_tableau_bit_exact(gpu, n, m, stops, fused, batch):
     assert moved_out  # (basic slacks did leave the sweep)
 
 
-@pytest.mark.parametrize("deact", [1, 0])
+@pytest.mark.parametrize("deact", [1, 8, 0])
 @pytest.mark.parametrize("n,m,seed", [(300, 1100, 41100), (64, 128, 6528), (16, 1536, 1637), (129, 1513, 77)])
 def test_deactivated_slacks_two_phase(gpu, n, m, seed, deact):
     p = sx.generateRandomProblem(n, m, seed, 1, 100)
@@ -86,7 +88,7 @@ def test_deactivated_slacks_two_phase(gpu, n, m, seed, deact):
         sx.set_deactivate(deact)
         got = sx.twoPhaseMethodEx(p)
     finally:
-        sx.set_deactivate(1)
+        sx.set_deactivate(sx.DEACTIVATE_EVERY)
     A, b, c = p.arrays()
     ref = two_phase_ref(A, b, c)
     assert got.status == ref["status"] and tuple(got.pivots) == ref["pivots"]

@@ -24,6 +24,7 @@ def main():
         [320, 1600, 2080, 5000, 10000, 20000, 40000, 60000, 80000]
     n, m, seed = bench.CONFIGS[name][:3]
     width = 1 + n + 2 * m
+    sx.set_deactivate(0)  # (what the sweep would move without moving basic slacks out)
     s = sx.Session(generated=(n, m, seed, 1, 100))
     for k in cps:
         t = s.pivots(k - s.total_pivots())
@@ -44,6 +45,7 @@ def main():
         if t.status != sx.NOT_ENDED:
             break
     s.close()
+    sx.set_deactivate(sx.DEACTIVATE_EVERY)
 
 
 if __name__ == "__main__":
