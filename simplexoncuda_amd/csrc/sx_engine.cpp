@@ -298,7 +298,8 @@ struct Shard {
     int *urow = nullptr;              //   unswept slack k -> the row of its unit vector [m]
     int *nact = nullptr;              //   swept slack columns (the swept block's width past 1+n)
     DeactList *dlist = nullptr;       //   basic slacks moved out of the sweep (one shard)
-    int *dcrow = nullptr;             //   its scratch: stored slack offset -> basic row [m]
+    unsigned long long *dtag = nullptr;  // its scratch: stored slack offset -> (round, basic row) [m]
+    unsigned dround = 0;                 //   rounds run
     double *F = nullptr;              // pending row factors [rows][SX_KMAX]
     PivRec *recs = nullptr;           // pending pivot records [SX_KMAX]
     unsigned long long *PM = nullptr; // [rows] pending leaving-row slots (batch-tagged)
@@ -882,7 +883,7 @@ class Engine {
                         (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
                         (void *)x.rhs_all, (void *)x.base, (void *)x.enter_parts, (void *)x.tiles_local, (void *)x.chan,
                         (void *)x.ga, (void *)x.gb, (void *)x.gdone, (void *)x.perm, (void *)x.iperm,
-                        (void *)x.ucol, (void *)x.urow, (void *)x.nact, (void *)x.dlist, (void *)x.dcrow,
+                        (void *)x.ucol, (void *)x.urow, (void *)x.nact, (void *)x.dlist, (void *)x.dtag,
                         (void *)x.tiles_all, (void *)x.st})
             if (p) (void)hipFree(p);
     }
@@ -1145,7 +1146,7 @@ class Engine {
                     x.urow = dalloc<int>(m);
                     x.nact = dalloc<int>(1);
                     x.dlist = dalloc<DeactList>(1);
-                    x.dcrow = dalloc<int>(m);
+                    x.dtag = dalloc<unsigned long long>(m);
                 }
                 SX_HIP(hipMemcpyAsync(x.perm, id.data(), sizeof(int) * m, hipMemcpyHostToDevice, x.s));
                 SX_HIP(hipMemcpyAsync(x.iperm, id.data(), sizeof(int) * m, hipMemcpyHostToDevice, x.s));
@@ -1153,6 +1154,8 @@ class Engine {
                 SX_HIP(hipMemcpyAsync(x.urow, id.data(), sizeof(int) * m, hipMemcpyHostToDevice, x.s));
                 SX_HIP(hipMemsetAsync(x.nact, 0, sizeof(int), x.s));
                 SX_HIP(hipMemsetAsync(x.dlist, 0, sizeof(DeactList), x.s));
+                SX_HIP(hipMemsetAsync(x.dtag, 0, sizeof(unsigned long long) * m, x.s));
+                x.dround = 0;
             }
             sync_all();
         }
@@ -1429,10 +1432,10 @@ class Engine {
             const char *e = getenv("SIMPLEX_DEACTIVATE");
             g_cfg.deact = e ? (atoi(e) > 0 ? atoi(e) : 0) : 8;
         }
-        if (compact && W == 1 && g_cfg.deact > 0 && (sweeps + 1) % g_cfg.deact == 0) {
+        if (compact && W == 1 && g_cfg.deact > 0 && (sweeps + 1) % g_cfg.deact == 0 && m <= 65536) {
             Shard &x = sh[0];
             sx_launch_deactivate(x.perm, x.iperm, x.ucol, x.urow, x.nact, x.base, n, m, cols(N).art0 != 0x7fffffff, x.T,
-                                 x.rows, tl, 1 + n, x.dcrow, x.dlist, x.s);
+                                 x.rows, tl, 1 + n, x.dtag, ++x.dround, x.dlist, x.s);
         }
         ++sweeps;
         q_host = 0;

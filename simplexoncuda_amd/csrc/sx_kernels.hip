@@ -3027,9 +3027,11 @@ __global__ __launch_bounds__(256) void k_activate(int *__restrict__ perm, int *_
 // slack columns whose slack is basic are therefore moved behind the swept block, like the untouched
 // slacks of slack compaction: the sweep stops before them, and the batch whose leaving row is r moves
 // the column back (activate_block / k_activate: ucol[r] is the unswept column that is e_r, urow[k]
-// the row of unswept slack k).  Four launches:
-//   k_deact_list   one block: the rows whose basic variable is a swept slack (the basis), in stored
-//                  position order (at most SX_DEACT_CAP; the rest wait for the next round);
+// the row of unswept slack k).  Five launches per round:
+//   k_deact_mark   one thread per row: a row whose basic variable is a swept slack tags that slack's
+//                  stored position with (round, row);
+//   k_deact_list   one block: the tagged positions in order (at most SX_DEACT_CAP; the rest wait for
+//                  the next round);
 //   k_deact_check  every row compares each listed column with e_r bit for bit (a column that is not
 //                  -- a non-finite entry when it entered -- stays swept);
 //   k_deact_plan   one block: the d checked columns keep their positions if they lie in the last d
@@ -3067,45 +3069,72 @@ __device__ __forceinline__ int block_exscan1024(int v, int *s_w, int *total) {
     return before + x - v;
 }
 
-__global__ __launch_bounds__(1024) void k_deact_list(const int *__restrict__ base, const int *__restrict__ perm,
-                                                     const int *__restrict__ nact_p, int n, int m, bool alias,
-                                                     int *__restrict__ crow, DeactList *L) {
+__global__ __launch_bounds__(256) void k_deact_mark(const int *__restrict__ base, const int *__restrict__ perm,
+                                                    const int *__restrict__ nact_p, int n, int m, bool alias,
+                                                    unsigned long long *__restrict__ tag, unsigned epoch) {
+    const int i = (int)blockIdx.x * 256 + (int)threadIdx.x;
+    if (i >= m) return;
+    const int k = deact_slack(base[i], n, m, alias);
+    if (k < 0) return;
+    const int x = perm[k];
+    if (x < *nact_p) tag[x] = ((unsigned long long)epoch << 32) | (unsigned)i;  // (a swept slack basic in row i)
+}
+
+__global__ __launch_bounds__(1024) void k_deact_list(const int *__restrict__ nact_p,
+                                                     const unsigned long long *__restrict__ tag, unsigned epoch,
+                                                     DeactList *L) {
     __shared__ int s_w[16];
     const int t = threadIdx.x;
     const int na = *nact_p;
-    for (int x = t; x < na; x += 1024) crow[x] = -1;
-    __syncthreads();
-    for (int i = t; i < m; i += 1024) {
-        const int k = deact_slack(base[i], n, m, alias);
-        if (k >= 0) {
-            const int x = perm[k];
-            if (x < na) crow[x] = i;  // (a swept slack basic in row i)
-        }
-    }
-    __syncthreads();
     const int chunk = (na + 1023) / 1024, x0 = t * chunk, x1 = x0 + chunk < na ? x0 + chunk : na;
-    int c = 0;
-    for (int x = x0; x < x1; ++x) c += crow[x] >= 0;
+    // the chunk's tags, 8 loads in flight at a time; a bit per tagged position (chunk <= 64: at most
+    // 65536 slacks, sx_launch_deactivate)
+    unsigned long long bits = 0ull;
+    for (int b = x0; b < x1; b += 8) {
+        unsigned long long v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = b + q < x1 ? tag[b + q] : 0ull;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (b + q < x1 && (unsigned)(v[q] >> 32) == epoch) bits |= 1ull << (b + q - x0);
+    }
     int total;
-    int o = block_exscan1024(c, s_w, &total);
-    for (int x = x0; x < x1 && o < SX_DEACT_CAP; ++x)
-        if (crow[x] >= 0) {
-            L->x[o] = x;
-            L->r[o] = crow[x];
-            L->bad[o] = 0;
-            ++o;
-        }
+    int o = block_exscan1024(__popcll(bits), s_w, &total);
+    while (bits && o < SX_DEACT_CAP) {
+        const int q = __builtin_ctzll(bits);
+        bits &= bits - 1ull;
+        L->x[o] = x0 + q;
+        L->r[o] = (int)(unsigned)tag[x0 + q];
+        L->bad[o] = 0;
+        ++o;
+    }
     if (t == 0) L->C = total < SX_DEACT_CAP ? total : SX_DEACT_CAP;
 }
 
 __global__ __launch_bounds__(256) void k_deact_check(const double *__restrict__ T, int rows, TLay tl, int s0,
                                                      DeactList *L) {
+    __shared__ int s_x[1024 + 8], s_r[1024 + 8];  // (+8: the unrolled tail reads past nj)
     const int C = L->C;
-    const int i = (int)blockIdx.x * 256 + (int)threadIdx.x;
-    if (i >= rows) return;
-    for (int j = 0; j < C; ++j) {
-        const double want = i == L->r[j] ? 1.0 : 0.0;
-        if (__double_as_longlong(T[tl.idx(i, s0 + L->x[j])]) != __double_as_longlong(want)) L->bad[j] = 1;
+    const int t = threadIdx.x, i = (int)blockIdx.x * 256 + t;
+    for (int j0 = 0; j0 < C; j0 += 1024) {  // the list through LDS, 1024 entries at a time
+        const int nj = C - j0 < 1024 ? C - j0 : 1024;
+        __syncthreads();
+        for (int q = t; q < nj; q += 256) {
+            s_x[q] = s0 + L->x[j0 + q];
+            s_r[q] = L->r[j0 + q];
+        }
+        __syncthreads();
+        if (i >= rows) continue;
+        for (int j = 0; j < nj; j += 8) {  // 8 loads in flight
+            double v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = j + q < nj ? T[tl.idx(i, s_x[j + q])] : 0.0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const double want = i == s_r[j + q] ? 1.0 : 0.0;
+                if (j + q < nj && __double_as_longlong(v[q]) != __double_as_longlong(want)) L->bad[j0 + j + q] = 1;
+            }
+        }
     }
 }
 
@@ -3488,10 +3517,13 @@ void sx_launch_activate(int *perm, int *iperm, int *ucol, const int *urow, int *
 }
 
 void sx_launch_deactivate(int *perm, int *iperm, int *ucol, int *urow, int *nact, const int *base, int n, int m,
-                          bool alias, double *T, int rows, TLay tl, int s0, int *crow, DeactList *L, hipStream_t s) {
+                          bool alias, double *T, int rows, TLay tl, int s0, unsigned long long *tag, unsigned epoch,
+                          DeactList *L, hipStream_t s) {
     if (rows <= 0 || m <= 0) return;
+    if (m > 65536) SX_FATAL("basic-slack deactivation: at most 65536 slacks");
     const int g = (rows + 255) / 256;
-    k_deact_list<<<1, 1024, 0, s>>>(base, perm, nact, n, m, alias, crow, L);
+    k_deact_mark<<<(m + 255) / 256, 256, 0, s>>>(base, perm, nact, n, m, alias, tag, epoch);
+    k_deact_list<<<1, 1024, 0, s>>>(nact, tag, epoch, L);
     k_deact_check<<<g, 256, 0, s>>>(T, rows, tl, s0, L);
     k_deact_plan<<<1, 1024, 0, s>>>(perm, iperm, ucol, urow, nact, L);
     k_deact_move<<<g, 256, 0, s>>>(T, rows, tl, s0, L);
