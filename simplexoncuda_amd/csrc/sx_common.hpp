@@ -216,10 +216,12 @@ struct DeactList {
     int x[SX_DEACT_CAP], r[SX_DEACT_CAP], bad[SX_DEACT_CAP];  // position, unit row, failed the check
     int dst[SX_DEACT_CAP], src[SX_DEACT_CAP], row[SX_DEACT_CAP];
 };
-// (tag: [m] position tags, zero at allocation; epoch: this round's number, from 1)
+// (tag: [m] position tags, zero at allocation; epoch: this round's number, from 1; check: compare each
+// column with its unit vector first -- required: an entered column is e_r only where its entries'
+// residuals a_k - fl(a_k / p) p round to 0)
 void sx_launch_deactivate(int *perm, int *iperm, int *ucol, int *urow, int *nact, const int *base, int n, int m,
-                          bool alias, double *T, int rows, TLay tl, int s0, unsigned long long *tag, unsigned epoch,
-                          DeactList *L, hipStream_t s);
+                          bool alias, double *T, int rows, int row0, TLay tl, int s0, unsigned long long *tag,
+                          unsigned epoch, bool check, DeactList *L, hipStream_t s);
 // fused batch of up to k pivots on one shard (ratio tiles + objective tiles in one resident
 // grid); returns false (nothing launched) when the grid cannot be resident at once
 bool sx_batch_fits(int rows, Cols c, int k);

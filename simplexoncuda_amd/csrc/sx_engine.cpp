@@ -1427,7 +1427,10 @@ class Engine {
         }
         if (rec_shard0) sx_set_sweep_record(nullptr);
         if (ev1) SX_HIP(hipEventRecord(ev1, s));
-        // one shard, every g_cfg.deact sweeps: the swept slacks that are basic leave the swept block
+        // one shard, every g_cfg.deact sweeps: the swept slacks whose columns are exactly their unit
+        // vectors leave the swept block.  (Not on several shards: each sees only its rows of a column,
+        // and the shards would have to agree on every check -- a column that entered keeps the
+        // residuals a_k - fl(a_k / p) p where they are not 0)
         if (g_cfg.deact < 0) {
             const char *e = getenv("SIMPLEX_DEACTIVATE");
             g_cfg.deact = e ? (atoi(e) > 0 ? atoi(e) : 0) : 8;
@@ -1435,7 +1438,7 @@ class Engine {
         if (compact && W == 1 && g_cfg.deact > 0 && (sweeps + 1) % g_cfg.deact == 0 && m <= 65536) {
             Shard &x = sh[0];
             sx_launch_deactivate(x.perm, x.iperm, x.ucol, x.urow, x.nact, x.base, n, m, cols(N).art0 != 0x7fffffff, x.T,
-                                 x.rows, tl, 1 + n, x.dtag, ++x.dround, x.dlist, x.s);
+                                 x.rows, x.row0, tl, 1 + n, x.dtag, ++x.dround, true, x.dlist, x.s);
         }
         ++sweeps;
         q_host = 0;

@@ -3019,12 +3019,14 @@ __global__ __launch_bounds__(256) void k_activate(int *__restrict__ perm, int *_
     if (t == 0) *nact_p = na0 + s_added;
 }
 
-// Basic slack columns out of the sweep (one shard; after a sweep, every few batches).  A variable
-// that enters at row r leaves its column exactly the unit vector e_r: the pivot row becomes p / p = 1
-// and every other row fma(-p / p, x, x) = x - x = +0 (solver.cu:34-46, finite x); every later pivot
-// row holds +0 there while the variable stays basic, so the reference's updates leave the column
-// bit-identical (fma(f, +0, +0) = +0, fma(f, +0, 1) = 1, finite f) until row r leaves.  The swept
-// slack columns whose slack is basic are therefore moved behind the swept block, like the untouched
+// Basic slack columns out of the sweep (one shard; after a sweep, every few batches).  When a variable
+// enters at row r the reference (solver.cu:34-46) makes its pivot-row entry p / p = 1 and every other
+// entry fma(-(a_k / p), p, a_k) = a_k - fl(a_k / p) p, rounded once: +0 wherever fl(a_k / p) p == a_k,
+// a residual of an ulp or so elsewhere.  A column whose residuals all vanished is exactly the unit
+// vector e_r, every later pivot row holds +0 there while the variable stays basic, and the updates
+// leave it bit-identical (fma(f, +0, +0) = +0, fma(f, +0, 1) = 1, finite f) until row r leaves.  The
+// swept slack columns whose slack is basic and whose column checks out as e_r, bit for bit, are
+// therefore moved behind the swept block, like the untouched
 // slacks of slack compaction: the sweep stops before them, and the batch whose leaving row is r moves
 // the column back (activate_block / k_activate: ucol[r] is the unswept column that is e_r, urow[k]
 // the row of unswept slack k).  Five launches per round:
@@ -3111,8 +3113,8 @@ __global__ __launch_bounds__(1024) void k_deact_list(const int *__restrict__ nac
     if (t == 0) L->C = total < SX_DEACT_CAP ? total : SX_DEACT_CAP;
 }
 
-__global__ __launch_bounds__(256) void k_deact_check(const double *__restrict__ T, int rows, TLay tl, int s0,
-                                                     DeactList *L) {
+__global__ __launch_bounds__(256) void k_deact_check(const double *__restrict__ T, int rows, int row0, TLay tl,
+                                                     int s0, DeactList *L) {
     __shared__ int s_x[1024 + 8], s_r[1024 + 8];  // (+8: the unrolled tail reads past nj)
     const int C = L->C;
     const int t = threadIdx.x, i = (int)blockIdx.x * 256 + t;
@@ -3131,7 +3133,7 @@ __global__ __launch_bounds__(256) void k_deact_check(const double *__restrict__ 
             for (int q = 0; q < 8; ++q) v[q] = j + q < nj ? T[tl.idx(i, s_x[j + q])] : 0.0;
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
-                const double want = i == s_r[j + q] ? 1.0 : 0.0;
+                const double want = i + row0 == s_r[j + q] ? 1.0 : 0.0;
                 if (j + q < nj && __double_as_longlong(v[q]) != __double_as_longlong(want)) L->bad[j0 + j + q] = 1;
             }
         }
@@ -3226,7 +3228,7 @@ __global__ __launch_bounds__(1024) void k_deact_plan(int *__restrict__ perm, int
     }
 }
 
-__global__ __launch_bounds__(256) void k_deact_move(double *__restrict__ T, int rows, TLay tl, int s0,
+__global__ __launch_bounds__(256) void k_deact_move(double *__restrict__ T, int rows, int row0, TLay tl, int s0,
                                                     const DeactList *__restrict__ L) {
     const int nsw = L->nsw;
     const int i = (int)blockIdx.x * 256 + (int)threadIdx.x;
@@ -3234,7 +3236,7 @@ __global__ __launch_bounds__(256) void k_deact_move(double *__restrict__ T, int 
     for (int j = 0; j < nsw; ++j) {
         const int P = s0 + L->dst[j], Q = s0 + L->src[j];
         T[tl.idx(i, P)] = T[tl.idx(i, Q)];
-        T[tl.idx(i, Q)] = i == L->row[j] ? 1.0 : 0.0;
+        T[tl.idx(i, Q)] = i + row0 == L->row[j] ? 1.0 : 0.0;
     }
 }
 
@@ -3517,16 +3519,16 @@ void sx_launch_activate(int *perm, int *iperm, int *ucol, const int *urow, int *
 }
 
 void sx_launch_deactivate(int *perm, int *iperm, int *ucol, int *urow, int *nact, const int *base, int n, int m,
-                          bool alias, double *T, int rows, TLay tl, int s0, unsigned long long *tag, unsigned epoch,
-                          DeactList *L, hipStream_t s) {
-    if (rows <= 0 || m <= 0) return;
+                          bool alias, double *T, int rows, int row0, TLay tl, int s0, unsigned long long *tag,
+                          unsigned epoch, bool check, DeactList *L, hipStream_t s) {
+    if (m <= 0) return;
     if (m > 65536) SX_FATAL("basic-slack deactivation: at most 65536 slacks");
-    const int g = (rows + 255) / 256;
+    const int g = rows > 0 ? (rows + 255) / 256 : 1;
     k_deact_mark<<<(m + 255) / 256, 256, 0, s>>>(base, perm, nact, n, m, alias, tag, epoch);
     k_deact_list<<<1, 1024, 0, s>>>(nact, tag, epoch, L);
-    k_deact_check<<<g, 256, 0, s>>>(T, rows, tl, s0, L);
+    if (check && rows > 0) k_deact_check<<<g, 256, 0, s>>>(T, rows, row0, tl, s0, L);
     k_deact_plan<<<1, 1024, 0, s>>>(perm, iperm, ucol, urow, nact, L);
-    k_deact_move<<<g, 256, 0, s>>>(T, rows, tl, s0, L);
+    if (rows > 0) k_deact_move<<<g, 256, 0, s>>>(T, rows, row0, tl, s0, L);
 }
 
 void sx_launch_sweep(double *T, int rows, int row0, size_t ld, TLay tl, int Ns, const int *nact, int s0,

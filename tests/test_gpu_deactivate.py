@@ -1,10 +1,11 @@
 """Basic slack columns moved out of the sweep (k_deact_* in sx_kernels.hip).
 
-A slack that enters the basis leaves its column exactly a unit vector (the reference's pivot,
-solver.cu:34-46, makes it p / p = 1 and x - x = +0) which later pivots leave bit-identical until its
-row leaves again; with slack compaction on one shard such columns are moved behind the swept block
-after each sweep and moved back when their row leaves.  Every logical entry of the tableau must
-stay the oracle's, through re-entries and re-activations, on the fused and the per-pivot paths,
+A slack that enters the basis leaves its column the unit vector e_r where the residuals
+a_k - fl(a_k / p) p of the reference's pivot (solver.cu:34-46) round to +0 (checked bit for bit), and
+later pivots leave it bit-identical until its row leaves again; with slack compaction such columns
+are moved behind the swept block every few
+sweeps and moved back when their row leaves.  Every logical entry of the tableau must stay the
+oracle's, through re-entries and re-activations, on the fused and the per-pivot paths (one shard),
 and the whole two-phase method must return the oracle's answer (needs an MI355X).
 """
 import numpy as np
@@ -95,3 +96,4 @@ def test_deactivated_slacks_two_phase(gpu, n, m, seed, deact):
     assert np.array_equal(got.base, ref["base"])
     if got.status == sx.FEASIBLE:
         assert same(got.optimal_value, ref["opt"]) and same(got.solution, ref["x"])
+

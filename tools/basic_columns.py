@@ -1,8 +1,8 @@
 """How much of each sweep moves basic columns (diagnostic).
 
-A column basic in row i is the exact unit vector e_i (+0 everywhere else: it entered through
-fma(-p/p, x, x) = +0 and x/p = 1, solver.cu:34-46) and every later pivot row holds +0 in it until
-row i leaves, so the sweep rewrites it unchanged while its factors are finite.  This counts, at
+A column basic in row i is the unit vector e_i wherever the residuals a_k - fl(a_k / p) p of its
+entry (solver.cu:34-46) rounded to +0, and every later pivot row holds +0 in it until row i leaves,
+so the sweep rewrites such a column unchanged while its factors are finite.  This counts, at
 phase-1 checkpoints of a generated instance, the stored columns a sweep moves (1 + n + touched
 slacks) and how many of them are basic (0-based variable indices in base, as the oracle's).
 usage: python tools/basic_columns.py [config] [checkpoint,...]
