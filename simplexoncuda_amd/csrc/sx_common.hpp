@@ -218,10 +218,11 @@ struct DeactList {
 };
 // (tag: [m] position tags, zero at allocation; epoch: this round's number, from 1; check: compare each
 // column with its unit vector first -- required: an entered column is e_r only where its entries'
-// residuals a_k - fl(a_k / p) p round to 0)
+// residuals a_k - fl(a_k / p) p round to 0; fail: [m] slack -> 1 + the row it failed the check in, zero
+// at allocation)
 void sx_launch_deactivate(int *perm, int *iperm, int *ucol, int *urow, int *nact, const int *base, int n, int m,
                           bool alias, double *T, int rows, int row0, TLay tl, int s0, unsigned long long *tag,
-                          unsigned epoch, bool check, DeactList *L, hipStream_t s);
+                          unsigned epoch, bool check, int *fail, DeactList *L, hipStream_t s);
 // fused batch of up to k pivots on one shard (ratio tiles + objective tiles in one resident
 // grid); returns false (nothing launched) when the grid cannot be resident at once
 bool sx_batch_fits(int rows, Cols c, int k);

@@ -300,6 +300,7 @@ struct Shard {
     DeactList *dlist = nullptr;       //   basic slacks moved out of the sweep (one shard)
     unsigned long long *dtag = nullptr;  // its scratch: stored slack offset -> (round, basic row) [m]
     unsigned dround = 0;                 //   rounds run
+    int *dfail = nullptr;                //   slack -> 1 + the row whose check it failed [m]
     double *F = nullptr;              // pending row factors [rows][SX_KMAX]
     PivRec *recs = nullptr;           // pending pivot records [SX_KMAX]
     unsigned long long *PM = nullptr; // [rows] pending leaving-row slots (batch-tagged)
@@ -883,7 +884,7 @@ class Engine {
                         (void *)x.coef, (void *)x.gemv_local, (void *)x.gemv_all, (void *)x.rhs_local,
                         (void *)x.rhs_all, (void *)x.base, (void *)x.enter_parts, (void *)x.tiles_local, (void *)x.chan,
                         (void *)x.ga, (void *)x.gb, (void *)x.gdone, (void *)x.perm, (void *)x.iperm,
-                        (void *)x.ucol, (void *)x.urow, (void *)x.nact, (void *)x.dlist, (void *)x.dtag,
+                        (void *)x.ucol, (void *)x.urow, (void *)x.nact, (void *)x.dlist, (void *)x.dtag, (void *)x.dfail,
                         (void *)x.tiles_all, (void *)x.st})
             if (p) (void)hipFree(p);
     }
@@ -1147,6 +1148,7 @@ class Engine {
                     x.nact = dalloc<int>(1);
                     x.dlist = dalloc<DeactList>(1);
                     x.dtag = dalloc<unsigned long long>(m);
+                    x.dfail = dalloc<int>(m);
                 }
                 SX_HIP(hipMemcpyAsync(x.perm, id.data(), sizeof(int) * m, hipMemcpyHostToDevice, x.s));
                 SX_HIP(hipMemcpyAsync(x.iperm, id.data(), sizeof(int) * m, hipMemcpyHostToDevice, x.s));
@@ -1155,6 +1157,7 @@ class Engine {
                 SX_HIP(hipMemsetAsync(x.nact, 0, sizeof(int), x.s));
                 SX_HIP(hipMemsetAsync(x.dlist, 0, sizeof(DeactList), x.s));
                 SX_HIP(hipMemsetAsync(x.dtag, 0, sizeof(unsigned long long) * m, x.s));
+                SX_HIP(hipMemsetAsync(x.dfail, 0, sizeof(int) * m, x.s));
                 x.dround = 0;
             }
             sync_all();
@@ -1438,7 +1441,7 @@ class Engine {
         if (compact && W == 1 && g_cfg.deact > 0 && (sweeps + 1) % g_cfg.deact == 0 && m <= 65536) {
             Shard &x = sh[0];
             sx_launch_deactivate(x.perm, x.iperm, x.ucol, x.urow, x.nact, x.base, n, m, cols(N).art0 != 0x7fffffff, x.T,
-                                 x.rows, x.row0, tl, 1 + n, x.dtag, ++x.dround, true, x.dlist, x.s);
+                                 x.rows, x.row0, tl, 1 + n, x.dtag, ++x.dround, true, x.dfail, x.dlist, x.s);
         }
         ++sweeps;
         q_host = 0;

@@ -3073,11 +3073,12 @@ __device__ __forceinline__ int block_exscan1024(int v, int *s_w, int *total) {
 
 __global__ __launch_bounds__(256) void k_deact_mark(const int *__restrict__ base, const int *__restrict__ perm,
                                                     const int *__restrict__ nact_p, int n, int m, bool alias,
-                                                    unsigned long long *__restrict__ tag, unsigned epoch) {
+                                                    const int *__restrict__ fail, unsigned long long *__restrict__ tag,
+                                                    unsigned epoch) {
     const int i = (int)blockIdx.x * 256 + (int)threadIdx.x;
     if (i >= m) return;
     const int k = deact_slack(base[i], n, m, alias);
-    if (k < 0) return;
+    if (k < 0 || fail[k] == i + 1) return;  // (failed the check while basic in this row: keeps its residual)
     const int x = perm[k];
     if (x < *nact_p) tag[x] = ((unsigned long long)epoch << 32) | (unsigned)i;  // (a swept slack basic in row i)
 }
@@ -3142,7 +3143,7 @@ __global__ __launch_bounds__(256) void k_deact_check(const double *__restrict__ 
 
 __global__ __launch_bounds__(1024) void k_deact_plan(int *__restrict__ perm, int *__restrict__ iperm,
                                                      int *__restrict__ ucol, int *__restrict__ urow,
-                                                     int *__restrict__ nact_p, DeactList *L) {
+                                                     int *__restrict__ nact_p, int *__restrict__ fail, DeactList *L) {
     __shared__ int s_w[16];
     __shared__ int s_free[SX_DEACT_CAP];           // tail positions that receive a candidate
     __shared__ unsigned s_tail[SX_DEACT_CAP / 32];  // tail positions held by a candidate (bits)
@@ -3156,6 +3157,7 @@ __global__ __launch_bounds__(1024) void k_deact_plan(int *__restrict__ perm, int
         const int j = PER * t + q;
         ok[q] = j < C && L->bad[j] == 0;
         nok += ok[q];
+        if (j < C && !ok[q]) fail[iperm[L->x[j]]] = L->r[j] + 1;  // (not listed again while basic there)
     }
     int d;
     const int before = block_exscan1024(nok, s_w, &d);
@@ -3520,14 +3522,14 @@ void sx_launch_activate(int *perm, int *iperm, int *ucol, const int *urow, int *
 
 void sx_launch_deactivate(int *perm, int *iperm, int *ucol, int *urow, int *nact, const int *base, int n, int m,
                           bool alias, double *T, int rows, int row0, TLay tl, int s0, unsigned long long *tag,
-                          unsigned epoch, bool check, DeactList *L, hipStream_t s) {
+                          unsigned epoch, bool check, int *fail, DeactList *L, hipStream_t s) {
     if (m <= 0) return;
     if (m > 65536) SX_FATAL("basic-slack deactivation: at most 65536 slacks");
     const int g = rows > 0 ? (rows + 255) / 256 : 1;
-    k_deact_mark<<<(m + 255) / 256, 256, 0, s>>>(base, perm, nact, n, m, alias, tag, epoch);
+    k_deact_mark<<<(m + 255) / 256, 256, 0, s>>>(base, perm, nact, n, m, alias, fail, tag, epoch);
     k_deact_list<<<1, 1024, 0, s>>>(nact, tag, epoch, L);
     if (check && rows > 0) k_deact_check<<<g, 256, 0, s>>>(T, rows, row0, tl, s0, L);
-    k_deact_plan<<<1, 1024, 0, s>>>(perm, iperm, ucol, urow, nact, L);
+    k_deact_plan<<<1, 1024, 0, s>>>(perm, iperm, ucol, urow, nact, fail, L);
     if (rows > 0) k_deact_move<<<g, 256, 0, s>>>(T, rows, row0, tl, s0, L);
 }
 
