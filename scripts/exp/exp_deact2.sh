@@ -1,7 +1,7 @@
 #!/bin/bash
 # Basic-slack deactivation, part 2: the rest of the GPU suite, then same-box bench lines with it on
 # and off (SIMPLEX_DEACTIVATE), window + whole solves.  (experiment helper)
-source "$(dirname "$0")/gpu_step.sh"
+source "$(dirname "$0")/../gpu_step.sh"
 step suite2 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_published.py tests/test_gpu_tabular.py tests/test_gpu_deactivate.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu || exit $?
 tail -1 $O/suite2.log
 for v in 1 0 1 0; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Basic-slack deactivation every few sweeps: its tests, the compaction / two-phase / long-pin tests,
 # then same-box bench lines with SIMPLEX_DEACTIVATE=8 and 0 alternating.  (experiment helper)
-source "$(dirname "$0")/gpu_step.sh"
+source "$(dirname "$0")/../gpu_step.sh"
 step deact 400 python -u -m pytest tests/test_gpu_deactivate.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu || exit $?
 tail -1 $O/deact.log
 step subset 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_large.py tests/test_gpu_published.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu -k "compaction or two_phase or region or long_pins or whole_solve or published or config2 or session or pivots" || exit $?

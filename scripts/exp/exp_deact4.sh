@@ -2,7 +2,7 @@
 # Basic-slack deactivation with the parallel mark kernel: its tests, the compaction / two-phase /
 # long-pin subset, a kernel trace of the bench (the k_deact_* durations), then same-box bench lines
 # with SIMPLEX_DEACTIVATE=8 / 0 alternating.  (experiment helper)
-source "$(dirname "$0")/gpu_step.sh"
+source "$(dirname "$0")/../gpu_step.sh"
 export TMPDIR=/tmp
 step deact 400 python -u -m pytest tests/test_gpu_deactivate.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu || exit $?
 tail -1 $O/deact.log

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Basic-slack deactivation, final form: the whole GPU suite, a kernel trace of the bench (k_deact_*
 # durations), then same-box bench lines with SIMPLEX_DEACTIVATE=8 / 0 alternating.  (experiment helper)
-source "$(dirname "$0")/gpu_step.sh"
+source "$(dirname "$0")/../gpu_step.sh"
 export TMPDIR=/tmp
 step suite 1000 python -u -m pytest tests -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu || exit $?
 tail -1 $O/suite.log

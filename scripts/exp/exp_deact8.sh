@@ -1,7 +1,7 @@
 #!/bin/bash
 # Deactivation with failed columns remembered: its tests, the long-pin / whole-solve subset, a kernel
 # trace of the bench and two bench lines.  (experiment helper)
-source "$(dirname "$0")/gpu_step.sh"
+source "$(dirname "$0")/../gpu_step.sh"
 export TMPDIR=/tmp
 step deact 400 python -u -m pytest tests/test_gpu_deactivate.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu || exit $?
 tail -1 $O/deact.log

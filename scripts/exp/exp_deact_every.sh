@@ -1,7 +1,7 @@
 #!/bin/bash
 # Deactivation cadence: bench lines (window, config 3, whole solves) with SIMPLEX_DEACTIVATE=4 / 8 / 16 / 32.
 # (experiment helper)
-source "$(dirname "$0")/gpu_step.sh"
+source "$(dirname "$0")/../gpu_step.sh"
 for v in 4 8 16 32 8 4; do
   export SIMPLEX_DEACTIVATE=$v; step bench_$v 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline || exit $?
   python3 - $O/bench_$v.log $v <<'PY'

@@ -2,7 +2,7 @@
 # Same-box A/B of the multi-rank (virtual peer-memory ranks) chain: the current library against
 # ablib/libsimplex_prev.so, tools/p2p_probe.py per config, split and replicated objective.
 # (experiment helper)
-source "$(dirname "$0")/gpu_step.sh"
+source "$(dirname "$0")/../gpu_step.sh"
 PREV=$(pwd)/ablib/libsimplex_prev.so
 if [ -n "${PK:-}" ]; then
   step parity 700 python -u -m pytest ${FILES:-tests} -x -q -p no:cacheprovider --timeout 250 --timeout-method thread -m gpu -k "$PK" || exit $?

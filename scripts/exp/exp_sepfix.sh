@@ -1,7 +1,7 @@
 #!/bin/bash
 # The sweep's leaving rows as a launch of their own (SIMPLEX_SEP_FIXUP=1) vs in the sweep's tail (0):
 # parity subset with it on, then same-box bench lines alternating.  (experiment helper)
-source "$(dirname "$0")/gpu_step.sh"
+source "$(dirname "$0")/../gpu_step.sh"
 export SIMPLEX_SEP_FIXUP=1
 step parity 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_large.py tests/test_gpu_deactivate.py -x -q -p no:cacheprovider --timeout 250 --timeout-method thread -m gpu -k "sweep or batch or leaves or fused or compaction or two_phase or long_pins or deactivated or virtual" || exit $?
 tail -1 $O/parity.log

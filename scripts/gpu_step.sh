@@ -2,7 +2,7 @@
 # GPU-call helpers: each step under its own time limit, its log under gpurun_out/$TAG; a failure
 # ends the calling script (source this file, then `step NAME SECONDS CMD...`).
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(git -C "$(dirname "$0")" rev-parse --show-toplevel 2>/dev/null || echo "$(dirname "$0")/..")}"
 export TMPDIR=/tmp
 TAG=${TAG:-run}
 O=gpurun_out/$TAG
